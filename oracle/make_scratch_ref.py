@@ -1,0 +1,99 @@
+"""Build a scratch Python-3 translation of the reference pyfasst in /tmp.
+
+TEST INFRASTRUCTURE ONLY.  Nothing here is shipped or imported by the
+product package `pyfasst_amd`.  The scratch copy lives under /tmp, is never
+committed, and never travels to the GPU box; it is used in this container
+only to (i) pin the committed NumPy restatement `oracle/fasst_ref.py` and
+(ii) generate the small golden fixtures under `tests/golden/`.
+
+Recipe:
+  1. copy /root/reference/pyfasst -> /tmp/pyfasst_scratch/pyfasst
+  2. python -m lib2to3 -w -n
+  3. fix the 2to3 artifacts and the Python-3 / NumPy-2 incompatibilities
+     listed in PATCHES below (mechanical textual substitutions only).
+The Cython Viterbi tracker is not needed by the EM / SIMM paths and is not
+built.
+
+Usage:  python oracle/make_scratch_ref.py  [dest_dir]
+then    sys.path.insert(0, dest_dir); import pyfasst.audioModel
+"""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+REF = "/root/reference/pyfasst"
+DEFAULT_DEST = "/tmp/pyfasst_scratch"
+
+# (file, regex, replacement).  Each is a mechanical py2->py3 / numpy-2 fix.
+PATCHES = [
+    # `from . import a.b as c` (2to3 artifact) -> `from .a import b as c`
+    ("audioModel.py", r"from \. import (\w+)\.(\w+) as (\w+)", r"from .\1 import \2 as \3"),
+    ("demixTF.py", r"from \. import (\w+)\.(\w+) as (\w+)", r"from .\1 import \2 as \3"),
+    ("tftransforms/nsgt/unslicing.py", r"importcycle", "import cycle"),
+    ("tftransforms/nsgt/nsigtf.py", r"importchain", "import chain"),
+    ("tftransforms/nsgt/slicq.py", r"importcycle", "import cycle"),
+    ("SeparateLeadStereo/SIMM/SIMM.py", r"from string import join\n", "\n"),
+    ("SeparateLeadStereo/SIMM/SIMMopt.py", r"from string import join\n", "\n"),
+    # integer divisions used as sizes/indices
+    ("audioModel.py", r"self\.sig_repr_params\['fsize'\]/2\+1", "self.sig_repr_params['fsize']//2+1"),
+    ("audioModel.py", r"nc \* \(nc \+ 1\) / 2", "nc * (nc + 1) // 2"),
+    ("audioModel.py", r"'hopsize': self\.sig_repr_params\['wlen'\]/2", "'hopsize': self.sig_repr_params['wlen']//2"),
+    # numpy 2 removed aliases
+    ("audioModel.py", r"np\.complex\b", "complex"),
+    ("tools/signalTools.py", r"np\.complex\b", "complex"),
+    ("demixTF.py", r"np\.complex\b", "complex"),
+    # stft.py float sizes/indices
+    ("tftransforms/stft.py", r"np\.zeros\(lengthWindow/2\.0\)", "np.zeros(int(lengthWindow//2))"),
+    ("tftransforms/stft.py", r"np\.zeros\(\[lengthWindow/2\.0, nc\]\)", "np.zeros([int(lengthWindow//2), nc])"),
+    ("tftransforms/stft.py", r"np\.zeros\(newLengthData - data\.size\)", "np.zeros(int(newLengthData - data.size))"),
+    ("tftransforms/stft.py", r"numberFrequencies = nfft / 2 \+ 1", "numberFrequencies = int(nfft // 2 + 1)"),
+    ("tftransforms/stft.py", r"np\.zeros\(\[numberFrequencies, numberFrames\], dtype=complex\)",
+     "np.zeros([numberFrequencies, int(numberFrames)], dtype=complex)"),
+    ("tftransforms/stft.py", r"for n in np\.arange\(numberFrames\):", "for n in np.arange(int(numberFrames)):"),
+    ("tftransforms/stft.py", r"beginFrame = n\*hopsize", "beginFrame = int(n*hopsize)"),
+    ("tftransforms/stft.py", r"beginFrame = n \* hopsize", "beginFrame = int(n * hopsize)"),
+    ("tftransforms/stft.py", r"endFrame = beginFrame\+lengthWindow", "endFrame = int(beginFrame+lengthWindow)"),
+    ("tftransforms/stft.py", r"endFrame = beginFrame \+ lengthWindow", "endFrame = int(beginFrame + lengthWindow)"),
+    ("tftransforms/stft.py", r"lengthData = hopsize\*\(numberFrames-1\) \+ lengthWindow",
+     "lengthData = int(hopsize*(numberFrames-1) + lengthWindow)"),
+    ("tftransforms/stft.py", r"\[\(lengthWindow/2\.0\):\]", "[int(lengthWindow//2):]"),
+    ("tftransforms/stft.py", r"self\.freqbins = self\.ftlen / 2 \+ 1", "self.freqbins = self.ftlen // 2 + 1"),
+    # the Cython tracker is not built: use the reference's own pure-Python
+    # fallback (tracking/tracking.py), only needed at import time here
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py",
+     r"from \.tracking\._tracking import viterbiTracking as viterbiTrackingArray",
+     "from .tracking.tracking import viterbiTrackingArray"),
+]
+
+
+def build(dest=DEFAULT_DEST):
+    if not os.path.isdir(REF):
+        raise RuntimeError("reference not present at %s" % REF)
+    pkg = os.path.join(dest, "pyfasst")
+    if os.path.isdir(dest):
+        shutil.rmtree(dest)
+    os.makedirs(dest)
+    shutil.copytree(REF, pkg)
+    for root, _, files in os.walk(pkg):
+        os.chmod(root, 0o755)
+        for f in files:
+            os.chmod(os.path.join(root, f), 0o644)
+    subprocess.check_call([sys.executable, "-m", "lib2to3", "-w", "-n", pkg],
+                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    for rel, pat, rep in PATCHES:
+        path = os.path.join(pkg, rel)
+        with open(path) as fh:
+            src = fh.read()
+        new, n = re.subn(pat, rep, src)
+        if n == 0:
+            print("warning: patch had no effect: %s %s" % (rel, pat))
+        with open(path, "w") as fh:
+            fh.write(new)
+    return dest
+
+
+if __name__ == "__main__":
+    d = build(sys.argv[1] if len(sys.argv) > 1 else DEFAULT_DEST)
+    print(d)

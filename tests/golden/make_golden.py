@@ -1,0 +1,177 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE.
+
+Run in the build container only (needs /root/reference):
+
+    python tests/golden/make_golden.py            # all cases
+    python tests/golden/make_golden.py em_inst    # one case
+
+Each case runs in a fresh interpreter (reference quirk N2: the default
+`ann_PSD_lim=[None, None]` list is shared by every model of a process,
+audioModel.py:166,242,320-323).  The reference is imported from a scratch
+py2->py3 translation built by oracle/make_scratch_ref.py under /tmp; only the
+numeric inputs/outputs are committed (as .npz), never reference source.
+
+Inputs are synthetic and seeded (no data derived from data/tamy.wav, which is
+CC BY-NC).  Separated images are captured at the reference's own
+`tft.invertTransform` call inside `separate_comps` (audioModel.py:1203), i.e.
+the STFT-domain images sum_c2 WG[c1,c2] X[c2] the reference inverts.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+SCRATCH = "/tmp/pyfasst_scratch"
+
+CASES = {
+    # name: (model class, kwargs, nbComps, nbNMFComps, spatial_rank, conv, wav seconds, fs)
+    "em_inst": dict(cls="MultiChanNMFInst_FASST", nbComps=2, nbNMFComps=4, spatial_rank=1,
+                    conv=False, n=6000, fs=8000, kw=dict(iter_num=6, wlen=256, hopsize=128)),
+    "em_inst_noann": dict(cls="MultiChanNMFInst_FASST", nbComps=3, nbNMFComps=5, spatial_rank=2,
+                          conv=False, n=5000, fs=8000,
+                          kw=dict(iter_num=4, wlen=128, hopsize=64, sim_ann_opt='no_ann',
+                                  nmfUpdateCoeff=0.7)),
+    "em_conv": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=8, spatial_rank=2,
+                    conv=True, n=6000, fs=8000, kw=dict(iter_num=5, wlen=256, hopsize=64)),
+    "em_conv_j4": dict(cls="MultiChanNMFConv", nbComps=4, nbNMFComps=16, spatial_rank=2,
+                       conv=True, n=6000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64)),
+    "em_conv_j1": dict(cls="MultiChanNMFConv", nbComps=1, nbNMFComps=3, spatial_rank=[2],
+                       conv=True, n=3000, fs=8000, kw=dict(iter_num=3, wlen=128, hopsize=32)),
+}
+
+
+def synth_wav(n, fs, seed):
+    """Seeded stereo int16 test signal: two panned, filtered noise bursts."""
+    import numpy as np
+    rs = np.random.RandomState(seed)
+    t = np.arange(n) / float(fs)
+    s1 = rs.randn(n) * (0.5 + 0.5 * np.sin(2 * np.pi * 1.3 * t)) + np.sin(2 * np.pi * 440 * t)
+    s2 = np.convolve(rs.randn(n), np.ones(5) / 5., mode='same') * (t > 0.1)
+    x = np.stack([0.8 * s1 + 0.3 * s2, 0.4 * s1 + 0.9 * np.roll(s2, 3)], axis=1)
+    x = x / np.abs(x).max() * 20000
+    return x.astype(np.int16)
+
+
+def run_case(name):
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    import scipy.io.wavfile as wf
+    import pyfasst.audioModel as am
+    cfg = CASES[name]
+    seed = sum(map(ord, name)) % 1000
+    data = synth_wav(cfg['n'], cfg['fs'], seed)
+    wav = "/tmp/golden_%s.wav" % name
+    wf.write(wav, cfg['fs'], data)
+    np.random.seed(0)
+    cls = getattr(am, cfg['cls'])
+    m = cls(wav, nbComps=cfg['nbComps'], nbNMFComps=cfg['nbNMFComps'],
+            spatial_rank=cfg['spatial_rank'], verbose=0, **cfg['kw'])
+    if cfg['conv']:
+        m.makeItConvolutive()
+    out = {'wav': data, 'fs': np.array(cfg['fs']), 'Cx': m.Cx,
+           'psd_lim0': np.asarray(m.noise['ann_PSD_lim'][0]),
+           'psd_lim1': np.asarray(m.noise['ann_PSD_lim'][1])}
+
+    def dump(prefix):
+        for j, sc in m.spat_comps.items():
+            out['%sparams_%d' % (prefix, j)] = np.array(sc['params'])
+        for k, comp in m.spec_comps.items():
+            f = comp['factor'][0]
+            out['%sFB_%d' % (prefix, k)] = np.array(f['FB'])
+            out['%sFW_%d' % (prefix, k)] = np.array(f['FW'])
+            out['%sTW_%d' % (prefix, k)] = np.array(f['TW'])
+    dump('init_')
+    # one E-step on the initial state (pins compute_suff_stat itself)
+    if m.noise['sim_ann_opt'] == 'ann':
+        m.noise['PSD'] = ((np.sqrt(m.noise['ann_PSD_lim'][0]) * m.iter_num) / m.iter_num) ** 2
+    else:
+        m.noise['PSD'] = m.noise['ann_PSD_lim'][1]
+    V, mix, parts = m.retrieve_subsrc_params()
+    _, hRxs, hRss, hWs, ll = m.compute_suff_stat(V, mix)
+    out.update(e_psd=np.asarray(m.noise['PSD']), e_hat_Rxs=hRxs, e_hat_Rss=hRss,
+               e_hat_Ws=hWs, e_loglik=np.array(ll))
+    logliks = m.estim_param_a_post_model()
+    out['logliks'] = np.real(logliks)
+    out['final_psd'] = np.asarray(m.noise['PSD'])
+    dump('final_')
+    # separation: capture STFT-domain images at invertTransform
+    images = []
+    orig = m.tft.invertTransform
+
+    def capture():
+        images.append(np.array(m.tft.transfo))
+        return orig()
+    m.tft.invertTransform = capture
+    outdir = "/tmp/golden_%s_sep" % name
+    os.makedirs(outdir, exist_ok=True)
+    m.separate_spat_comps(dir_results=outdir)
+    J = len(m.spat_comps)
+    out['images'] = np.array(images).reshape(J, 2, *images[0].shape)
+    for n, fn in enumerate(m.files['spat_comp']):
+        out['sep_wav_%d' % n] = wf.read(fn)[1]
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, {k: np.shape(v) for k, v in out.items() if k in ('Cx', 'images', 'logliks')})
+
+
+def run_stft():
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    from pyfasst.tftransforms import stft as S
+    rs = np.random.RandomState(7)
+    x = rs.randn(3001)
+    out = {'x': x}
+    for nfft, hop in ((256, 64), (512, 128), (1024, 256)):
+        tr = S.STFT(linFTLen=nfft, atomHopFactor=hop / float(nfft))
+        tr.computeTransform(x)
+        out['X_%d_%d' % (nfft, hop)] = tr.transfo
+        out['y_%d_%d' % (nfft, hop)] = tr.invertTransform()
+    np.savez_compressed(os.path.join(HERE, "stft.npz"), **out)
+    print("stft")
+
+
+def run_nmf():
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    from pyfasst.tools import nmf
+    rs = np.random.RandomState(3)
+    SX = rs.gamma(0.7, 1.0, size=(97, 150)) * np.outer(rs.gamma(2, 1, 97), np.ones(150))
+    np.random.seed(1)
+    W, H = nmf.NMF_decomposition(SX, nbComps=6, niter=7)
+    np.savez_compressed(os.path.join(HERE, "nmf.npz"), SX=SX, W=W, H=H)
+    print("nmf")
+
+
+def run_inv_herm():
+    """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
+    import numpy as np
+    sys.path.insert(0, SCRATCH)
+    src = open("/root/reference/pyfasst_tests/pyfasst/tools/test_signalTools.py").read()
+    ns = {'np': np}
+    start = src.index("sigma_x_diag = np.array(")
+    stop = src.index("def test_inv_herm_mat_2d")
+    exec(compile(src[start:stop], "fixture", "exec"), ns)
+    from pyfasst.tools import signalTools as st
+    d, o, det = st.inv_herm_mat_2d(ns['sigma_x_diag'], ns['sigma_x_off'])
+    np.savez_compressed(os.path.join(HERE, "inv_herm.npz"),
+                        sigma_x_diag=ns['sigma_x_diag'], sigma_x_off=ns['sigma_x_off'],
+                        inv_diag_ref=ns['inv_sigma_x_diag_ref'], inv_off_ref=ns['inv_sigma_x_off_ref'],
+                        inv_diag_run=d, inv_off_run=o, det_run=det)
+    print("inv_herm")
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    if len(sys.argv) > 2 and sys.argv[1] == "--case":
+        name = sys.argv[2]
+        {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm}.get(
+            name, lambda: run_case(name))()
+        sys.exit(0)
+    import make_scratch_ref
+    if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
+        make_scratch_ref.build(SCRATCH)
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf"] + list(CASES))
+    for name in names:
+        subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])
