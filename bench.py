@@ -1,0 +1,196 @@
+"""bench.py -- EM iterations/sec of the FASST GEM loop on MI355X.
+
+Workload (BASELINE.json configs[2] / [3]): synthetic stereo STFT-domain clip,
+F=2049 bins x T=10000 frames, J=4 convolutive sources of spatial rank 2,
+K=32 NMF components (MultiChanNMFConv + makeItConvolutive).  One clip per
+GPU (config 4 = 8 independent clips): weak scaling, no collective in the
+data path; torch.distributed (RCCL) only provides the start/stop barrier and
+the max-over-ranks time.
+
+A "step" is one GEM iteration (audioModel.py:384-428) on the GPU, inputs
+resident in HBM.  Prints ONE JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+F_BINS, T_FRAMES, J_SRC, RANK, K_NMF = 2049, 10000, 4, 2, 32
+FP64_MFMA_PEAK = 78.6e12   # MI355X dense FP64 matrix, FLOP/s (spec)
+FP64_VALU_PEAK = 78.6e12   # MI355X FP64 vector, FLOP/s (spec)
+HBM_PEAK = 8.0e12          # B/s (spec)
+
+
+def kernel_work(F, T, J, R, K):
+    """Algorithmic FLOPs / bytes per launch of each GEM-iteration kernel.
+
+    k_estep:       V^T tiles 2JK, E-step VALU ~ (8J + 70 + 9 J(J+1)/2 + 17J + 10R) per (f,t);
+                   bytes 32 (Cx) + 8J (hat_W write) per (f,t)
+    k_fb_contract: V^T 2K + num/den 4K per (f,t,j); bytes 8 (hat_W) per (f,t,j)
+    k_tw_contract: V_old, V_new 4K + num/den 4K per (f,t,j); bytes 8 per (f,t,j)
+    """
+    ft = float(F) * T
+    np_ = J * (J + 1) / 2
+    return {
+        "k_estep": dict(flops=ft * (2 * J * K + 8 * J + 70 + 9 * np_ + 17 * J + 10 * R),
+                        bytes=ft * (32 + 8 * J)),
+        "k_fb_contract": dict(flops=ft * J * 6 * K, bytes=ft * J * 8),
+        "k_tw_contract": dict(flops=ft * J * 8 * K, bytes=ft * J * 8),
+    }
+
+
+def build_model(seed, device, T=T_FRAMES):
+    import pyfasst_amd.audioModel as am
+    from pyfasst_amd import synthetic
+    from pyfasst_amd.audioObject import SpectralAudio
+    X = synthetic.stereo_mixture(F_BINS, T, J=J_SRC, K_true=8, rank=RANK, seed=seed)
+    np.random.seed(1)
+    m = am.MultiChanNMFConv(SpectralAudio(X=X), nbComps=J_SRC, nbNMFComps=K_NMF,
+                            spatial_rank=RANK, iter_num=1, wlen=4096, hopsize=512,
+                            device=device)
+    m.makeItConvolutive()
+    return m
+
+
+def psd_schedule(m, n):
+    N = m.iter_num = max(n, 1)
+    return np.array([m._annealed_psd(i % N) for i in range(n)])
+
+
+def cpu_baseline(T_sample=1000):
+    """The oracle (NumPy restatement with the reference's operation structure)
+    on a bounded sample: same F, J, rank, K but T_sample frames, one GEM
+    iteration; scaled to the full T (the iteration is linear in T)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import fasst_ref as R
+    from pyfasst_amd import synthetic
+    X = synthetic.stereo_mixture(F_BINS, T_sample, J=J_SRC, K_true=8, rank=RANK, seed=0)
+    o = R.RefFASST(iter_num=1)
+    o.set_transform([X[0], X[1]])
+    np.random.seed(1)
+    R.init_nmf_inst(o, J_SRC, K_NMF, RANK)
+    R.make_convolutive(o)
+    o.noise['PSD'] = o.annealed_psd(0)
+    t0 = time.perf_counter()
+    o.GEM_iteration()
+    dt = time.perf_counter() - t0
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get('num_threads', 1) for p in threadpool_info()] + [1])
+    except Exception:
+        cores = 1
+    scale = T_FRAMES / float(T_sample)
+    return {"value": 1.0 / (dt * scale), "unit": "EM it/s", "cores": int(cores), "kind": "port",
+            "sample": "oracle/fasst_ref.py, 1 GEM iteration at F=%d T=%d J=%d r=%d K=%d "
+                      "(%.2f s), scaled x%.0f to T=%d; BLAS threads=%d, elementwise NumPy "
+                      "single-threaded" % (F_BINS, T_sample, J_SRC, RANK, K_NMF, dt, scale,
+                                           T_FRAMES, cores)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--T", type=int, default=T_FRAMES)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    m = build_model(seed=rank, device=local, T=args.T)
+    eng = m._engine
+    order, Ks, conv = m._upload()
+    rows_w = psd_schedule(m, max(args.warmup, 1))
+    if args.warmup:
+        eng.run(rows_w[:args.warmup], m.nmfUpdateCoeff)
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    rows = psd_schedule(m, args.steps)
+    barrier_sync()
+    t0 = time.perf_counter()
+    done = 0
+    while done < args.steps:
+        _, n, mask = eng.run(rows[done:], m.nmfUpdateCoeff)
+        done += n
+        if mask:   # random TW restart (host RNG) then resume, as the product does
+            m._download(order, Ks, conv)
+            m._restart_tw(mask, order)
+            order, Ks, conv = m._upload()
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda:%d" % local)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # per-kernel HIP-event timing on the engine's stream (separate, untimed pass)
+    eng.set_profiling(True)
+    eng.run(psd_schedule(m, 3), m.nmfUpdateCoeff)
+    times = eng.kernel_times()
+    eng.set_profiling(False)
+
+    if rank == 0:
+        R = sum(m.rank)
+        work = kernel_work(m.nbFreqsSigRepr, m.nbFramesSigRepr, J_SRC, R, K_NMF)
+        dom = max(times, key=lambda k: times[k][0])
+        rl = None
+        if dom in work:
+            sec = times[dom][0] * 1e-3
+            achieved = work[dom]["flops"] / sec / 1e12
+            rl = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_MFMA_PEAK / 1e12,
+                  "unit": "TFLOP/s", "frac": round(achieved * 1e12 / FP64_MFMA_PEAK, 4),
+                  "traffic": None, "kernel": dom, "kernel_ms": round(times[dom][0], 4),
+                  "dtype": "f64"}
+        out = {
+            "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",
+            "value": round(world * args.steps / dt, 4),
+            "unit": "EM it/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (STFT-domain stereo NMF mixture, RandomState(rank); init seed 1)",
+            "config": {"workload": "C3/C4: MultiChanNMFConv GEM, F=%d T=%d J=%d spatial_rank=%d "
+                                   "K=%d, one clip per GPU" % (m.nbFreqsSigRepr, m.nbFramesSigRepr,
+                                                              J_SRC, RANK, K_NMF),
+                       "parallelism": "clip-per-GPU x%d" % world},
+            "roofline": rl,
+            "kernels_ms": {k: round(v[0], 4) for k, v in sorted(times.items())},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,127 @@
+/*
+ * fasst_hip.h -- C ABI of the MI355X FASST EM engine (libfasst_hip.so).
+ *
+ * The reference (s-ben/pyfasst) has no FFI layer: its seam is the Python
+ * class surface of audioModel.py operating on NumPy state.
+ * Each entry point below replaces one reference routine; the Python host
+ * side (pyfasst_amd/audioModel.py) binds them with ctypes and keeps the
+ * reference's class surface, argument meaning and exceptions.
+ *
+ * Conventions
+ *   - all arrays are host arrays, C (row-major) order, caller-owned, copied in
+ *     and out; the library owns every device allocation;
+ *   - real data is float64; complex data is complex128 == interleaved
+ *     (re, im) float64 pairs, exactly NumPy's memory layout;
+ *   - one context = one GPU + one HIP stream; calls on a context are
+ *     serialised by the caller; distinct contexts may live on distinct threads;
+ *   - every function returns a status code (FASST_OK == 0); the message of
+ *     the last failure of the calling thread is in fasst_last_error().
+ */
+#ifndef FASST_HIP_H
+#define FASST_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FASST_OK               0
+#define FASST_ERR_SHAPE        1  /* -> AttributeError / ValueError          */
+#define FASST_ERR_SINGULAR     2  /* -> np.linalg.LinAlgError('Singular Matrix'),
+                                     audioModel.py:855-863                    */
+#define FASST_ERR_DEVICE       3  /* HIP runtime / kernel failure             */
+#define FASST_ERR_OOM          4  /* device allocation failed                 */
+#define FASST_TW_RESTART       5  /* renormalize_parameters found sum(TW)<eps
+                                     (audioModel.py:2023-2028): the host must
+                                     draw the random restart and resume       */
+#define FASST_ERR_UNSUPPORTED  6  /* model structure outside the HIP path     */
+
+typedef struct fasst_ctx fasst_ctx;
+
+const char *fasst_last_error(void);
+int fasst_device_count(int *n);
+
+/* ---- model context ------------------------------------------------------
+ * Replaces the NumPy state of FASST (audioModel.py:159-248,2349-2393).
+ * fasst_create allocates the observation (F freq bins x T frames, stereo:
+ * the reference GEM is stereo-only, audioModel.py:394,418-420,605-607);
+ * fasst_configure (re)allocates the model: J spatial components (= sources),
+ * rank[J] spatial ranks, K[J] NMF components, mix_conv 0 = 'inst' (params
+ * C x r), 1 = 'conv' (params r x C x F).  Reconfiguring keeps Cx / X.       */
+int fasst_create(int device, int F, int T, fasst_ctx **out);
+int fasst_configure(fasst_ctx *ctx, int J, const int *rank, const int *K, int mix_conv);
+int fasst_destroy(fasst_ctx *ctx);
+
+/* comp_transf_Cx (audioModel.py:250-302) on the device: data[L][2] float64
+ * (already scaled as AudioObject, audioObject.py:124-127), Hann or any
+ * window[wlen], nfft (== fsize), hop.  Keeps the channel STFTs resident for
+ * the Wiener images and builds Cx.  T must equal ceil(L/hop)+2.            */
+int fasst_set_audio(fasst_ctx *ctx, const double *data, int L, const double *window,
+                    int wlen, int nfft, int hop);
+/* mix_psd[F] = mean_t over the channel PSDs / 2 (audioModel.py:304-319).   */
+int fasst_mix_psd(fasst_ctx *ctx, double *mix_psd);
+
+/* Cx: complex128 [3][F][T], packed upper triangle {X0 X0*, X0 X1*, X1 X1*}
+ * exactly as FASST.Cx (audioModel.py:293-302).                              */
+int fasst_set_cx(fasst_ctx *ctx, const double *cx);
+int fasst_get_cx(fasst_ctx *ctx, double *cx);
+/* X: complex128 [2][F][T] channel STFTs kept resident for the Wiener images
+ * (replaces the per-source STFT recomputation of audioModel.py:1188-1192);
+ * Cx is rebuilt from them on the device (audioModel.py:293-302).           */
+int fasst_set_stft(fasst_ctx *ctx, const double *X);
+
+/* Spatial component j: params in the reference layout (complex128; for
+ * 'inst' the C x r matrix, for 'conv' r x C x F); free = frdm_prior=='free'.*/
+int fasst_set_spatial(fasst_ctx *ctx, int j, const double *params, int free_);
+int fasst_get_spatial(fasst_ctx *ctx, int j, double *params);
+/* Spectral component of source j (single NMF factor, TB empty):
+ * FB F x K, FW K x K, TW K x T (float64).                                    */
+int fasst_set_spectral(fasst_ctx *ctx, int j, const double *FB, const double *FW,
+                       const double *TW, int fb_free, int tw_free);
+int fasst_get_spectral(fasst_ctx *ctx, int j, double *FB, double *FW, double *TW);
+
+/* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j is
+ * set when sum(TW_j) < eps: the caller draws the restart (host RNG order).  */
+int fasst_renormalize(fasst_ctx *ctx, int *restart_mask);
+
+/* n_iter GEM iterations (GEM_iteration, audioModel.py:384-428), with the
+ * annealed noise PSD rows psd[n_iter][F] (audioModel.py:364-373) and the NMF
+ * exponent omega (nmfUpdateCoeff).  logliks[n_iter] receives the loglik of
+ * each iteration.  On FASST_TW_RESTART, *iters_done iterations are complete
+ * (the last one ended in the restart condition reported in restart_mask).   */
+int fasst_run(fasst_ctx *ctx, int n_iter, const double *psd, double omega,
+              double *logliks, int *restart_mask, int *iters_done);
+
+/* Per-source STFT-domain Wiener images (separate_comps,
+ * audioModel.py:1088-1217 up to the iSTFT; compute_sigma_comp_2d :1327,
+ * compute_inv_sigma_mix_2d :1374, compute_Wiener_gain_2d :1396).  psd[F] is
+ * the last annealed PSD; X complex128 [2][F][T] or NULL to use the resident
+ * STFT; S out complex128 [J][2][F][T].                                       */
+int fasst_wiener_images(fasst_ctx *ctx, const double *psd, const double *X, double *S);
+
+/* Per-kernel timing with HIP events recorded on the context's stream
+ * (used by bench.py for the roofline of the dominant kernel).
+ * fasst_kernel_times returns the number of kernel slots and fills the mean
+ * duration in ms of each slot over the profiled iterations.                */
+int fasst_set_profiling(fasst_ctx *ctx, int on);
+int fasst_kernel_times(fasst_ctx *ctx, double *avg_ms, long *counts, int nk);
+const char *fasst_kernel_name(int i);
+
+/* ---- stateless kernels --------------------------------------------------
+ * stft (tftransforms/stft.py:3-69): x[L] float64, window[wlen], nfft a power
+ * of two >= wlen, hop; X out complex128 [nfft/2+1][n_frames] with
+ * n_frames = ceil(L/hop)+2 (query with X == NULL).                           */
+int fasst_stft(int device, const double *x, int L, const double *window, int wlen,
+               int nfft, int hop, double *X, int *n_frames);
+/* istft (tftransforms/stft.py:71-131): X complex128 [nfft/2+1][n_frames];
+ * y out float64 [hop*(n_frames-1)+wlen - wlen/2].                           */
+int fasst_istft(int device, const double *X, int n_frames, const double *window,
+                const double *analysis_window, int wlen, int nfft, int hop, double *y);
+/* inv_herm_mat_2d (tools/signalTools.py:132-196) on n matrices:
+ * diag[2][n], off complex128[n] -> inv_diag[2][n], inv_off complex128[n], det[n]. */
+int fasst_inv_herm_mat_2d(int device, int n, const double *diag, const double *off,
+                          double *inv_diag, double *inv_off, double *det);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FASST_HIP_H */

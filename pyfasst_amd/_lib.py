@@ -1,0 +1,120 @@
+"""ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing this
+module raises at import time, and every compute call raises if the device
+call fails.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FASST_HIP_LIB", os.path.join(_HERE, "libfasst_hip.so"))
+
+FASST_OK = 0
+FASST_ERR_SHAPE = 1
+FASST_ERR_SINGULAR = 2
+FASST_ERR_DEVICE = 3
+FASST_ERR_OOM = 4
+FASST_TW_RESTART = 5
+FASST_ERR_UNSUPPORTED = 6
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "pyfasst_amd: HIP library %s not found; build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` or "
+        "`make -C pyfasst_amd/csrc` (hipcc --offload-arch=gfx950)" % LIB_PATH)
+
+lib = ctypes.CDLL(LIB_PATH)
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/fasst_hip.h exactly
+SIGNATURES = {
+    "fasst_last_error": (ctypes.c_char_p, []),
+    "fasst_device_count": (ctypes.c_int, [_ip]),
+    "fasst_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "fasst_configure": (ctypes.c_int, [_vp, ctypes.c_int, _ip, _ip, ctypes.c_int]),
+    "fasst_destroy": (ctypes.c_int, [_vp]),
+    "fasst_set_audio": (ctypes.c_int, [_vp, _dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int]),
+    "fasst_mix_psd": (ctypes.c_int, [_vp, _dp]),
+    "fasst_set_cx": (ctypes.c_int, [_vp, _dp]),
+    "fasst_get_cx": (ctypes.c_int, [_vp, _dp]),
+    "fasst_set_stft": (ctypes.c_int, [_vp, _dp]),
+    "fasst_set_spatial": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_int]),
+    "fasst_get_spatial": (ctypes.c_int, [_vp, ctypes.c_int, _dp]),
+    "fasst_set_spectral": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _dp, ctypes.c_int,
+                                          ctypes.c_int]),
+    "fasst_get_spectral": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _dp]),
+    "fasst_renormalize": (ctypes.c_int, [_vp, _ip]),
+    "fasst_run": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_double, _dp, _ip, _ip]),
+    "fasst_wiener_images": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
+    "fasst_stft": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, _dp, _ip]),
+    "fasst_istft": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, _dp]),
+    "fasst_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "fasst_kernel_times": (ctypes.c_int, [_vp, _dp, ctypes.POINTER(ctypes.c_long), ctypes.c_int]),
+    "fasst_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "fasst_inv_herm_mat_2d": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp,
+                                             _dp]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+class FasstError(RuntimeError):
+    pass
+
+
+def last_error():
+    msg = lib.fasst_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(status, what=""):
+    """Map a status code to the reference's exceptions."""
+    if status == FASST_OK:
+        return
+    msg = "%s: %s" % (what, last_error())
+    if status == FASST_ERR_SINGULAR:
+        raise np.linalg.LinAlgError('Singular Matrix')
+    if status == FASST_ERR_SHAPE:
+        raise ValueError(msg)
+    if status == FASST_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    if status == FASST_ERR_OOM:
+        raise MemoryError(msg)
+    raise FasstError("%s (status %d)" % (msg, status))
+
+
+def dptr(a):
+    """float64 / complex128 C-contiguous array -> double*"""
+    assert a.flags['C_CONTIGUOUS'] and a.dtype in (np.float64, np.complex128), (a.dtype, a.flags)
+    return a.ctypes.data_as(_dp)
+
+
+def iptr(a):
+    assert a.flags['C_CONTIGUOUS'] and a.dtype == np.int32
+    return a.ctypes.data_as(_ip)
+
+
+def default_device():
+    """Device index for this process: FASST_DEVICE, else LOCAL_RANK, else 0."""
+    for var in ("FASST_DEVICE", "LOCAL_RANK"):
+        if var in os.environ:
+            return int(os.environ[var])
+    return 0
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib.fasst_device_count(ctypes.byref(n)), "fasst_device_count")
+    return n.value

@@ -1,0 +1,462 @@
+"""FASST model classes with the reference's surface, running on MI355X.
+
+Drop-in for pyfasst.audioModel (audioModel.py:66-2508): same class names,
+constructor keyword arguments, `spat_comps` / `spec_comps` / `noise` dicts
+and public methods.  Between calls the NumPy dicts are the source of truth;
+`estim_param_a_post_model()` uploads them once, runs every GEM iteration on
+the GPU (pyfasst_amd/csrc/fasst_em.hip) and downloads the result;
+`separate_spat_comps()` computes the Wiener images and iSTFTs on the GPU.
+
+There is no CPU fallback: structures outside the HIP path raise
+NotImplementedError, a missing library raises ImportError.
+
+Deliberate deviation: the reference stores the shared
+mutable default `ann_PSD_lim=[None, None]` by reference, so a second model
+in the same process inherits the first model's annealing limits
+(audioModel.py:166,242,320-323); here each model copies the list.
+"""
+import os
+import warnings
+
+import numpy as np
+
+from . import audioObject as ao
+from .engine import Engine
+from .tftransforms import stft as stft_mod
+
+eps = 1e-10              # audioModel.py:61
+log_prior_small_cst = 1e-70
+soundCelerity = 340.
+
+
+class FASST(object):
+    """FASST base class (audioModel.py:66-248)."""
+    implemented_transf = ['stft']
+    implemented_annealing = ['ann', 'no_ann']
+
+    def __init__(self, audio, transf='stft', wlen=2048, hopsize=512, iter_num=50,
+                 sim_ann_opt='ann', ann_PSD_lim=[None, None], verbose=0, nmfUpdateCoeff=1.,
+                 tffmin=25, tffmax=18000, tfWinFunc=None, tfbpo=48, lambdaCorr=0.,
+                 device=None):
+        self.verbose = verbose
+        self.nmfUpdateCoeff = nmfUpdateCoeff
+        if isinstance(audio, ao.AudioObject):
+            self.audioObject = audio
+        elif isinstance(audio, str):
+            self.audioObject = ao.AudioObject(filename=audio)
+        else:
+            raise AttributeError("The provided audio parameter is" + "not a supported format.")
+        self.device = device
+        self.sig_repr_params = {}
+        self.sig_repr_params['transf'] = transf.lower()
+        self.sig_repr_params['wlen'] = ao.nextpow2(wlen)
+        self.sig_repr_params['fsize'] = ao.nextpow2(wlen)
+        self.sig_repr_params['hopsize'] = hopsize
+        self.sig_repr_params['tffmin'] = tffmin
+        self.sig_repr_params['tffmax'] = tffmax
+        self.sig_repr_params['tfbpo'] = tfbpo
+        self.sig_repr_params['tfWinFunc'] = tfWinFunc
+        self.sig_repr_params['hopfactor'] = 1. * hopsize / self.sig_repr_params['wlen']
+        if self.sig_repr_params['transf'] not in self.implemented_transf:
+            raise NotImplementedError(self.sig_repr_params['transf'] + " not yet implemented.")
+        self.tft = stft_mod.STFT(linFTLen=self.sig_repr_params['fsize'],
+                                 atomHopFactor=self.sig_repr_params['hopfactor'],
+                                 fs=self._samplerate_or_default(), device=device)
+        self.demixParams = {
+            'tffmin': tffmin, 'tffmax': tffmax, 'tfbpo': tfbpo,
+            'tfrepresentation': transf.lower(), 'wlen': self.sig_repr_params['wlen'],
+            'hopsize': self.sig_repr_params['wlen'] // 2, 'neighbors': 20, 'winFunc': tfWinFunc}
+        self.noise = {}
+        self.noise['PSD'] = np.zeros(self.sig_repr_params['fsize'] // 2 + 1)
+        self.noise['sim_ann_opt'] = sim_ann_opt
+        self.noise['ann_PSD_lim'] = list(ann_PSD_lim)
+        self.spat_comps = {}
+        self.spec_comps = {}
+        self.iter_num = iter_num
+        self.lambdaCorr = lambdaCorr
+        self._engine = None
+        self._Cx = None
+
+    def _samplerate_or_default(self):
+        try:
+            return self.audioObject.samplerate
+        except Exception:
+            return 44100
+
+    # ---------------------------------------------------------------- Cx
+    @property
+    def Cx(self):
+        """Packed covariance [3, F, T] (audioModel.py:293-302), fetched lazily."""
+        if self._Cx is None and self._engine is not None:
+            self._Cx = self._engine.get_cx()
+        return self._Cx
+
+    @Cx.setter
+    def Cx(self, value):
+        value = np.asarray(value, dtype=np.complex128)
+        self._Cx = value
+        if value.ndim == 3:
+            self.nbFreqsSigRepr, self.nbFramesSigRepr = value.shape[1:]
+            if (self._engine is None or self._engine.F != value.shape[1]
+                    or self._engine.T != value.shape[2]):
+                self._engine = Engine(value.shape[1], value.shape[2], self.device)
+            self._engine.set_cx(value)
+
+    def comp_transf_Cx(self):
+        """Signal representation on the GPU (audioModel.py:250-328)."""
+        if self.sig_repr_params['transf'] not in self.implemented_transf:
+            raise ValueError(self.sig_repr_params['transf'] + " not implemented - yet?")
+        aud = self.audioObject
+        if isinstance(aud, ao.SpectralAudio):
+            F, T = aud.nbFreqs, aud.nbFrames
+            self._engine = Engine(F, T, self.device)
+            self.nbFreqsSigRepr, self.nbFramesSigRepr = F, T
+            if aud.X is not None:
+                self._engine.set_stft(aud.X)   # Cx packed on the device
+                self._Cx = None
+            else:
+                self.Cx = aud.Cx
+        else:
+            if not hasattr(aud, '_data'):
+                aud._read()
+            nc = aud.channels
+            if nc != 2:
+                raise NotImplementedError("the HIP path handles stereo signals (got %d)" % nc)
+            data = np.asarray(aud.data, dtype=np.float64)
+            L = data.shape[0]
+            hop = self.tft.fthop
+            T = int(np.ceil(L / np.double(hop))) + 2
+            F = self.tft.freqbins
+            self._engine = Engine(F, T, self.device)
+            self._engine.set_audio(data, self.tft.window, self.tft.ftlen, hop)
+            self.tft.datalen_init = L
+            self.nbFreqsSigRepr, self.nbFramesSigRepr = F, T
+            self._Cx = None
+        lim = self.noise['ann_PSD_lim']
+        if lim[0] is None or lim[1] is None:
+            mix_psd = self._engine.mix_psd()
+            if lim[0] is None:
+                lim[0] = np.real(mix_psd) / 100.
+            if lim[1] is None:
+                lim[1] = np.real(mix_psd) / 10000.
+        if self.noise['sim_ann_opt'] in ('ann'):   # substring test, as the reference (:324)
+            self.noise['PSD'] = lim[0]
+
+    # ---------------------------------------------------------------- structure
+    def _structure(self):
+        """Check the model is on the HIP path; return (order, ranks, Ks, conv).
+
+        HIP path: stereo; one single-factor NMF spectral component per spatial
+        component (TB empty, TW_constr 'NMF', FW fixed); all spatial
+        components 'inst' or all 'conv'; lambdaCorr == 0.
+        """
+        if self.audioObject.channels != 2:
+            raise AttributeError("Nb channels " + str(self.audioObject.channels) +
+                                 " not implemented yet")
+        if self.lambdaCorr > 0:
+            raise NotImplementedError("lambdaCorr > 0 is outside the HIP path")
+        J = len(self.spat_comps)
+        if sorted(self.spat_comps.keys()) != list(range(J)):
+            raise NotImplementedError("spatial components must be numbered 0..J-1")
+        owner = {}
+        for k, comp in self.spec_comps.items():
+            j = comp['spat_comp_ind']
+            if j in owner:
+                raise NotImplementedError("several spectral components per spatial component "
+                                          "are outside the HIP path")
+            owner[j] = k
+            facs = comp['factor']
+            if list(facs.keys()) != [0]:
+                raise NotImplementedError("multi-factor spectral components are outside the HIP path")
+            fac = facs[0]
+            if len(fac['TB']):
+                raise NotImplementedError("time blobs (TB) are outside the HIP path")
+            if fac.get('TW_constr', 'NMF') != 'NMF':
+                raise NotImplementedError("TW_constr=%s is outside the HIP path" % fac['TW_constr'])
+            if fac.get('FW_frdm_prior', 'fixed') == 'free':
+                raise NotImplementedError("free FW is outside the HIP path")
+        if sorted(owner.keys()) != list(range(J)):
+            raise NotImplementedError("every spatial component needs one spectral component")
+        types = set(sc['mix_type'] for sc in self.spat_comps.values())
+        if len(types) != 1:
+            raise NotImplementedError("mixed inst/conv spatial components are outside the HIP path")
+        conv = types.pop() == 'conv'
+        if conv:
+            frees = set(sc['frdm_prior'] == 'free' for sc in self.spat_comps.values())
+            if len(frees) != 1:
+                raise NotImplementedError("mixed free/fixed convolutive components")
+        ranks, Ks = [], []
+        for j in range(J):
+            p = self.spat_comps[j]['params']
+            ranks.append(p.shape[0] if conv else p.shape[1])
+            Ks.append(self.spec_comps[owner[j]]['factor'][0]['FB'].shape[1])
+        return [owner[j] for j in range(J)], ranks, Ks, conv
+
+    def _upload(self):
+        order, ranks, Ks, conv = self._structure()
+        eng = self._engine
+        eng.configure(ranks, Ks, conv)
+        for j in range(len(order)):
+            sc = self.spat_comps[j]
+            eng.set_spatial(j, sc['params'], sc['frdm_prior'] == 'free')
+            fac = self.spec_comps[order[j]]['factor'][0]
+            eng.set_spectral(j, fac['FB'], fac['FW'], fac['TW'],
+                             fac.get('FB_frdm_prior', 'free') == 'free',
+                             fac.get('TW_frdm_prior', 'free') == 'free')
+        return order, Ks, conv
+
+    def _download(self, order, Ks, conv, updated_spatial=True):
+        eng = self._engine
+        for j in range(len(order)):
+            sc = self.spat_comps[j]
+            p = eng.get_spatial(j, sc['params'].shape)
+            if not np.iscomplexobj(sc['params']) and not (updated_spatial and
+                                                          sc['frdm_prior'] == 'free'):
+                p = p.real.copy()
+            sc['params'] = p
+            fac = self.spec_comps[order[j]]['factor'][0]
+            FB, FW, TW = eng.get_spectral(j, Ks[j])
+            for key, val in (('FB', FB), ('FW', FW), ('TW', TW)):
+                if isinstance(fac[key], np.ndarray) and fac[key].shape == val.shape \
+                        and fac[key].dtype == val.dtype:
+                    fac[key][...] = val
+                else:
+                    fac[key] = val
+
+    def _restart_tw(self, mask, order):
+        """Random TW restart of renormalize_parameters (audioModel.py:2023-2028),
+        drawn on the host RNG in spectral-component order."""
+        for k in sorted(self.spec_comps.keys()):
+            j = self.spec_comps[k]['spat_comp_ind']
+            if mask & (1 << j):
+                fac = self.spec_comps[k]['factor'][0]
+                fac['TW'] = np.random.randn(*fac['TW'].shape) ** 2
+                fac['TW'] *= 1e3 * eps
+                if self.verbose:
+                    print("    renorm: reinitialized TW for spec", k, "factor", 0)
+
+    # ---------------------------------------------------------------- EM
+    def _annealed_psd(self, i):
+        lim = self.noise['ann_PSD_lim']
+        return ((np.sqrt(lim[0]) * (self.iter_num - i) + np.sqrt(lim[1]) * i)
+                / self.iter_num) ** 2
+
+    def estim_param_a_post_model(self,):
+        """Run iter_num GEM iterations on the GPU (audioModel.py:330-382)."""
+        logliks = np.ones(self.iter_num)
+        opt = self.noise['sim_ann_opt']
+        if opt in ['ann', ]:
+            self.noise['PSD'] = self.noise['ann_PSD_lim'][0]
+        elif opt == 'no_ann':
+            self.noise['PSD'] = self.noise['ann_PSD_lim'][1]
+        else:
+            warnings.warn("To add noise to the signal, provide the " +
+                          "sim_ann_opt from any of 'ann', " + "'no_ann' or 'ann_ns_inj' ")
+        rows = []
+        for i in range(self.iter_num):
+            if opt in ['ann', 'ann_ns_inj']:
+                rows.append(self._annealed_psd(i))
+            else:
+                rows.append(np.asarray(self.noise['PSD'], dtype=np.float64) *
+                            np.ones(self.nbFreqsSigRepr))
+        if not rows:
+            return logliks
+        rows = np.array(rows, dtype=np.float64)
+        order, Ks, conv = self._upload()
+        i0 = 0
+        while i0 < self.iter_num:
+            ll, done, mask = self._engine.run(rows[i0:], self.nmfUpdateCoeff)
+            logliks[i0:i0 + done] = ll
+            i0 += done
+            if mask:
+                self._download(order, Ks, conv)
+                self._restart_tw(mask, order)
+                order, Ks, conv = self._upload()
+        self._download(order, Ks, conv)
+        self.noise['PSD'] = rows[-1]
+        if self.verbose:
+            for i in range(self.iter_num):
+                print("Iteration", i + 1, "on", self.iter_num, "    log-likelihood:", logliks[i])
+        return logliks
+
+    def GEM_iteration(self,):
+        """One GEM iteration with the current noise PSD (audioModel.py:384-428)."""
+        order, Ks, conv = self._upload()
+        psd = np.asarray(self.noise['PSD'], dtype=np.float64) * np.ones(self.nbFreqsSigRepr)
+        ll, done, mask = self._engine.run(psd[None, :], self.nmfUpdateCoeff)
+        self._download(order, Ks, conv)
+        if mask:
+            self._restart_tw(mask, order)
+        return ll[0]
+
+    def renormalize_parameters(self):
+        """renormalize_parameters on the GPU (audioModel.py:1980-2040)."""
+        order, Ks, conv = self._upload()
+        mask = self._engine.renormalize()
+        self._download(order, Ks, conv, updated_spatial=False)
+        if mask:
+            self._restart_tw(mask, order)
+
+    # ---------------------------------------------------------------- separation
+    def separate_spat_comps(self, dir_results=None, suffix=None):
+        """One source per spatial component (audioModel.py:1063-1086)."""
+        spec_comp_ind = {}
+        for spat_ind in range(len(self.spat_comps)):
+            spec_comp_ind[spat_ind] = []
+        for spec_ind, spec_comp in self.spec_comps.items():
+            spec_comp_ind[spec_comp['spat_comp_ind']].append(spec_ind)
+        self.separate_comps(dir_results=dir_results, spec_comp_ind=spec_comp_ind, suffix=suffix)
+
+    def separated_images(self, spec_comp_ind=None):
+        """STFT-domain Wiener images S[n, c] = sum_c2 WG_n[c, c2] X[c2], as the
+        reference computes before its iSTFT (audioModel.py:1136-1214)."""
+        if spec_comp_ind is None:
+            spec_comp_ind = {}
+            for spec_ind in range(len(self.spec_comps)):
+                spec_comp_ind[spec_ind] = [spec_ind, ]
+        order, Ks, conv = self._upload()
+        src_spat = []
+        for n in range(len(spec_comp_ind)):
+            spats = np.unique([self.spec_comps[k]['spat_comp_ind'] for k in spec_comp_ind[n]])
+            if len(spats) != 1 or sorted(spec_comp_ind[n]) != [order[spats[0]]]:
+                raise NotImplementedError("sources must map one-to-one to spatial components "
+                                          "on the HIP path")
+            src_spat.append(int(spats[0]))
+        if len(set(src_spat)) != len(src_spat) or len(src_spat) != len(order):
+            raise NotImplementedError("sources must map one-to-one to spatial components")
+        psd = np.asarray(self.noise['PSD'], dtype=np.float64) * np.ones(self.nbFreqsSigRepr)
+        S = self._engine.wiener_images(psd)
+        return S[src_spat]
+
+    def separate_comps(self, dir_results=None, spec_comp_ind=None, suffix=None):
+        """Wiener-filter and write one WAV per source (audioModel.py:1088-1236)."""
+        if dir_results is None:
+            dir_results = '/'.join(self.audioObject.filename.split('/')[:-1])
+        nc = self.audioObject.channels
+        if nc != 2:
+            raise NotImplementedError()
+        S = self.separated_images(spec_comp_ind)
+        nbSources = S.shape[0]
+        if not hasattr(self, "files"):
+            self.files = {}
+        self.files['spat_comp'] = []
+        fileroot = self.audioObject.filename.split('/')[-1][:-4]
+        for n in range(nbSources):
+            ndata = []
+            for chan1 in range(nc):
+                self.tft.transfo = S[n, chan1]
+                ndata.append(self.tft.invertTransform())
+                del self.tft.transfo
+            ndata = np.array(ndata).T
+            _suffix = ''
+            if suffix is not None and n in suffix:
+                _suffix = '_' + suffix[n]
+            outAudioName = (dir_results + '/' + fileroot + '_' + str(n) + '-' +
+                            str(nbSources) + _suffix + '.wav')
+            self.files['spat_comp'].append(outAudioName)
+            out = ao.AudioObject(filename=outAudioName, mode='w')
+            out._data = np.int16(ndata[:self.audioObject.nframes, :] * self.audioObject._maxdata)
+            out._maxdata = 1
+            out._encoding = 'pcm16'
+            out.samplerate = self.audioObject.samplerate
+            out._write()
+
+    # ---------------------------------------------------------------- helpers
+    def comp_spat_comp_power(self, spat_comp_ind, spec_comp_ind=[], factor_ind=[]):
+        """Host-side V = prod_factors (FB.FW).(TW[.TB]) (audioModel.py:430-498);
+        a parameter inspection helper, not used by the GPU iteration."""
+        V = np.zeros([self.nbFreqsSigRepr, self.nbFramesSigRepr])
+        keys = spec_comp_ind if len(spec_comp_ind) else list(self.spec_comps.keys())
+        for k in keys:
+            if spat_comp_ind != self.spec_comps[k]['spat_comp_ind']:
+                continue
+            Vc = np.ones([self.nbFreqsSigRepr, self.nbFramesSigRepr])
+            facs = factor_ind if len(factor_ind) else list(self.spec_comps[k]['factor'].keys())
+            for fi in facs:
+                fac = self.spec_comps[k]['factor'][fi]
+                H = np.dot(fac['TW'], fac['TB']) if len(fac['TB']) else fac['TW']
+                Vc *= np.dot(np.dot(fac['FB'], fac['FW']), H)
+            V += Vc
+        return V
+
+
+class MultiChanNMFInst_FASST(FASST):
+    """Multichannel NMF, instantaneous mixing (audioModel.py:2296-2420)."""
+
+    def __init__(self, audio, nbComps=3, nbNMFComps=4, spatial_rank=2, **kwargs):
+        super(MultiChanNMFInst_FASST, self).__init__(audio=audio, **kwargs)
+        self.comp_transf_Cx()
+        self.nbComps = nbComps
+        self.nbNMFComps = nbNMFComps
+        self.rank = np.atleast_1d(spatial_rank)
+        if self.rank.size < self.nbComps:
+            self.rank = [self.rank[0], ] * self.nbComps
+        self._initialize_structures()
+
+    def _initialize_structures(self):
+        """Initial parameters; consumes the global np.random stream in the
+        reference's order (audioModel.py:2349-2393)."""
+        nc = self.audioObject.channels
+        self.spat_comps = {}
+        self.spec_comps = {}
+        for j in range(self.nbComps):
+            self.spat_comps[j] = {}
+            self.spat_comps[j]['time_dep'] = 'indep'
+            self.spat_comps[j]['mix_type'] = 'inst'
+            self.spat_comps[j]['frdm_prior'] = 'free'
+            self.spat_comps[j]['params'] = np.random.randn(nc, self.rank[j])
+            if nc == 2:
+                self.spat_comps[j]['params'] = (
+                    np.array([np.sin((j + 1) * np.pi / (2. * (self.nbComps + 1))) +
+                              np.random.randn(self.rank[j]) * np.sqrt(0.01),
+                              np.cos((j + 1) * np.pi / (2. * (self.nbComps + 1))) +
+                              np.random.randn(self.rank[j]) * np.sqrt(0.01)]))
+            self.spec_comps[j] = {}
+            self.spec_comps[j]['spat_comp_ind'] = j
+            self.spec_comps[j]['factor'] = {}
+            fac = {}
+            fac['FB'] = 0.75 * np.abs(np.random.randn(self.nbFreqsSigRepr, self.nbNMFComps)) + 0.25
+            fac['FW'] = np.eye(self.nbNMFComps)
+            fac['TW'] = 0.75 * np.abs(np.random.randn(self.nbNMFComps, self.nbFramesSigRepr)) + 0.25
+            fac['TB'] = []
+            fac['FB_frdm_prior'] = 'free'
+            fac['FW_frdm_prior'] = 'fixed'
+            fac['TW_frdm_prior'] = 'free'
+            fac['TB_frdm_prior'] = []
+            fac['TW_constr'] = 'NMF'
+            self.spec_comps[j]['factor'][0] = fac
+        self.renormalize_parameters()
+
+    def setSpecCompFB(self, compNb, FB, FB_frdm_prior='fixed'):
+        """audioModel.py:2395-2420"""
+        speccomp = self.spec_comps[compNb]['factor'][0]
+        if self.nbFreqsSigRepr != FB.shape[0]:
+            raise AttributeError("Size of provided FB is not consistent" + " with inner attributes")
+        speccomp['FB'] = np.copy(FB)
+        ncomp = FB.shape[1]
+        speccomp['FW'] = np.eye(ncomp)
+        speccomp['TW'] = 0.75 * np.abs(np.random.randn(ncomp, self.nbFramesSigRepr)) + 0.25
+        speccomp['FB_frdm_prior'] = FB_frdm_prior
+
+
+class MultiChanNMFConv(MultiChanNMFInst_FASST):
+    """Convolutive multichannel NMF (audioModel.py:2422-2508)."""
+
+    def __init__(self, audio, nbComps=3, nbNMFComps=4, spatial_rank=2, **kwargs):
+        super(MultiChanNMFConv, self).__init__(audio=audio, nbComps=nbComps,
+                                               nbNMFComps=nbNMFComps,
+                                               spatial_rank=spatial_rank, **kwargs)
+
+    def makeItConvolutive(self):
+        """Replicate the instantaneous params over bins (audioModel.py:2488-2508)."""
+        nc = self.audioObject.channels
+        for nspat, (spat_ind, spat_comp) in enumerate(self.spat_comps.items()):
+            if spat_comp['mix_type'] != 'inst':
+                warnings.warn("Spatial component %d " % spat_ind +
+                              "already not instantaneous, skipping...")
+            else:
+                spat_comp['mix_type'] = 'conv'
+                inst = spat_comp['params']
+                p = np.zeros([self.rank[nspat], nc, self.nbFreqsSigRepr], dtype=complex)
+                p[:] = inst.T[:, :, None]
+                spat_comp['params'] = p

@@ -1,0 +1,81 @@
+// Shared definitions of the MI355X FASST engine (gfx950, HIP).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdarg>
+#include <string>
+#include <vector>
+
+#include "../../include/fasst_hip.h"
+
+namespace fasst {
+
+constexpr double kEps = 1e-10;  // audioModel.py:61, tools/signalTools.py:11
+constexpr int kMaxJ = 4;        // sources handled by the fused E-step
+constexpr int kMaxR = 8;        // total spatial rank
+constexpr int kMaxKP = 64;      // padded NMF components
+constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+void set_error(const char *fmt, ...);
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+#define FASST_HIP(call)                                                      \
+  do {                                                                       \
+    hipError_t e_ = (call);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      ::fasst::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,          \
+                         hipGetErrorString(e_));                             \
+      return e_ == hipErrorOutOfMemory ? FASST_ERR_OOM : FASST_ERR_DEVICE;   \
+    }                                                                        \
+  } while (0)
+
+#define FASST_LAUNCH_CHECK()                                                 \
+  do {                                                                       \
+    hipError_t e_ = hipGetLastError();                                       \
+    if (e_ != hipSuccess) {                                                  \
+      ::fasst::set_error("%s:%d kernel launch: %s", __FILE__, __LINE__,      \
+                         hipGetErrorString(e_));                             \
+      return FASST_ERR_DEVICE;                                               \
+    }                                                                        \
+  } while (0)
+
+// Scoped device selection (restores the caller's device).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Device buffer owned by a context; freed in the destructor.
+template <typename T>
+struct DBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    release();
+    if (count == 0) return FASST_OK;
+    FASST_HIP(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+    // zero-fill and wait: the context stream is non-blocking, so a pending
+    // null-stream memset could otherwise land after later stream work
+    FASST_HIP(hipMemset(p, 0, count * sizeof(T)));
+    FASST_HIP(hipDeviceSynchronize());
+    return FASST_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DBuf() { release(); }
+};
+
+}  // namespace fasst

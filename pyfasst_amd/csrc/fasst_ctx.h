@@ -1,0 +1,56 @@
+// Device-resident state of one FASST model (one GPU, one stream).
+//
+// HBM layout (all float64; Fp = F rounded up to 16, Tp = T rounded up to 16,
+// KP = max K rounded up to 16; padding is zero and masked where it matters):
+//   cx      4 planes [Tp][Fp]   Cx00, Cx11, Re Cx01, Im Cx01  (frame-major,
+//                               bins contiguous: the E-step's V^T tiles read
+//                               16 consecutive bins per 128-B segment)
+//   X       [2][Tp][Fp] double2 resident channel STFTs (optional)
+//   FB      [J][Fp][KP]         frequency bases           (canonical)
+//   FW      [J][KP][KP]         frequency weights         (canonical)
+//   TW      [J][KP][Tp]         time weights              (canonical)
+//   Pinst   [R][2] double2      'inst' mixing params       (canonical)
+//   A       [R][2][Fp] double2  per-bin mixing matrix ('conv' canonical)
+//   Wkf     [J][KP][Fp]         W = FB.FW   (MFMA operand layout)
+//   Wkf_new / Wfk_new           W after the FB update, both operand layouts
+//   FWHt    [J][Tp][KP]         (FW.TW)^T  (B operand of the FB contraction)
+//   hatW    [J][Tp][Fp]         posterior source power hat_W
+#pragma once
+#include "fasst_common.h"
+
+struct fasst_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // observation
+  int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
+  fasst::DBuf<double> cx;        // 4*Tp*Fp
+  fasst::DBuf<double2> X;        // 2*Tp*Fp (resident STFT, optional)
+  bool have_X = false;
+  // model
+  int J = 0, R = 0, KP = 0, conv = 0, configured = 0;
+  int rank[fasst::kMaxJ] = {0}, roff[fasst::kMaxJ + 1] = {0}, K[fasst::kMaxJ] = {0};
+  int spat_free[fasst::kMaxJ] = {0}, fb_free[fasst::kMaxJ] = {0}, tw_free[fasst::kMaxJ] = {0};
+  fasst::DBuf<double> FB, FW, TW, Wkf, Wkf_new, Wfk_new, FWHt, hatW;
+  fasst::DBuf<double2> A, Pinst;
+  // work space
+  int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
+  fasst::DBuf<double> epart, llpart, bnum, bden, psd, ll;
+  fasst::DBuf<double2> rss, rxs;
+  fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart
+  int *h_flags = nullptr;        // pinned host mirror
+  double *h_ll = nullptr;        // pinned host mirror (one value)
+  int psd_cap = 0, ll_cap = 0;
+  // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
+  static constexpr int kNK = 11;
+  int prof = 0;
+  hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};
+  int used[kNK] = {0};
+  double prof_ms[kNK] = {0};
+  long prof_cnt[kNK] = {0};
+};
+
+namespace fasst {
+int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv);
+int build_inst_A(fasst_ctx *c);
+int launch_w_old(fasst_ctx *c);  // Wkf = FB.FW
+}  // namespace fasst

@@ -1,0 +1,1487 @@
+// FASST generalized-EM iteration on MI355X (gfx950), FP64 throughout.
+//
+// One GEM iteration (audioModel.py:384-428) is a fixed sequence of launches
+// on the context's stream:
+//   k_w_from_fb   W = FB.FW                       (comp_spat_comp_power :485)
+//   k_fwh_t       (FW.TW)^T                       (update_spectral_components :1541)
+//   k_inst_A      per-bin mixing from 'inst' params (retrieve_subsrc_params :570-574)
+//   k_estep<J>    fused E-step: V^T tiles on FP64 MFMA, Sigma_x, 2x2 inverse,
+//                 loglik, posterior powers hat_W, per-bin sufficient
+//                 statistics (compute_suff_stat :580-764)
+//   k_loglik      loglik = -mean(...)             (:660-664)
+//   k_mix_conv / k_mix_stats + k_mix_inst          (update_mix_matrix :766-889)
+//   k_fb_contract FB numerator/denominator over t (MFMA, :1521-1575)
+//   k_fb_update   FB *= (num/den)^omega, W_new = FB.FW
+//   k_tw_contract TW numerator/denominator over f (MFMA) + TW update (:1634-1727)
+//   k_renorm      renormalize_parameters          (:1980-2040)
+//
+// E-step restructuring (exact algebra, verified to 1e-15 against the
+// reference): with S = Sigma_x^-1, N = S Cx S - S and P = Cx S (2x2 per
+// (f,t)), the reference's R x R pair loop (:698-731) is
+//   hat_Rss[f][r1,r2] = a_r1^H (sum_t V_j1 V_j2 N) a_r2 / T + d_r1r2 mean_t V_r1
+//   hat_Rxs[f][c,r]   = sum_c' (sum_t V_j P)[c,c'] A_r,c' / T
+//   hat_Ws[r](f,t)    = | V_j^2 a_r^H N a_r + V_j |
+// because the mixing a_r is constant over t.  The t-reductions shrink from
+// R^2 complex products per (f,t) to J(J+1)/2 x 4 + 9J real FMAs.
+#include "fasst_ctx.h"
+
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
+namespace fasst {
+
+static thread_local std::string g_err;
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+__device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------- prep
+// W[j] = FB[j] . FW[j], written [KP][Fp] (f contiguous).
+__global__ void k_w_from_fb(const double *__restrict__ FB, const double *__restrict__ FW,
+                            double *__restrict__ Wkf, double *__restrict__ Wfk, int J, int Fp,
+                            int KP) {
+  const size_t n = (size_t)J * Fp * KP;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int f = idx % Fp;
+    const int k = (idx / Fp) % KP;
+    const int j = idx / ((size_t)Fp * KP);
+    const double *fb = FB + ((size_t)j * Fp + f) * KP;
+    const double *fw = FW + (size_t)j * KP * KP + k;
+    double s = 0.0;
+    for (int q = 0; q < KP; ++q) s += fb[q] * fw[(size_t)q * KP];
+    Wkf[((size_t)j * KP + k) * Fp + f] = s;
+    if (Wfk) Wfk[((size_t)j * Fp + f) * KP + k] = s;
+  }
+}
+
+// FWHt[j][t][k] = sum_q FW[j][k][q] TW[j][q][t]
+__global__ void k_fwh_t(const double *__restrict__ FW, const double *__restrict__ TW,
+                        double *__restrict__ FWHt, int J, int Tp, int KP) {
+  const size_t n = (size_t)J * Tp * KP;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int k = idx % KP;
+    const int t = (idx / KP) % Tp;
+    const int j = idx / ((size_t)Tp * KP);
+    const double *fw = FW + ((size_t)j * KP + k) * KP;
+    const double *tw = TW + (size_t)j * KP * Tp + t;
+    double s = 0.0;
+    for (int q = 0; q < KP; ++q) s += fw[q] * tw[(size_t)q * Tp];
+    FWHt[idx] = s;
+  }
+}
+
+// 'inst' mixing replicated over bins: A[r][c][f] = params[c][r]
+__global__ void k_inst_A(const double2 *__restrict__ Pinst, double2 *__restrict__ A, int R,
+                         int F, int Fp) {
+  const int n = R * 2 * Fp;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int f = idx % Fp;
+    const int rc = idx / Fp;
+    A[idx] = f < F ? Pinst[rc] : make_double2(0.0, 0.0);
+  }
+}
+
+// ---------------------------------------------------------------- E-step
+struct EArgs {
+  const double *cx00, *cx11, *cxr, *cxi;  // [Tp][Fp]
+  const double *TW;                       // [J][KP][Tp]
+  const double *Wkf;                      // [J][KP][Fp]
+  const double2 *A;                       // [R][2][Fp]
+  const double *psd;                      // [Fp]
+  double *hatW;                           // [J][Tp][Fp]
+  double *part;                           // [nchunk][Fp][NACC]
+  double *llpart;                         // [nchunk][nft]
+  int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
+  int roff[kMaxJ + 1];
+};
+
+// Block: 4 waves on one 16-bin tile; wave w walks frame tiles w, w+4, ... of
+// the block's chunk.  Each lane owns ONE bin (f = f0 + lane%16) and 4 frames
+// per tile, so all per-bin statistics stay in registers across the t-loop.
+template <int J>
+__global__ __launch_bounds__(256) void k_estep(const EArgs a) {
+  constexpr int NP = J * (J + 1) / 2;
+  constexpr int NACC = 4 * NP + 9 * J;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double *s_cr = smem;                     // [kMaxR][4][16]
+  double *s_cj = s_cr + kMaxR * 4 * 16;    // [J][4][16]
+  double *s_ll = s_cj + J * 4 * 16;        // [4]
+  double *s_w = s_ll + 4;                  // [J][KP][16]   (t-loop)
+  double *s_red = s_w;                     // [4][NACC][16] (epilogue, aliases s_w)
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fl = lane & 15, tq = lane >> 4;
+  const int f0 = blockIdx.x * 16;
+  const int f = f0 + fl;
+
+  for (int idx = tid; idx < J * a.KP * 16; idx += 256) {
+    const int ff = idx & 15, jk = idx >> 4;
+    s_w[idx] = a.Wkf[(size_t)jk * a.Fp + f0 + ff];
+  }
+  if (tid < 16) {
+    const int ff = f0 + tid;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      double al = 0, be = 0, gr = 0, gi = 0;
+      for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
+        const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + ff];
+        const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + ff];
+        const double aa = a0.x * a0.x + a0.y * a0.y;
+        const double bb = a1.x * a1.x + a1.y * a1.y;
+        const double cr = a0.x * a1.x + a0.y * a1.y;  // Re a0 conj(a1)
+        const double ci = a0.y * a1.x - a0.x * a1.y;  // Im a0 conj(a1)
+        s_cr[(r * 4 + 0) * 16 + tid] = aa;
+        s_cr[(r * 4 + 1) * 16 + tid] = bb;
+        s_cr[(r * 4 + 2) * 16 + tid] = cr;
+        s_cr[(r * 4 + 3) * 16 + tid] = ci;
+        al += aa;
+        be += bb;
+        gr += cr;
+        gi += ci;
+      }
+      s_cj[(j * 4 + 0) * 16 + tid] = al;
+      s_cj[(j * 4 + 1) * 16 + tid] = be;
+      s_cj[(j * 4 + 2) * 16 + tid] = gr;
+      s_cj[(j * 4 + 3) * 16 + tid] = gi;
+    }
+  }
+  __syncthreads();
+
+  double cal[J], cbe[J], cgr[J], cgi[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    cal[j] = s_cj[(j * 4 + 0) * 16 + fl];
+    cbe[j] = s_cj[(j * 4 + 1) * 16 + fl];
+    cgr[j] = s_cj[(j * 4 + 2) * 16 + fl];
+    cgi[j] = s_cj[(j * 4 + 3) * 16 + fl];
+  }
+  const double psd = a.psd[f];
+  const bool fvalid = f < a.F;
+
+  double sn[NP][4], q[J][8], sv[J];
+  double ll = 0.0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sn[p][u] = 0.0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    sv[j] = 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) q[j][u] = 0.0;
+  }
+
+  const int tb = blockIdx.y * a.tpc;
+  const int te = min(tb + a.tpc, a.ntt);
+  const int nks = a.KP >> 2;
+  for (int tt = tb + wv; tt < te; tt += 4) {
+    const int t0 = tt * 16;
+    double c00[4], c11[4], cre[4], cim[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
+      c00[i] = a.cx00[off];
+      c11[i] = a.cx11[off];
+      cre[i] = a.cxr[off];
+      cim[i] = a.cxi[off];
+    }
+    d4 v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      v[j] = d4{0.0, 0.0, 0.0, 0.0};
+      const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+      const double *sw = s_w + (j * a.KP + tq) * 16 + fl;
+      for (int s = 0; s < nks; ++s)
+        v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], sw[4 * s * 16], v[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 4 * i;
+      double V[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) V[j] = v[j][i];
+      double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        d0 += cal[j] * V[j];
+        d1 += cbe[j] * V[j];
+        ore += cgr[j] * V[j];
+        oim += cgi[j] * V[j];
+      }
+      // inv_herm_mat_2d (signalTools.py:177-194)
+      double det = d0 * d1 - (ore * ore + oim * oim);
+      const double dg = det + kEps;
+      const double sg = dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0);
+      det = sg * fmax(fabs(det), kEps);
+      const double rd = 1.0 / det;
+      const double i0 = d1 * rd, i1 = d0 * rd, ior = -ore * rd, ioi = -oim * rd;
+      const double x00 = c00[i], x11 = c11[i], xr = cre[i], xi = cim[i];
+      if (fvalid && t < a.T)
+        ll += log(det * M_PI) + i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
+      // P = Cx S
+      const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
+      const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
+      const double p10r = xr * i0 + x11 * ior, p10i = -xi * i0 - x11 * ioi;
+      const double p11r = xr * ior + xi * ioi + x11 * i1, p11i = xr * ioi - xi * ior;
+      // N = S Cx S - S = P^H S - S
+      const double n00 = p00r * i0 + (p10r * ior - p10i * ioi) - i0;
+      const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
+      const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
+      const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
+      int p = 0;
+#pragma unroll
+      for (int j1 = 0; j1 < J; ++j1) {
+#pragma unroll
+        for (int j2 = j1; j2 < J; ++j2, ++p) {
+          const double vv = V[j1] * V[j2];
+          sn[p][0] += vv * n00;
+          sn[p][1] += vv * n11;
+          sn[p][2] += vv * n01r;
+          sn[p][3] += vv * n01i;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        q[j][0] += V[j] * p00r;
+        q[j][1] += V[j] * p00i;
+        q[j][2] += V[j] * p01r;
+        q[j][3] += V[j] * p01i;
+        q[j][4] += V[j] * p10r;
+        q[j][5] += V[j] * p10i;
+        q[j][6] += V[j] * p11r;
+        q[j][7] += V[j] * p11i;
+        sv[j] += V[j];
+      }
+      // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414)
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        double acc = 0.0;
+        const double v2 = V[j] * V[j];
+        for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
+          const double qa = s_cr[(r * 4 + 0) * 16 + fl] * n00 + s_cr[(r * 4 + 1) * 16 + fl] * n11 +
+                            2.0 * (s_cr[(r * 4 + 2) * 16 + fl] * n01r +
+                                   s_cr[(r * 4 + 3) * 16 + fl] * n01i);
+          acc += fabs(v2 * qa + V[j]);
+        }
+        a.hatW[((size_t)j * a.Tp + t) * a.Fp + f] = acc / (double)(a.roff[j + 1] - a.roff[j]);
+      }
+    }
+  }
+
+  // reduce the 4 lanes sharing a bin, then the 4 waves, then write the chunk partial
+  __syncthreads();  // s_red aliases s_w: every wave must be done with its last tile
+  double *red = s_red + wv * NACC * 16;
+  auto put = [&](int idx, double x) {
+    x += __shfl_xor(x, 16, 64);
+    x += __shfl_xor(x, 32, 64);
+    if (tq == 0) red[idx * 16 + fl] = x;
+  };
+  {
+    int idx = 0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) put(idx++, sn[p][u]);
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) put(idx++, q[j][u]);
+#pragma unroll
+    for (int j = 0; j < J; ++j) put(idx++, sv[j]);
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) ll += __shfl_xor(ll, m, 64);
+  if (lane == 0) s_ll[wv] = ll;
+  __syncthreads();
+  for (int idx = tid; idx < NACC * 16; idx += 256) {
+    const int u = idx >> 4, ff = idx & 15;
+    const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
+                     s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
+    a.part[((size_t)blockIdx.y * a.Fp + f0 + ff) * NACC + u] = x;
+  }
+  if (tid == 0) a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+}
+
+__global__ void k_loglik(const double *__restrict__ llpart, int n, double *__restrict__ out,
+                         double inv_FT) {
+  __shared__ double s[256];
+  double x = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) x += llpart[i];
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = -(s[0] * inv_FT);
+}
+
+// ---------------------------------------------------------------- mixing
+struct MArgs {
+  const double *part;  // [nchunk][Fp][NACC]
+  double2 *A;          // [R][2][Fp]
+  double2 *rss, *rxs;  // inst: [Fp][R][R], [Fp][2][R]
+  int *flags;
+  int F, Fp, J, R, nchunk, nacc, conv_update;
+  double invT;
+  int jr[kMaxR];
+};
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) {
+  return make_double2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ double2 csub(double2 a, double2 b) {
+  return make_double2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ double2 cscale(double2 a, double s) {
+  return make_double2(a.x * s, a.y * s);
+}
+__device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
+  // Smith's algorithm (as the C99 / numpy complex division)
+  if (fabs(b.x) >= fabs(b.y)) {
+    const double r = b.y / b.x, d = b.x + b.y * r;
+    return make_double2((a.x + a.y * r) / d, (a.y - a.x * r) / d);
+  }
+  const double r = b.x / b.y, d = b.x * r + b.y;
+  return make_double2((a.x * r + a.y) / d, (a.y * r - a.x) / d);
+}
+
+// One thread per bin: sufficient statistics -> hat_Rss, hat_Rxs (:698-755),
+// then for 'conv' the per-bin LAPACK-style solve of hat_Rss^T X = hat_Rxs^T
+// (:854-863); for 'inst' the per-bin statistics are stored for k_mix_inst.
+__global__ void k_mix(const MArgs a) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= a.F) return;
+  const int J = a.J, R = a.R, NACC = a.nacc;
+  const int NP = J * (J + 1) / 2;
+  double acc[4 * 10 + 9 * kMaxJ];
+  for (int u = 0; u < NACC; ++u) acc[u] = 0.0;
+  for (int c = 0; c < a.nchunk; ++c) {
+    const double *src = a.part + ((size_t)c * a.Fp + f) * NACC;
+    for (int u = 0; u < NACC; ++u) acc[u] += src[u];
+  }
+  double2 Am[kMaxR][2];
+  for (int r = 0; r < R; ++r) {
+    Am[r][0] = a.A[(size_t)(2 * r) * a.Fp + f];
+    Am[r][1] = a.A[(size_t)(2 * r + 1) * a.Fp + f];
+  }
+  double2 M[kMaxR][kMaxR];
+  for (int r1 = 0; r1 < R; ++r1) {
+    for (int r2 = 0; r2 < R; ++r2) {
+      int j1 = a.jr[r1], j2 = a.jr[r2];
+      const int lo = min(j1, j2), hi = max(j1, j2);
+      const int p = lo * J - lo * (lo - 1) / 2 + (hi - lo);
+      const double n00 = acc[4 * p], n11 = acc[4 * p + 1];
+      const double2 n01 = make_double2(acc[4 * p + 2], acc[4 * p + 3]);
+      // a_r1^H Nsum a_r2
+      const double2 c10 = cconj(Am[r1][0]), c11 = cconj(Am[r1][1]);
+      double2 v = cscale(cmul(c10, Am[r2][0]), n00);
+      v = cadd(v, cmul(cmul(c10, n01), Am[r2][1]));
+      v = cadd(v, cmul(cmul(c11, cconj(n01)), Am[r2][0]));
+      v = cadd(v, cscale(cmul(c11, Am[r2][1]), n11));
+      v = cscale(v, a.invT);
+      if (r1 == r2) v.x += acc[4 * NP + 8 * J + j1] * a.invT;
+      M[r1][r2] = v;
+    }
+  }
+  // hermitise (:734-740)
+  for (int r1 = 0; r1 < R; ++r1)
+    for (int r2 = r1; r2 < R; ++r2) {
+      const double2 x = M[r1][r2], y = M[r2][r1];
+      M[r1][r2] = cscale(cadd(x, cconj(y)), 0.5);
+      M[r2][r1] = cscale(cadd(y, cconj(x)), 0.5);
+    }
+  double2 B[kMaxR][2];  // hat_Rxs^T
+  for (int r = 0; r < R; ++r) {
+    const double *qq = acc + 4 * NP + 8 * a.jr[r];
+    for (int c = 0; c < 2; ++c) {
+      const double2 q0 = make_double2(qq[4 * c + 0], qq[4 * c + 1]);
+      const double2 q1 = make_double2(qq[4 * c + 2], qq[4 * c + 3]);
+      B[r][c] = cscale(cadd(cmul(q0, Am[r][0]), cmul(q1, Am[r][1])), a.invT);
+    }
+  }
+  if (!a.conv_update) {
+    if (a.rss) {
+      for (int r1 = 0; r1 < R; ++r1)
+        for (int r2 = 0; r2 < R; ++r2) a.rss[((size_t)f * R + r1) * R + r2] = M[r1][r2];
+      for (int c = 0; c < 2; ++c)
+        for (int r = 0; r < R; ++r) a.rxs[((size_t)f * 2 + c) * R + r] = B[r][c];
+    }
+    return;
+  }
+  // solve M^T X = B (LU with partial pivoting on |re|+|im|, as LAPACK zgesv)
+  double2 L[kMaxR][kMaxR];
+  for (int r1 = 0; r1 < R; ++r1)
+    for (int r2 = 0; r2 < R; ++r2) L[r1][r2] = M[r2][r1];
+  for (int k = 0; k < R; ++k) {
+    int piv = k;
+    double best = fabs(L[k][k].x) + fabs(L[k][k].y);
+    for (int i = k + 1; i < R; ++i) {
+      const double m = fabs(L[i][k].x) + fabs(L[i][k].y);
+      if (m > best) {
+        best = m;
+        piv = i;
+      }
+    }
+    if (best == 0.0) {
+      atomicOr(a.flags, 1);
+      return;
+    }
+    if (piv != k) {
+      for (int c = 0; c < R; ++c) {
+        const double2 tmp = L[k][c];
+        L[k][c] = L[piv][c];
+        L[piv][c] = tmp;
+      }
+      for (int c = 0; c < 2; ++c) {
+        const double2 tmp = B[k][c];
+        B[k][c] = B[piv][c];
+        B[piv][c] = tmp;
+      }
+    }
+    const double2 rinv = cdiv(make_double2(1.0, 0.0), L[k][k]);
+    for (int i = k + 1; i < R; ++i) {
+      const double2 l = cmul(L[i][k], rinv);
+      for (int c = k + 1; c < R; ++c) L[i][c] = csub(L[i][c], cmul(l, L[k][c]));
+      for (int c = 0; c < 2; ++c) B[i][c] = csub(B[i][c], cmul(l, B[k][c]));
+    }
+  }
+  for (int i = R - 1; i >= 0; --i) {
+    for (int c = 0; c < 2; ++c) {
+      double2 x = B[i][c];
+      for (int q = i + 1; q < R; ++q) x = csub(x, cmul(L[i][q], B[q][c]));
+      B[i][c] = cdiv(x, L[i][i]);
+    }
+  }
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < 2; ++c) a.A[(size_t)(2 * r + c) * a.Fp + f] = B[r][c];
+}
+
+// 'inst' update (:808-839): f-means of the statistics, real R_u x R_u solve.
+struct IArgs {
+  const double2 *rss, *rxs, *A;
+  double2 *Pinst;
+  int *flags;
+  int F, Fp, R, nu, no;
+  int upd[kMaxR], oth[kMaxR];
+};
+__global__ void k_mix_inst(const IArgs a) {
+  __shared__ double s_b[kMaxR][2];
+  __shared__ double s_m[kMaxR][kMaxR];
+  const int nu = a.nu, R = a.R;
+  const int tid = threadIdx.x;
+  const int nb = 2 * nu, nm = nu * nu;
+  if (tid < nb + nm) {
+    double s = 0.0;
+    if (tid < nb) {
+      const int c = tid / nu, u = tid % nu, ru = a.upd[u];
+      for (int f = 0; f < a.F; ++f) {
+        double2 x = a.rxs[((size_t)f * 2 + c) * R + ru];
+        for (int o = 0; o < a.no; ++o) {
+          const int ro = a.oth[o];
+          x = csub(x, cmul(a.A[(size_t)(2 * ro + c) * a.Fp + f], a.rss[((size_t)f * R + ro) * R + ru]));
+        }
+        s += x.x;
+      }
+      s_b[u][c] = s / a.F;
+    } else {
+      const int e = tid - nb, u1 = e / nu, u2 = e % nu;
+      for (int f = 0; f < a.F; ++f) s += a.rss[((size_t)f * R + a.upd[u1]) * R + a.upd[u2]].x;
+      s_m[u1][u2] = s / a.F;
+    }
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double Lm[kMaxR][kMaxR], B[kMaxR][2];
+  for (int i = 0; i < nu; ++i) {
+    for (int k = 0; k < nu; ++k) Lm[i][k] = s_m[k][i];  // rm^T
+    B[i][0] = s_b[i][0];
+    B[i][1] = s_b[i][1];
+  }
+  for (int k = 0; k < nu; ++k) {
+    int piv = k;
+    double best = fabs(Lm[k][k]);
+    for (int i = k + 1; i < nu; ++i)
+      if (fabs(Lm[i][k]) > best) {
+        best = fabs(Lm[i][k]);
+        piv = i;
+      }
+    if (best == 0.0) {
+      atomicOr(a.flags, 1);
+      return;
+    }
+    if (piv != k) {
+      for (int c = 0; c < nu; ++c) {
+        const double t = Lm[k][c];
+        Lm[k][c] = Lm[piv][c];
+        Lm[piv][c] = t;
+      }
+      for (int c = 0; c < 2; ++c) {
+        const double t = B[k][c];
+        B[k][c] = B[piv][c];
+        B[piv][c] = t;
+      }
+    }
+    const double rinv = 1.0 / Lm[k][k];
+    for (int i = k + 1; i < nu; ++i) {
+      const double l = Lm[i][k] * rinv;
+      for (int c = k + 1; c < nu; ++c) Lm[i][c] -= l * Lm[k][c];
+      for (int c = 0; c < 2; ++c) B[i][c] -= l * B[k][c];
+    }
+  }
+  for (int i = nu - 1; i >= 0; --i)
+    for (int c = 0; c < 2; ++c) {
+      double x = B[i][c];
+      for (int q = i + 1; q < nu; ++q) x -= Lm[i][q] * B[q][c];
+      B[i][c] = x / Lm[i][i];
+    }
+  for (int u = 0; u < nu; ++u)
+    for (int c = 0; c < 2; ++c) a.Pinst[a.upd[u] * 2 + c] = make_double2(B[u][c], 0.0);
+}
+
+// ---------------------------------------------------------------- FB update
+struct BArgs {
+  const double *TW, *Wkf, *FWHt, *hatW;
+  double *bnum, *bden;  // [nchunk][J][Fp][KP]
+  int F, T, Fp, Tp, KP, J, ntt, tpc;
+};
+
+// One wave per (bin tile, source, frame chunk):
+//   num[f][k] = sum_t hat_W/V^2 * V * (FW.H)^T[t][k],  den = sum_t V/V * (FW.H)^T
+// (single-factor N1 quirk: other_fact_power == V, audioModel.py:1511-1520).
+template <int NKC>
+__global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int f0 = blockIdx.x * 16, j = blockIdx.y;
+  const int f = f0 + fl;
+  d4 num[NKC], den[NKC];
+#pragma unroll
+  for (int kc = 0; kc < NKC; ++kc) num[kc] = den[kc] = d4{0.0, 0.0, 0.0, 0.0};
+  const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
+  const int nks = a.KP >> 2;
+  const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
+  const double *hw = a.hatW + (size_t)j * a.Tp * a.Fp + f;
+  const double *fwh = a.FWHt + (size_t)j * a.Tp * a.KP + fl;
+  for (int tt = tb; tt < te; ++tt) {
+    const int t0 = tt * 16;
+    d4 v = d4{0.0, 0.0, 0.0, 0.0};
+    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+    for (int s = 0; s < nks; ++s) v = mfma4(tw[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v);
+    double r1[4], r2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 4 * i;
+      const double h = hw[(size_t)t * a.Fp];
+      const double vm = fmax(v[i], kEps);
+      const double rv = 1.0 / vm;
+      const bool ok = t < a.T;
+      r1[i] = ok ? (h * (rv * rv)) * vm : 0.0;
+      r2[i] = ok ? vm * rv : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double *b = fwh + (size_t)(t0 + 4 * i + tq) * a.KP;
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) {
+        const double bb = b[kc * 16];
+        num[kc] = mfma4(r1[i], bb, num[kc]);
+        den[kc] = mfma4(r2[i], bb, den[kc]);
+      }
+    }
+  }
+  const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Fp;
+#pragma unroll
+  for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const size_t o = (base + f0 + tq + 4 * m) * a.KP + kc * 16 + fl;
+      a.bnum[o] = num[kc][m];
+      a.bden[o] = den[kc][m];
+    }
+}
+
+struct UArgs {
+  double *FB;
+  const double *FW, *bnum, *bden;
+  double *Wkf_new, *Wfk_new;
+  int F, Fp, KP, J, nchunk;
+  double omega;
+  int K[kMaxJ], fb_free[kMaxJ];
+};
+__global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double s_fb[];  // [16][KP]
+  const int f0 = blockIdx.x * 16, j = blockIdx.y;
+  const int KP = a.KP;
+  for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+    const int fl = idx / KP, k = idx % KP, f = f0 + fl;
+    const size_t o = ((size_t)j * a.Fp + f) * KP + k;
+    double fb = a.FB[o];
+    if (a.fb_free[j] && f < a.F && k < a.K[j]) {
+      double num = 0.0, den = 0.0;
+      for (int c = 0; c < a.nchunk; ++c) {
+        const size_t po = (((size_t)c * a.J + j) * a.Fp + f) * KP + k;
+        num += a.bnum[po];
+        den += a.bden[po];
+      }
+      const double ratio = num / fmax(den, kEps);
+      fb *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
+      a.FB[o] = fb;
+    }
+    s_fb[idx] = fb;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+    const int fl = idx / KP, k = idx % KP, f = f0 + fl;
+    const double *fw = a.FW + (size_t)j * KP * KP + k;
+    double s = 0.0;
+    for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * fw[(size_t)q * KP];
+    a.Wkf_new[((size_t)j * KP + k) * a.Fp + f] = s;
+    a.Wfk_new[((size_t)j * a.Fp + f) * KP + k] = s;
+  }
+}
+
+// ---------------------------------------------------------------- TW update
+struct TArgs {
+  double *TW;
+  const double *Wkf_old, *Wkf_new, *Wfk_new, *hatW;
+  int F, T, Fp, Tp, KP, nft;
+  double omega;
+  int K[kMaxJ], tw_free[kMaxJ];
+};
+
+// One wave per (frame tile, source), looping over all bins:
+//   num[k][t] = sum_f W_new[f][k] * V_old * hat_W / V_new^2,
+//   den[k][t] = sum_f W_new[f][k] * V_old / V_new            (:1694-1726)
+template <int NKC>
+__global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int t0 = blockIdx.x * 16, j = blockIdx.y;
+  const int t = t0 + fl;
+  const int nks = a.KP >> 2;
+  double bt[kMaxKP / 4];
+  {
+    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+#pragma unroll
+    for (int s = 0; s < kMaxKP / 4; ++s) bt[s] = s < nks ? tw[(size_t)(4 * s) * a.Tp] : 0.0;
+  }
+  d4 num[NKC], den[NKC];
+#pragma unroll
+  for (int kc = 0; kc < NKC; ++kc) num[kc] = den[kc] = d4{0.0, 0.0, 0.0, 0.0};
+  const double *wo = a.Wkf_old + ((size_t)j * a.KP + tq) * a.Fp + fl;
+  const double *wn = a.Wkf_new + ((size_t)j * a.KP + tq) * a.Fp + fl;
+  const double *hw = a.hatW + ((size_t)j * a.Tp + t) * a.Fp;
+  const double *wfk = a.Wfk_new + (size_t)j * a.Fp * a.KP + fl;
+  const bool tok = t < a.T;
+  for (int ft = 0; ft < a.nft; ++ft) {
+    const int f0 = ft * 16;
+    d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
+#pragma unroll
+    for (int s = 0; s < kMaxKP / 4; ++s) {
+      if (s < nks) {
+        vo = mfma4(wo[(size_t)(4 * s) * a.Fp + f0], bt[s], vo);
+        vn = mfma4(wn[(size_t)(4 * s) * a.Fp + f0], bt[s], vn);
+      }
+    }
+    double r3[4], r4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + tq + 4 * i;
+      const double h = hw[f];
+      const double other = fmax(vo[i], kEps);
+      const double vm = fmax(vn[i], kEps);
+      const double rv = 1.0 / vm;
+      const bool ok = tok && f < a.F;
+      r3[i] = ok ? other * (h * (rv * rv)) : 0.0;
+      r4[i] = ok ? other * rv : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double *b = wfk + (size_t)(f0 + 4 * i + tq) * a.KP;
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) {
+        const double bb = b[kc * 16];
+        num[kc] = mfma4(r3[i], bb, num[kc]);
+        den[kc] = mfma4(r4[i], bb, den[kc]);
+      }
+    }
+  }
+  if (!a.tw_free[j]) return;
+#pragma unroll
+  for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int tt = t0 + tq + 4 * m, k = kc * 16 + fl;
+      if (tt < a.T && k < a.K[j]) {
+        const double ratio = num[kc][m] / fmax(den[kc][m], kEps);
+        double *p = a.TW + ((size_t)j * a.KP + k) * a.Tp + tt;
+        *p *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
+      }
+    }
+}
+
+// ---------------------------------------------------------------- renormalize
+struct RArgs {
+  double2 *A, *Pinst;
+  double *FB, *FW, *TW;
+  int *flags;
+  int F, T, Fp, Tp, KP, conv;
+  int K[kMaxJ], roff[kMaxJ + 1];
+};
+
+__device__ double block_sum(double x, double *s) {
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double r = s[0];
+  __syncthreads();
+  return r;
+}
+
+// One 1024-thread block per source (audioModel.py:1991-2037).
+__global__ __launch_bounds__(1024) void k_renorm(const RArgs a) {
+  __shared__ double s_red[1024];
+  __shared__ double s_w[kMaxKP];
+  const int j = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+  const int K = a.K[j], KP = a.KP;
+  // spatial energy: mean |params|^2
+  double e = 0.0;
+  if (a.conv) {
+    const int n = nr * 2 * a.F;
+    for (int idx = tid; idx < n; idx += nt) {
+      const int f = idx % a.F, rc = idx / a.F;
+      const double2 x = a.A[(size_t)(2 * r0 + rc) * a.Fp + f];
+      e += x.x * x.x + x.y * x.y;
+    }
+    e = block_sum(e, s_red) / (double)n;
+  } else {
+    for (int idx = tid; idx < nr * 2; idx += nt) {
+      const double2 x = a.Pinst[2 * r0 + idx];
+      e += x.x * x.x + x.y * x.y;
+    }
+    e = block_sum(e, s_red) / (double)(nr * 2);
+  }
+  const double se = sqrt(e);
+  if (a.conv) {
+    const int n = nr * 2 * a.F;
+    for (int idx = tid; idx < n; idx += nt) {
+      const int f = idx % a.F, rc = idx / a.F;
+      double2 *p = a.A + (size_t)(2 * r0 + rc) * a.Fp + f;
+      *p = make_double2(p->x / se, p->y / se);
+    }
+  } else if (tid < nr * 2) {
+    double2 *p = a.Pinst + 2 * r0 + tid;
+    *p = make_double2(p->x / se, p->y / se);
+  }
+  // FB *= e ; w = max_f FB ; FB /= w ; FW *= w[:,None]
+  double *FB = a.FB + (size_t)j * a.Fp * KP;
+  const int groups = nt / KP;
+  {
+    const int k = tid % KP, g = tid / KP;
+    double m = -INFINITY;
+    if (g < groups && k < K)
+      for (int f = g; f < a.F; f += groups) {
+        double *p = FB + (size_t)f * KP + k;
+        const double x = *p * e;
+        *p = x;
+        m = fmax(m, x);
+      }
+    s_red[tid] = m;
+  }
+  __syncthreads();
+  if (tid < K) {
+    double m = -INFINITY;
+    for (int g = 0; g < groups; ++g) m = fmax(m, s_red[g * KP + tid]);
+    s_w[tid] = m == 0.0 ? 1.0 : m;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < a.F * K; idx += nt) {
+    const int f = idx / K, k = idx % K;
+    FB[(size_t)f * KP + k] /= s_w[k];
+  }
+  double *FW = a.FW + (size_t)j * KP * KP;
+  for (int idx = tid; idx < K * K; idx += nt) {
+    const int r = idx / K, c = idx % K;
+    FW[r * KP + c] *= s_w[r];
+  }
+  __syncthreads();
+  // w2 = FW.mean(axis=0) ; FW /= w2 ; TW *= w2[:,None]
+  if (tid < K) {
+    double s = 0.0;
+    for (int r = 0; r < K; ++r) s += FW[r * KP + tid];
+    s /= (double)K;
+    s_w[tid] = s == 0.0 ? 1.0 : s;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < K * K; idx += nt) {
+    const int r = idx / K, c = idx % K;
+    FW[r * KP + c] /= s_w[c];
+  }
+  double *TW = a.TW + (size_t)j * KP * a.Tp;
+  double tsum = 0.0;
+  for (int idx = tid; idx < K * a.T; idx += nt) {
+    const int k = idx / a.T, t = idx % a.T;
+    double *p = TW + (size_t)k * a.Tp + t;
+    const double x = *p * s_w[k];
+    *p = x;
+    tsum += x;
+  }
+  tsum = block_sum(tsum, s_red);
+  if (tid == 0) a.flags[1 + j] = tsum < kEps ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- host side
+enum KernelId {
+  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN
+};
+static const char *kKernelNames[fasst_ctx::kNK] = {
+    "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep", "k_loglik", "k_mix",
+    "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm"};
+
+static inline void prof_begin(fasst_ctx *c, int id) {
+  if (c->prof) {
+    (void)hipEventRecord(c->ev0[id], c->stream);
+    c->used[id] = 1;
+  }
+}
+static inline void prof_end(fasst_ctx *c, int id) {
+  if (c->prof) (void)hipEventRecord(c->ev1[id], c->stream);
+}
+// after a stream sync: fold the recorded event pairs into the averages
+static void prof_collect(fasst_ctx *c) {
+  if (!c->prof) return;
+  for (int i = 0; i < fasst_ctx::kNK; ++i) {
+    if (!c->used[i]) continue;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0[i], c->ev1[i]) == hipSuccess) {
+      c->prof_ms[i] += ms;
+      c->prof_cnt[i] += 1;
+    }
+    c->used[i] = 0;
+  }
+}
+
+static int launch_grid(size_t n, int block = 256) {
+  size_t g = (n + block - 1) / block;
+  if (g > 8192) g = 8192;
+  return (int)(g ? g : 1);
+}
+
+int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv) {
+  if (J < 1 || J > kMaxJ) {
+    set_error("J=%d outside the HIP path (1..%d sources)", J, kMaxJ);
+    return FASST_ERR_UNSUPPORTED;
+  }
+  int R = 0, kmax = 0;
+  for (int j = 0; j < J; ++j) {
+    if (rank[j] < 1 || K[j] < 1) {
+      set_error("bad rank/K for source %d", j);
+      return FASST_ERR_SHAPE;
+    }
+    R += rank[j];
+    kmax = std::max(kmax, K[j]);
+  }
+  if (R > kMaxR || kmax > kMaxKP) {
+    set_error("total rank %d (max %d) / K %d (max %d) outside the HIP path", R, kMaxR, kmax,
+              kMaxKP);
+    return FASST_ERR_UNSUPPORTED;
+  }
+  c->J = J;
+  c->R = R;
+  c->conv = conv;
+  c->KP = round_up(kmax, 16);
+  c->roff[0] = 0;
+  for (int j = 0; j < J; ++j) {
+    c->rank[j] = rank[j];
+    c->K[j] = K[j];
+    c->roff[j + 1] = c->roff[j] + rank[j];
+    c->spat_free[j] = c->fb_free[j] = c->tw_free[j] = 1;
+  }
+  const int Fp = c->Fp, Tp = c->Tp, KP = c->KP;
+  // E-step chunks: enough blocks to cover the chip (>= ~4 blocks per CU)
+  c->tpc_e = std::max(4, (c->ntt + 7) / 8);
+  while (c->tpc_e > 4 && (size_t)c->nft * ((c->ntt + c->tpc_e - 1) / c->tpc_e) < 1024) c->tpc_e /= 2;
+  c->nchunk_e = (c->ntt + c->tpc_e - 1) / c->tpc_e;
+  c->tpc_b = std::max(1, (c->ntt + 3) / 4);
+  while (c->tpc_b > 8 && (size_t)c->nft * J * ((c->ntt + c->tpc_b - 1) / c->tpc_b) < 2048)
+    c->tpc_b /= 2;
+  c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
+  const int NP = J * (J + 1) / 2;
+  c->nacc = 4 * NP + 9 * J;
+  int st;
+#define ALLOC(buf, n) \
+  if ((st = c->buf.alloc(n)) != FASST_OK) return st
+  ALLOC(FB, (size_t)J * Fp * KP);
+  ALLOC(FW, (size_t)J * KP * KP);
+  ALLOC(TW, (size_t)J * KP * Tp);
+  ALLOC(Wkf, (size_t)J * KP * Fp);
+  ALLOC(Wkf_new, (size_t)J * KP * Fp);
+  ALLOC(Wfk_new, (size_t)J * Fp * KP);
+  ALLOC(FWHt, (size_t)J * Tp * KP);
+  ALLOC(hatW, (size_t)J * Tp * Fp);
+  ALLOC(A, (size_t)R * 2 * Fp);
+  ALLOC(Pinst, (size_t)R * 2);
+  ALLOC(epart, (size_t)c->nchunk_e * Fp * c->nacc);
+  ALLOC(llpart, (size_t)c->nchunk_e * c->nft);
+  ALLOC(bnum, (size_t)c->nchunk_b * J * Fp * KP);
+  ALLOC(bden, (size_t)c->nchunk_b * J * Fp * KP);
+  ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
+  ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
+  ALLOC(flags, 1 + kMaxJ);
+#undef ALLOC
+  c->configured = 1;
+  return FASST_OK;
+}
+
+int build_inst_A(fasst_ctx *c) {
+  if (c->conv) return FASST_OK;
+  prof_begin(c, KINSTA);
+  k_inst_A<<<launch_grid((size_t)c->R * 2 * c->Fp), 256, 0, c->stream>>>(c->Pinst.p, c->A.p, c->R,
+                                                                        c->F, c->Fp);
+  prof_end(c, KINSTA);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+int launch_w_old(fasst_ctx *c) {
+  prof_begin(c, KW);
+  k_w_from_fb<<<launch_grid((size_t)c->J * c->Fp * c->KP), 256, 0, c->stream>>>(
+      c->FB.p, c->FW.p, c->Wkf.p, nullptr, c->J, c->Fp, c->KP);
+  prof_end(c, KW);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+static int launch_renorm(fasst_ctx *c) {
+  RArgs r;
+  r.A = c->A.p;
+  r.Pinst = c->Pinst.p;
+  r.FB = c->FB.p;
+  r.FW = c->FW.p;
+  r.TW = c->TW.p;
+  r.flags = c->flags.p;
+  r.F = c->F;
+  r.T = c->T;
+  r.Fp = c->Fp;
+  r.Tp = c->Tp;
+  r.KP = c->KP;
+  r.conv = c->conv;
+  for (int j = 0; j < kMaxJ; ++j) r.K[j] = j < c->J ? c->K[j] : 0;
+  for (int j = 0; j <= kMaxJ; ++j) r.roff[j] = j <= c->J ? c->roff[j] : c->R;
+  prof_begin(c, KREN);
+  k_renorm<<<c->J, 1024, 0, c->stream>>>(r);
+  prof_end(c, KREN);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+template <int J>
+static void launch_estep(fasst_ctx *c, const EArgs &e) {
+  const size_t smem =
+      (size_t)(kMaxR * 4 * 16 + J * 4 * 16 + 4 +
+               std::max(J * c->KP * 16, 4 * (4 * (J * (J + 1) / 2) + 9 * J) * 16)) *
+      sizeof(double);
+  dim3 grid(c->nft, c->nchunk_e);
+  prof_begin(c, KESTEP);
+  k_estep<J><<<grid, 256, smem, c->stream>>>(e);
+  prof_end(c, KESTEP);
+}
+
+template <int NKC>
+static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb) {
+  if (fb) {
+    prof_begin(c, KFBC);
+    k_fb_contract<NKC><<<dim3(c->nft, c->J, c->nchunk_b), 64, 0, c->stream>>>(b);
+    prof_end(c, KFBC);
+  } else {
+    prof_begin(c, KTWC);
+    k_tw_contract<NKC><<<dim3(c->ntt, c->J), 64, 0, c->stream>>>(t);
+    prof_end(c, KTWC);
+  }
+}
+
+// One GEM iteration, all launches asynchronous on c->stream.
+static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega) {
+  const int J = c->J;
+  int st = launch_w_old(c);
+  if (st) return st;
+  prof_begin(c, KFWH);
+  k_fwh_t<<<launch_grid((size_t)J * c->Tp * c->KP), 256, 0, c->stream>>>(c->FW.p, c->TW.p,
+                                                                        c->FWHt.p, J, c->Tp, c->KP);
+  prof_end(c, KFWH);
+  st = build_inst_A(c);
+  if (st) return st;
+  EArgs e;
+  e.cx00 = c->cx.p;
+  e.cx11 = c->cx.p + (size_t)c->Tp * c->Fp;
+  e.cxr = c->cx.p + 2 * (size_t)c->Tp * c->Fp;
+  e.cxi = c->cx.p + 3 * (size_t)c->Tp * c->Fp;
+  e.TW = c->TW.p;
+  e.Wkf = c->Wkf.p;
+  e.A = c->A.p;
+  e.psd = psd_dev;
+  e.hatW = c->hatW.p;
+  e.part = c->epart.p;
+  e.llpart = c->llpart.p;
+  e.F = c->F;
+  e.T = c->T;
+  e.Fp = c->Fp;
+  e.Tp = c->Tp;
+  e.KP = c->KP;
+  e.R = c->R;
+  e.ntt = c->ntt;
+  e.tpc = c->tpc_e;
+  e.nft = c->nft;
+  for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
+  switch (J) {
+    case 1: launch_estep<1>(c, e); break;
+    case 2: launch_estep<2>(c, e); break;
+    case 3: launch_estep<3>(c, e); break;
+    default: launch_estep<4>(c, e); break;
+  }
+  FASST_LAUNCH_CHECK();
+  prof_begin(c, KLL);
+  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
+                                     1.0 / ((double)c->F * (double)c->T));
+  prof_end(c, KLL);
+  FASST_LAUNCH_CHECK();
+  // mixing update
+  bool any_free = false, all_free = true;
+  for (int j = 0; j < J; ++j) {
+    any_free |= c->spat_free[j] != 0;
+    all_free &= c->spat_free[j] != 0;
+  }
+  if (any_free) {
+    MArgs m;
+    m.part = c->epart.p;
+    m.A = c->A.p;
+    m.rss = c->rss.p;
+    m.rxs = c->rxs.p;
+    m.flags = c->flags.p;
+    m.F = c->F;
+    m.Fp = c->Fp;
+    m.J = J;
+    m.R = c->R;
+    m.nchunk = c->nchunk_e;
+    m.nacc = c->nacc;
+    m.conv_update = c->conv ? 1 : 0;
+    m.invT = 1.0 / (double)c->T;
+    for (int j = 0; j < J; ++j)
+      for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
+    prof_begin(c, KMIX);
+    k_mix<<<(c->F + 63) / 64, 64, 0, c->stream>>>(m);
+    prof_end(c, KMIX);
+    FASST_LAUNCH_CHECK();
+    if (!c->conv) {
+      IArgs ia;
+      ia.rss = c->rss.p;
+      ia.rxs = c->rxs.p;
+      ia.A = c->A.p;
+      ia.Pinst = c->Pinst.p;
+      ia.flags = c->flags.p;
+      ia.F = c->F;
+      ia.Fp = c->Fp;
+      ia.R = c->R;
+      ia.nu = ia.no = 0;
+      for (int j = 0; j < J; ++j)
+        for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) {
+          if (c->spat_free[j])
+            ia.upd[ia.nu++] = r;
+          else
+            ia.oth[ia.no++] = r;
+        }
+      prof_begin(c, KMIXI);
+      k_mix_inst<<<1, 256, 0, c->stream>>>(ia);
+      prof_end(c, KMIXI);
+      FASST_LAUNCH_CHECK();
+    }
+  }
+  (void)all_free;
+  // spectral update: FB then TW (one NMF factor per source)
+  BArgs b;
+  b.TW = c->TW.p;
+  b.Wkf = c->Wkf.p;
+  b.FWHt = c->FWHt.p;
+  b.hatW = c->hatW.p;
+  b.bnum = c->bnum.p;
+  b.bden = c->bden.p;
+  b.F = c->F;
+  b.T = c->T;
+  b.Fp = c->Fp;
+  b.Tp = c->Tp;
+  b.KP = c->KP;
+  b.J = J;
+  b.ntt = c->ntt;
+  b.tpc = c->tpc_b;
+  TArgs t;
+  t.TW = c->TW.p;
+  t.Wkf_old = c->Wkf.p;
+  t.Wkf_new = c->Wkf_new.p;
+  t.Wfk_new = c->Wfk_new.p;
+  t.hatW = c->hatW.p;
+  t.F = c->F;
+  t.T = c->T;
+  t.Fp = c->Fp;
+  t.Tp = c->Tp;
+  t.KP = c->KP;
+  t.nft = c->nft;
+  t.omega = omega;
+  UArgs u;
+  u.FB = c->FB.p;
+  u.FW = c->FW.p;
+  u.bnum = c->bnum.p;
+  u.bden = c->bden.p;
+  u.Wkf_new = c->Wkf_new.p;
+  u.Wfk_new = c->Wfk_new.p;
+  u.F = c->F;
+  u.Fp = c->Fp;
+  u.KP = c->KP;
+  u.J = J;
+  u.nchunk = c->nchunk_b;
+  u.omega = omega;
+  for (int j = 0; j < kMaxJ; ++j) {
+    const bool in = j < J;
+    t.K[j] = u.K[j] = in ? c->K[j] : 0;
+    t.tw_free[j] = in ? c->tw_free[j] : 0;
+    u.fb_free[j] = in ? c->fb_free[j] : 0;
+  }
+  const int nkc = c->KP / 16;
+  switch (nkc) {
+    case 1: launch_contract<1>(c, b, t, true); break;
+    case 2: launch_contract<2>(c, b, t, true); break;
+    case 3: launch_contract<3>(c, b, t, true); break;
+    default: launch_contract<4>(c, b, t, true); break;
+  }
+  FASST_LAUNCH_CHECK();
+  prof_begin(c, KFBU);
+  k_fb_update<<<dim3(c->nft, J), 256, 16 * c->KP * sizeof(double), c->stream>>>(u);
+  prof_end(c, KFBU);
+  FASST_LAUNCH_CHECK();
+  switch (nkc) {
+    case 1: launch_contract<1>(c, b, t, false); break;
+    case 2: launch_contract<2>(c, b, t, false); break;
+    case 3: launch_contract<3>(c, b, t, false); break;
+    default: launch_contract<4>(c, b, t, false); break;
+  }
+  FASST_LAUNCH_CHECK();
+  return launch_renorm(c);
+}
+
+}  // namespace fasst
+
+using namespace fasst;
+
+// ============================================================================ C ABI
+extern "C" {
+
+const char *fasst_last_error(void) { return fasst::g_err.c_str(); }
+
+int fasst_device_count(int *n) {
+  FASST_HIP(hipGetDeviceCount(n));
+  return FASST_OK;
+}
+
+int fasst_create(int device, int F, int T, fasst_ctx **out) {
+  if (!out || F < 1 || T < 1) {
+    set_error("fasst_create: bad arguments F=%d T=%d", F, T);
+    return FASST_ERR_SHAPE;
+  }
+  int ndev = 0;
+  FASST_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) {
+    set_error("fasst_create: device %d not present (%d visible)", device, ndev);
+    return FASST_ERR_DEVICE;
+  }
+  DeviceGuard g(device);
+  fasst_ctx *c = new fasst_ctx();
+  c->device = device;
+  c->F = F;
+  c->T = T;
+  c->Fp = round_up(F, kTile);
+  c->Tp = round_up(T, kTile);
+  c->nft = c->Fp / kTile;
+  c->ntt = c->Tp / kTile;
+  int st = FASST_OK;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    set_error("hipStreamCreate failed");
+    st = FASST_ERR_DEVICE;
+  }
+  if (!st) st = c->cx.alloc((size_t)4 * c->Tp * c->Fp);
+  if (!st && hipHostMalloc((void **)&c->h_flags, (1 + kMaxJ) * sizeof(int)) != hipSuccess)
+    st = FASST_ERR_OOM;
+  if (!st && hipHostMalloc((void **)&c->h_ll, 64 * sizeof(double)) != hipSuccess) st = FASST_ERR_OOM;
+  if (st) {
+    fasst_destroy(c);
+    return st;
+  }
+  *out = c;
+  return FASST_OK;
+}
+
+int fasst_configure(fasst_ctx *c, int J, const int *rank, const int *K, int mix_conv) {
+  if (!c || !rank || !K) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  return configure_model(c, J, rank, K, mix_conv);
+}
+
+int fasst_destroy(fasst_ctx *c) {
+  if (!c) return FASST_OK;
+  {
+    DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->h_flags) (void)hipHostFree(c->h_flags);
+    if (c->h_ll) (void)hipHostFree(c->h_ll);
+    c->cx.release();
+    c->X.release();
+    c->FB.release();
+    c->FW.release();
+    c->TW.release();
+    c->Wkf.release();
+    c->Wkf_new.release();
+    c->Wfk_new.release();
+    c->FWHt.release();
+    c->hatW.release();
+    c->A.release();
+    c->Pinst.release();
+    c->epart.release();
+    c->llpart.release();
+    c->bnum.release();
+    c->bden.release();
+    c->psd.release();
+    c->ll.release();
+    c->rss.release();
+    c->rxs.release();
+    c->flags.release();
+    for (int i = 0; i < fasst_ctx::kNK; ++i) {
+      if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
+      if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+  return FASST_OK;
+}
+
+static int need_model(fasst_ctx *c, int j) {
+  if (!c || !c->configured) {
+    set_error("context not configured");
+    return FASST_ERR_SHAPE;
+  }
+  if (j < 0 || j >= c->J) {
+    set_error("component %d out of range (J=%d)", j, c->J);
+    return FASST_ERR_SHAPE;
+  }
+  return FASST_OK;
+}
+
+int fasst_set_spatial(fasst_ctx *c, int j, const double *params, int free_) {
+  int st = need_model(c, j);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  c->spat_free[j] = free_ ? 1 : 0;
+  const int r0 = c->roff[j], nr = c->rank[j];
+  const double2 *p = reinterpret_cast<const double2 *>(params);
+  if (c->conv) {
+    // params [r][C][F] -> A[r][c][f] (row pitch Fp)
+    FASST_HIP(hipMemcpy2DAsync(c->A.p + (size_t)2 * r0 * c->Fp, c->Fp * sizeof(double2), p,
+                               c->F * sizeof(double2), c->F * sizeof(double2), (size_t)nr * 2,
+                               hipMemcpyHostToDevice, c->stream));
+  } else {
+    // params [C][r] -> Pinst[r][c]
+    std::vector<double2> tmp((size_t)nr * 2);
+    for (int r = 0; r < nr; ++r)
+      for (int ch = 0; ch < 2; ++ch) tmp[(size_t)r * 2 + ch] = p[(size_t)ch * nr + r];
+    FASST_HIP(hipMemcpyAsync(c->Pinst.p + 2 * r0, tmp.data(), tmp.size() * sizeof(double2),
+                             hipMemcpyHostToDevice, c->stream));
+    FASST_HIP(hipStreamSynchronize(c->stream));
+  }
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_get_spatial(fasst_ctx *c, int j, double *params) {
+  int st = need_model(c, j);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  const int r0 = c->roff[j], nr = c->rank[j];
+  double2 *p = reinterpret_cast<double2 *>(params);
+  if (c->conv) {
+    FASST_HIP(hipMemcpy2DAsync(p, c->F * sizeof(double2), c->A.p + (size_t)2 * r0 * c->Fp,
+                               c->Fp * sizeof(double2), c->F * sizeof(double2), (size_t)nr * 2,
+                               hipMemcpyDeviceToHost, c->stream));
+    FASST_HIP(hipStreamSynchronize(c->stream));
+  } else {
+    std::vector<double2> tmp((size_t)nr * 2);
+    FASST_HIP(hipMemcpyAsync(tmp.data(), c->Pinst.p + 2 * r0, tmp.size() * sizeof(double2),
+                             hipMemcpyDeviceToHost, c->stream));
+    FASST_HIP(hipStreamSynchronize(c->stream));
+    for (int r = 0; r < nr; ++r)
+      for (int ch = 0; ch < 2; ++ch) p[(size_t)ch * nr + r] = tmp[(size_t)r * 2 + ch];
+  }
+  return FASST_OK;
+}
+
+int fasst_set_spectral(fasst_ctx *c, int j, const double *FB, const double *FW, const double *TW,
+                       int fb_free, int tw_free) {
+  int st = need_model(c, j);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  const int K = c->K[j], KP = c->KP;
+  c->fb_free[j] = fb_free ? 1 : 0;
+  c->tw_free[j] = tw_free ? 1 : 0;
+  FASST_HIP(hipMemsetAsync(c->FW.p + (size_t)j * KP * KP, 0, (size_t)KP * KP * sizeof(double),
+                           c->stream));
+  FASST_HIP(hipMemcpy2DAsync(c->FB.p + (size_t)j * c->Fp * KP, KP * sizeof(double), FB,
+                             K * sizeof(double), K * sizeof(double), c->F, hipMemcpyHostToDevice,
+                             c->stream));
+  FASST_HIP(hipMemcpy2DAsync(c->FW.p + (size_t)j * KP * KP, KP * sizeof(double), FW,
+                             K * sizeof(double), K * sizeof(double), K, hipMemcpyHostToDevice,
+                             c->stream));
+  FASST_HIP(hipMemcpy2DAsync(c->TW.p + (size_t)j * KP * c->Tp, c->Tp * sizeof(double), TW,
+                             c->T * sizeof(double), c->T * sizeof(double), K,
+                             hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_get_spectral(fasst_ctx *c, int j, double *FB, double *FW, double *TW) {
+  int st = need_model(c, j);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  const int K = c->K[j], KP = c->KP;
+  if (FB)
+    FASST_HIP(hipMemcpy2DAsync(FB, K * sizeof(double), c->FB.p + (size_t)j * c->Fp * KP,
+                               KP * sizeof(double), K * sizeof(double), c->F,
+                               hipMemcpyDeviceToHost, c->stream));
+  if (FW)
+    FASST_HIP(hipMemcpy2DAsync(FW, K * sizeof(double), c->FW.p + (size_t)j * KP * KP,
+                               KP * sizeof(double), K * sizeof(double), K, hipMemcpyDeviceToHost,
+                               c->stream));
+  if (TW)
+    FASST_HIP(hipMemcpy2DAsync(TW, c->T * sizeof(double), c->TW.p + (size_t)j * KP * c->Tp,
+                               c->Tp * sizeof(double), c->T * sizeof(double), K,
+                               hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_renormalize(fasst_ctx *c, int *restart_mask) {
+  int st = need_model(c, 0);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  FASST_HIP(hipMemsetAsync(c->flags.p, 0, (1 + kMaxJ) * sizeof(int), c->stream));
+  st = launch_renorm(c);
+  if (st) return st;
+  FASST_HIP(hipMemcpyAsync(c->h_flags, c->flags.p, (1 + kMaxJ) * sizeof(int),
+                           hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  int mask = 0;
+  for (int j = 0; j < c->J; ++j)
+    if (c->h_flags[1 + j]) mask |= 1 << j;
+  if (restart_mask) *restart_mask = mask;
+  return FASST_OK;
+}
+
+int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double *logliks,
+              int *restart_mask, int *iters_done) {
+  int st = need_model(c, 0);
+  if (st) return st;
+  if (n_iter < 0 || (n_iter > 0 && (!psd || !logliks))) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  if (iters_done) *iters_done = 0;
+  if (restart_mask) *restart_mask = 0;
+  if (n_iter == 0) return FASST_OK;
+  if (c->psd_cap < n_iter) {
+    if ((st = c->psd.alloc((size_t)n_iter * c->Fp))) return st;
+    c->psd_cap = n_iter;
+  }
+  if (c->ll_cap < n_iter) {
+    if ((st = c->ll.alloc(n_iter))) return st;
+    c->ll_cap = n_iter;
+  }
+  FASST_HIP(hipMemsetAsync(c->psd.p, 0, (size_t)n_iter * c->Fp * sizeof(double), c->stream));
+  FASST_HIP(hipMemcpy2DAsync(c->psd.p, c->Fp * sizeof(double), psd, c->F * sizeof(double),
+                             c->F * sizeof(double), n_iter, hipMemcpyHostToDevice, c->stream));
+  for (int it = 0; it < n_iter; ++it) {
+    FASST_HIP(hipMemsetAsync(c->flags.p, 0, (1 + kMaxJ) * sizeof(int), c->stream));
+    st = gem_iteration(c, c->psd.p + (size_t)it * c->Fp, c->ll.p + it, omega);
+    if (st) return st;
+    FASST_HIP(hipMemcpyAsync(c->h_flags, c->flags.p, (1 + kMaxJ) * sizeof(int),
+                             hipMemcpyDeviceToHost, c->stream));
+    FASST_HIP(hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (c->h_flags[0]) {
+      set_error("Singular Matrix");
+      return FASST_ERR_SINGULAR;
+    }
+    int mask = 0;
+    for (int j = 0; j < c->J; ++j)
+      if (c->h_flags[1 + j]) mask |= 1 << j;
+    if (iters_done) *iters_done = it + 1;
+    if (mask) {
+      if (restart_mask) *restart_mask = mask;
+      FASST_HIP(hipMemcpy(logliks, c->ll.p, (size_t)(it + 1) * sizeof(double),
+                          hipMemcpyDeviceToHost));
+      return FASST_TW_RESTART;
+    }
+  }
+  FASST_HIP(hipMemcpyAsync(logliks, c->ll.p, (size_t)n_iter * sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int fasst_set_profiling(fasst_ctx *c, int on) {
+  if (!c) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  if (on && !c->ev0[0])
+    for (int i = 0; i < fasst_ctx::kNK; ++i) {
+      FASST_HIP(hipEventCreate(&c->ev0[i]));
+      FASST_HIP(hipEventCreate(&c->ev1[i]));
+    }
+  c->prof = on ? 1 : 0;
+  for (int i = 0; i < fasst_ctx::kNK; ++i) {
+    c->prof_ms[i] = 0.0;
+    c->prof_cnt[i] = 0;
+    c->used[i] = 0;
+  }
+  return FASST_OK;
+}
+
+int fasst_kernel_times(fasst_ctx *c, double *avg_ms, long *counts, int nk) {
+  if (!c || !avg_ms) return FASST_ERR_SHAPE;
+  for (int i = 0; i < nk && i < fasst_ctx::kNK; ++i) {
+    avg_ms[i] = c->prof_cnt[i] ? c->prof_ms[i] / (double)c->prof_cnt[i] : 0.0;
+    if (counts) counts[i] = c->prof_cnt[i];
+  }
+  return fasst_ctx::kNK;
+}
+
+const char *fasst_kernel_name(int i) {
+  return (i >= 0 && i < fasst_ctx::kNK) ? kKernelNames[i] : "";
+}
+
+}  // extern "C"

@@ -1,0 +1,615 @@
+// Time-frequency front/back end and the per-bin Wiener filter on MI355X.
+//
+//   k_stft_frames   Hann-windowed frames -> radix-2 FFT in LDS (FP64)
+//                   (tftransforms/stft.py:3-69; numpy.fft.rfft)
+//   k_istft_frames  Hermitian-extended inverse FFT per frame (stft.py:108-113)
+//   k_ola           deterministic gather overlap-add + window normalisation
+//                   (stft.py:110-129, same per-sample summation order)
+//   k_cx_from_X     Cx packing X0 X0*, X0 X1*, X1 X1* (audioModel.py:293-302)
+//   k_wiener<J>     Sigma_n = R_n V_n, Sigma_x^-1, WG_n = Sigma_n Sigma_x^-1,
+//                   S_n = WG_n X  (audioModel.py:1327-1467, :1205-1214)
+#include "fasst_ctx.h"
+
+#include <cmath>
+
+namespace fasst {
+
+__device__ __forceinline__ d4 mfma4b(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// In-LDS complex FFT of size N (power of two), data already in bit-reversed
+// order.  tw[k] = exp(sign * 2 pi i k / N), k < N/2.
+__device__ void lds_fft(double2 *x, const double2 *__restrict__ tw, int N, int logN) {
+  for (int s = 0; s < logN; ++s) {
+    const int m = 1 << s;
+    const int stride = N >> (s + 1);
+    for (int b = threadIdx.x; b < (N >> 1); b += blockDim.x) {
+      const int grp = b >> s, pos = b & (m - 1);
+      const int i0 = grp * 2 * m + pos, i1 = i0 + m;
+      const double2 w = tw[pos * stride];
+      const double2 u = x[i0], v = x[i1];
+      const double2 t = make_double2(w.x * v.x - w.y * v.y, w.x * v.y + w.y * v.x);
+      x[i0] = make_double2(u.x + t.x, u.y + t.y);
+      x[i1] = make_double2(u.x - t.x, u.y - t.y);
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int bitrev(int i, int logN) { return (int)(__brev((unsigned)i) >> (32 - logN)); }
+
+// One block per (frame, channel).  x: [nch][L] channel-major; output either
+// [frame][bin] into a pitched device image (ld = row pitch in bins) or, for
+// the stateless API, the same.
+__global__ __launch_bounds__(256) void k_stft_frames(const double *__restrict__ x, int L,
+                                                     const double *__restrict__ win, int wlen,
+                                                     const double2 *__restrict__ tw, int N,
+                                                     int logN, int hop, double2 *__restrict__ X,
+                                                     int ld, size_t ch_stride) {
+  extern __shared__ __attribute__((aligned(16))) double2 buf[];
+  const int n = blockIdx.x, ch = blockIdx.y;
+  const double *xc = x + (size_t)ch * L;
+  const int half = wlen / 2;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    double v = 0.0;
+    if (i < wlen) {
+      const long s = (long)n * hop + i - half;
+      if (s >= 0 && s < L) v = win[i] * xc[s];
+    }
+    buf[bitrev(i, logN)] = make_double2(v, 0.0);
+  }
+  __syncthreads();
+  lds_fft(buf, tw, N, logN);
+  double2 *out = X + ch * ch_stride + (size_t)n * ld;
+  for (int k = threadIdx.x; k <= N / 2; k += blockDim.x) out[k] = buf[k];
+}
+
+// Inverse: X [frame][bin] (ld pitch) -> frames [frame][wlen] = window * irfft[:wlen]
+__global__ __launch_bounds__(256) void k_istft_frames(const double2 *__restrict__ X, int ld,
+                                                      const double *__restrict__ win, int wlen,
+                                                      const double2 *__restrict__ tw, int N,
+                                                      int logN, double *__restrict__ frames) {
+  extern __shared__ __attribute__((aligned(16))) double2 buf[];
+  const int n = blockIdx.x;
+  const double2 *xn = X + (size_t)n * ld;
+  const int h = N / 2;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    double2 z;
+    if (i == 0)
+      z = make_double2(xn[0].x, 0.0);
+    else if (i == h)
+      z = make_double2(xn[h].x, 0.0);
+    else if (i < h)
+      z = xn[i];
+    else {
+      const double2 c = xn[N - i];
+      z = make_double2(c.x, -c.y);
+    }
+    buf[bitrev(i, logN)] = z;
+  }
+  __syncthreads();
+  lds_fft(buf, tw, N, logN);
+  const double invN = 1.0 / (double)N;
+  for (int i = threadIdx.x; i < wlen; i += blockDim.x)
+    frames[(size_t)n * wlen + i] = win[i] * (buf[i].x * invN);
+}
+
+// out[s] for s in [half, len): gather the frames covering s in frame order.
+__global__ void k_ola(const double *__restrict__ frames, int nframes, int wlen, int hop,
+                      const double *__restrict__ win, const double *__restrict__ awin,
+                      double *__restrict__ y, int len_out) {
+  const int half = wlen / 2;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < len_out; o += gridDim.x * blockDim.x) {
+    const long s = (long)o + half;
+    long nlo = (s - wlen) / hop + 1;
+    if (s - wlen < 0) nlo = 0;
+    long nhi = s / hop;
+    if (nhi > nframes - 1) nhi = nframes - 1;
+    double acc = 0.0, nrm = 0.0;
+    for (long n = nlo; n <= nhi; ++n) {
+      const int p = (int)(s - n * hop);
+      if (p < 0 || p >= wlen) continue;
+      nrm = nrm + win[p] * awin[p];
+      acc = acc + frames[(size_t)n * wlen + p];
+    }
+    y[o] = acc / (nrm == 0.0 ? 1.0 : nrm);
+  }
+}
+
+// Cx planes from the resident STFT images X[c][t][f].
+__global__ void k_cx_from_X(const double2 *__restrict__ X, double *__restrict__ cx, size_t plane) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < plane;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const double2 a = X[i], b = X[plane + i];
+    cx[i] = a.x * a.x + a.y * a.y;
+    cx[plane + i] = b.x * b.x + b.y * b.y;
+    cx[2 * plane + i] = a.x * b.x + a.y * b.y;
+    cx[3 * plane + i] = a.y * b.x - a.x * b.y;
+  }
+}
+
+// host Cx [3][F][T] complex  <->  device planes [4][Tp][Fp]
+__global__ void k_cx_unpack(const double2 *__restrict__ h, double *__restrict__ cx, int F, int T,
+                            int Fp, int Tp) {
+  __shared__ double2 tile[3][16][17];
+  const int f0 = blockIdx.y * 16, t0 = blockIdx.x * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  for (int q = 0; q < 3; ++q) {
+    const int f = f0 + ty, t = t0 + tx;
+    tile[q][ty][tx] = (f < F && t < T) ? h[((size_t)q * F + f) * T + t] : make_double2(0.0, 0.0);
+  }
+  __syncthreads();
+  const int t = t0 + ty, f = f0 + tx;
+  const size_t plane = (size_t)Tp * Fp, o = (size_t)t * Fp + f;
+  cx[o] = tile[0][tx][ty].x;
+  cx[plane + o] = tile[2][tx][ty].x;
+  cx[2 * plane + o] = tile[1][tx][ty].x;
+  cx[3 * plane + o] = tile[1][tx][ty].y;
+}
+__global__ void k_cx_pack(const double *__restrict__ cx, double2 *__restrict__ h, int F, int T,
+                          int Fp, int Tp) {
+  __shared__ double tile[4][16][17];
+  const int f0 = blockIdx.y * 16, t0 = blockIdx.x * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const size_t plane = (size_t)Tp * Fp;
+  {
+    const int t = t0 + ty, f = f0 + tx;
+    const size_t o = (size_t)t * Fp + f;
+    for (int q = 0; q < 4; ++q) tile[q][ty][tx] = cx[q * plane + o];
+  }
+  __syncthreads();
+  const int f = f0 + ty, t = t0 + tx;
+  if (f < F && t < T) {
+    h[((size_t)0 * F + f) * T + t] = make_double2(tile[0][tx][ty], 0.0);
+    h[((size_t)1 * F + f) * T + t] = make_double2(tile[2][tx][ty], tile[3][tx][ty]);
+    h[((size_t)2 * F + f) * T + t] = make_double2(tile[1][tx][ty], 0.0);
+  }
+}
+
+// generic complex [nm][F][T] (host order) <-> [nm][Tp][Fp] transposes
+__global__ void k_ft_to_tf(const double2 *__restrict__ src, double2 *__restrict__ dst, int F, int T,
+                           int Fp, int Tp) {
+  __shared__ double2 tile[16][17];
+  const int f0 = blockIdx.y * 16, t0 = blockIdx.x * 16, m = blockIdx.z;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  {
+    const int f = f0 + ty, t = t0 + tx;
+    tile[ty][tx] = (f < F && t < T) ? src[((size_t)m * F + f) * T + t] : make_double2(0.0, 0.0);
+  }
+  __syncthreads();
+  const int t = t0 + ty, f = f0 + tx;
+  if (t < Tp && f < Fp) dst[((size_t)m * Tp + t) * Fp + f] = tile[tx][ty];
+}
+__global__ void k_tf_to_ft(const double2 *__restrict__ src, double2 *__restrict__ dst, int F, int T,
+                           int Fp, int Tp) {
+  __shared__ double2 tile[16][17];
+  const int f0 = blockIdx.y * 16, t0 = blockIdx.x * 16, m = blockIdx.z;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  {
+    const int t = t0 + ty, f = f0 + tx;
+    tile[ty][tx] = (t < Tp && f < Fp) ? src[((size_t)m * Tp + t) * Fp + f] : make_double2(0.0, 0.0);
+  }
+  __syncthreads();
+  const int f = f0 + ty, t = t0 + tx;
+  if (f < F && t < T) dst[((size_t)m * F + f) * T + t] = tile[tx][ty];
+}
+
+__global__ void k_mix_psd(const double *__restrict__ cx, int F, int T, int Fp, int Tp,
+                          double *__restrict__ out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  const size_t plane = (size_t)Tp * Fp;
+  double s0 = 0.0, s2 = 0.0;
+  for (int t = 0; t < T; ++t) {
+    s0 += cx[(size_t)t * Fp + f];
+    s2 += cx[plane + (size_t)t * Fp + f];
+  }
+  out[f] = ((0.0 + s0 / T) + s2 / T) / 2.0;
+}
+
+// R_n coefficients per bin: sum over the ranks of n of |a0|^2, |a1|^2, a0 conj(a1)
+__global__ void k_mixcoef(const double2 *__restrict__ A, double *__restrict__ coef, int J,
+                          const int *__restrict__ roff_dev, int F, int Fp) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= Fp) return;
+  for (int j = 0; j < J; ++j) {
+    double al = 0, be = 0, gr = 0, gi = 0;
+    if (f < F)
+      for (int r = roff_dev[j]; r < roff_dev[j + 1]; ++r) {
+        const double2 a0 = A[(size_t)(2 * r) * Fp + f], a1 = A[(size_t)(2 * r + 1) * Fp + f];
+        al += a0.x * a0.x + a0.y * a0.y;
+        be += a1.x * a1.x + a1.y * a1.y;
+        gr += a0.x * a1.x + a0.y * a1.y;
+        gi += a0.y * a1.x - a0.x * a1.y;
+      }
+    coef[(size_t)(j * 4 + 0) * Fp + f] = al;
+    coef[(size_t)(j * 4 + 1) * Fp + f] = be;
+    coef[(size_t)(j * 4 + 2) * Fp + f] = gr;
+    coef[(size_t)(j * 4 + 3) * Fp + f] = gi;
+  }
+}
+
+struct WArgs {
+  const double *TW, *Wkf, *coef, *psd;
+  const double2 *X;  // [2][Tp][Fp]
+  double2 *S;        // [J][2][Tp][Fp]
+  int F, T, Fp, Tp, KP;
+};
+
+// one wave per 16x16 (frame, bin) tile; V^T from FP64 MFMA (V = W.H, no eps,
+// as comp_spat_comp_power inside compute_sigma_comp_2d)
+template <int J>
+__global__ __launch_bounds__(64) void k_wiener(const WArgs a) {
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int t0 = blockIdx.x * 16, f0 = blockIdx.y * 16, f = f0 + fl;
+  const int nks = a.KP >> 2;
+  d4 v[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    v[j] = d4{0.0, 0.0, 0.0, 0.0};
+    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+    const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
+    for (int s = 0; s < nks; ++s) v[j] = mfma4b(tw[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v[j]);
+  }
+  double cal[J], cbe[J], cgr[J], cgi[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    cal[j] = a.coef[(size_t)(j * 4 + 0) * a.Fp + f];
+    cbe[j] = a.coef[(size_t)(j * 4 + 1) * a.Fp + f];
+    cgr[j] = a.coef[(size_t)(j * 4 + 2) * a.Fp + f];
+    cgi[j] = a.coef[(size_t)(j * 4 + 3) * a.Fp + f];
+  }
+  const double psd = a.psd[f];
+  const size_t plane = (size_t)a.Tp * a.Fp;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + tq + 4 * i;
+    const size_t o = (size_t)t * a.Fp + f;
+    double d0 = 0.0, d1 = 0.0, orr = 0.0, oi = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      d0 += cal[j] * v[j][i];
+      d1 += cbe[j] * v[j][i];
+      orr += cgr[j] * v[j][i];
+      oi += cgi[j] * v[j][i];
+    }
+    d0 += psd;
+    d1 += psd;
+    double det = d0 * d1 - (orr * orr + oi * oi);
+    const double dg = det + kEps;
+    det = (dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0)) * fmax(fabs(det), kEps);
+    const double i0 = d1 / det, i1 = d0 / det;
+    const double ior = -orr / det, ioi = -oi / det;
+    const double2 x0 = a.X[o], x1 = a.X[plane + o];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const double vv = v[j][i];
+      const double s0 = cal[j] * vv, s1 = cbe[j] * vv, sr = cgr[j] * vv, si = cgi[j] * vv;
+      // WG00 = so conj(iso) + sd0 isd0 ; WG11 = conj(so conj(iso)) + sd1 isd1
+      const double pr = sr * ior + si * ioi, pi = si * ior - sr * ioi;
+      const double w00r = pr + s0 * i0, w00i = pi;
+      const double w11r = pr + s1 * i1, w11i = -pi;
+      // WG01 = sd0 iso + so isd1 ; WG10 = conj(so) isd0 + sd1 conj(iso)
+      const double w01r = s0 * ior + sr * i1, w01i = s0 * ioi + si * i1;
+      const double w10r = sr * i0 + s1 * ior, w10i = -si * i0 - s1 * ioi;
+      const double2 y0 = make_double2(w00r * x0.x - w00i * x0.y + (w01r * x1.x - w01i * x1.y),
+                                      w00r * x0.y + w00i * x0.x + (w01r * x1.y + w01i * x1.x));
+      const double2 y1 = make_double2(w10r * x0.x - w10i * x0.y + (w11r * x1.x - w11i * x1.y),
+                                      w10r * x0.y + w10i * x0.x + (w11r * x1.y + w11i * x1.x));
+      a.S[((size_t)j * 2 + 0) * plane + o] = y0;
+      a.S[((size_t)j * 2 + 1) * plane + o] = y1;
+    }
+  }
+}
+
+__global__ void k_inv_herm(int n, const double *__restrict__ d, const double2 *__restrict__ off,
+                           double *__restrict__ id, double2 *__restrict__ ioff,
+                           double *__restrict__ det_out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const double d0 = d[i], d1 = d[n + i];
+    const double2 o = off[i];
+    double det = d0 * d1 - (o.x * o.x + o.y * o.y);
+    const double dg = det + kEps;
+    det = (dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0)) * fmax(fabs(det), kEps);
+    ioff[i] = make_double2(-o.x / det, -o.y / det);
+    id[i] = d1 / det;
+    id[n + i] = d0 / det;
+    det_out[i] = det;
+  }
+}
+
+// twiddles exp(sign 2 pi i k / N), k < N/2, computed on the host in long double
+static std::vector<double2> twiddles(int N, int sign) {
+  std::vector<double2> tw(N / 2);
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (int k = 0; k < N / 2; ++k) {
+    const long double ang = 2.0L * pi * (long double)k / (long double)N;
+    tw[k] = make_double2((double)cosl(ang), (double)(sign * sinl(ang)));
+  }
+  return tw;
+}
+
+static int ilog2(int n) {
+  int l = 0;
+  while ((1 << l) < n) ++l;
+  return (1 << l) == n ? l : -1;
+}
+
+static int check_fft(int nfft, int wlen, int hop) {
+  if (ilog2(nfft) < 1 || wlen < 2 || wlen > nfft || hop < 1 || nfft > 8192) {
+    set_error("FFT size %d must be a power of two >= wlen %d (hop %d)", nfft, wlen, hop);
+    return FASST_ERR_SHAPE;
+  }
+  return FASST_OK;
+}
+
+static int fft_smem(int N) {
+  const size_t bytes = (size_t)N * sizeof(double2);
+  if (bytes > 64 * 1024) {
+    FASST_HIP(hipFuncSetAttribute((const void *)k_stft_frames,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    FASST_HIP(hipFuncSetAttribute((const void *)k_istft_frames,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  }
+  return FASST_OK;
+}
+
+}  // namespace fasst
+
+using namespace fasst;
+
+extern "C" {
+
+int fasst_stft(int device, const double *x, int L, const double *window, int wlen, int nfft,
+               int hop, double *X, int *n_frames) {
+  int st = check_fft(nfft, wlen, hop);
+  if (st) return st;
+  const int T = (L + hop - 1) / hop + 2;
+  if (n_frames) *n_frames = T;
+  if (!X) return FASST_OK;
+  DeviceGuard g(device);
+  if ((st = fft_smem(nfft))) return st;
+  const int F = nfft / 2 + 1;
+  DBuf<double> dx, dw;
+  DBuf<double2> dtw, dX, dXt;
+  if ((st = dx.alloc(std::max(L, 1))) || (st = dw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)) ||
+      (st = dX.alloc((size_t)T * F)) || (st = dXt.alloc((size_t)T * F)))
+    return st;
+  auto tw = twiddles(nfft, -1);
+  FASST_HIP(hipMemcpy(dx.p, x, (size_t)L * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dw.p, window, (size_t)wlen * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dtw.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
+  k_stft_frames<<<dim3(T, 1), 256, nfft * sizeof(double2)>>>(dx.p, L, dw.p, wlen, dtw.p, nfft,
+                                                             ilog2(nfft), hop, dX.p, F, 0);
+  FASST_LAUNCH_CHECK();
+  // [T][F] -> [F][T]
+  k_tf_to_ft<<<dim3((T + 15) / 16, (F + 15) / 16, 1), 256>>>(dX.p, dXt.p, F, T, F, T);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipDeviceSynchronize());
+  FASST_HIP(hipMemcpy(X, dXt.p, (size_t)T * F * sizeof(double2), hipMemcpyDeviceToHost));
+  return FASST_OK;
+}
+
+int fasst_istft(int device, const double *X, int n_frames, const double *window,
+                const double *analysis_window, int wlen, int nfft, int hop, double *y) {
+  int st = check_fft(nfft, wlen, hop);
+  if (st) return st;
+  if (n_frames < 1 || !X || !y) return FASST_ERR_SHAPE;
+  DeviceGuard g(device);
+  if ((st = fft_smem(nfft))) return st;
+  const int F = nfft / 2 + 1, T = n_frames;
+  const int len_out = hop * (T - 1) + wlen - wlen / 2;
+  DBuf<double> dw, daw, dframes, dy;
+  DBuf<double2> dtw, dX, dXt;
+  if ((st = dw.alloc(wlen)) || (st = daw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)) ||
+      (st = dX.alloc((size_t)T * F)) || (st = dXt.alloc((size_t)T * F)) ||
+      (st = dframes.alloc((size_t)T * wlen)) || (st = dy.alloc(len_out)))
+    return st;
+  auto tw = twiddles(nfft, +1);
+  FASST_HIP(hipMemcpy(dw.p, window, (size_t)wlen * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(daw.p, analysis_window ? analysis_window : window,
+                      (size_t)wlen * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dtw.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dX.p, X, (size_t)T * F * sizeof(double2), hipMemcpyHostToDevice));
+  // [F][T] -> [T][F]
+  k_ft_to_tf<<<dim3((T + 15) / 16, (F + 15) / 16, 1), 256>>>(dX.p, dXt.p, F, T, F, T);
+  FASST_LAUNCH_CHECK();
+  k_istft_frames<<<T, 256, nfft * sizeof(double2)>>>(dXt.p, F, dw.p, wlen, dtw.p, nfft,
+                                                     ilog2(nfft), dframes.p);
+  FASST_LAUNCH_CHECK();
+  k_ola<<<(len_out + 255) / 256, 256>>>(dframes.p, T, wlen, hop, dw.p, daw.p, dy.p, len_out);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipDeviceSynchronize());
+  FASST_HIP(hipMemcpy(y, dy.p, (size_t)len_out * sizeof(double), hipMemcpyDeviceToHost));
+  return FASST_OK;
+}
+
+int fasst_set_audio(fasst_ctx *c, const double *data, int L, const double *window, int wlen,
+                    int nfft, int hop) {
+  if (!c || !data || !window) return FASST_ERR_SHAPE;
+  int st = check_fft(nfft, wlen, hop);
+  if (st) return st;
+  const int T = (L + hop - 1) / hop + 2;
+  if (nfft / 2 + 1 != c->F || T != c->T) {
+    set_error("fasst_set_audio: context is %dx%d, audio gives %dx%d", c->F, c->T, nfft / 2 + 1, T);
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(c->device);
+  if ((st = fft_smem(nfft))) return st;
+  if (!c->X.p && (st = c->X.alloc((size_t)2 * c->Tp * c->Fp))) return st;
+  std::vector<double> chans((size_t)2 * L);
+  for (int i = 0; i < L; ++i) {
+    chans[i] = data[(size_t)i * 2];
+    chans[(size_t)L + i] = data[(size_t)i * 2 + 1];
+  }
+  DBuf<double> dx, dw;
+  DBuf<double2> dtw;
+  if ((st = dx.alloc((size_t)2 * L)) || (st = dw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)))
+    return st;
+  auto tw = twiddles(nfft, -1);
+  FASST_HIP(hipMemcpyAsync(dx.p, chans.data(), chans.size() * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(dw.p, window, (size_t)wlen * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+  FASST_HIP(hipMemcpyAsync(dtw.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice,
+                           c->stream));
+  FASST_HIP(hipMemsetAsync(c->X.p, 0, c->X.n * sizeof(double2), c->stream));
+  k_stft_frames<<<dim3(T, 2), 256, nfft * sizeof(double2), c->stream>>>(
+      dx.p, L, dw.p, wlen, dtw.p, nfft, ilog2(nfft), hop, c->X.p, c->Fp, (size_t)c->Tp * c->Fp);
+  FASST_LAUNCH_CHECK();
+  const size_t plane = (size_t)c->Tp * c->Fp;
+  k_cx_from_X<<<2048, 256, 0, c->stream>>>(c->X.p, c->cx.p, plane);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  c->have_X = true;
+  return FASST_OK;
+}
+
+int fasst_mix_psd(fasst_ctx *c, double *mix_psd) {
+  if (!c || !mix_psd) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  DBuf<double> d;
+  int st;
+  if ((st = d.alloc(c->F))) return st;
+  k_mix_psd<<<(c->F + 255) / 256, 256, 0, c->stream>>>(c->cx.p, c->F, c->T, c->Fp, c->Tp, d.p);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipMemcpyAsync(mix_psd, d.p, c->F * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_set_cx(fasst_ctx *c, const double *cx) {
+  if (!c || !cx) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  DBuf<double2> h;
+  int st;
+  if ((st = h.alloc((size_t)3 * c->F * c->T))) return st;
+  FASST_HIP(hipMemcpyAsync(h.p, cx, h.n * sizeof(double2), hipMemcpyHostToDevice, c->stream));
+  k_cx_unpack<<<dim3(c->ntt, c->nft), 256, 0, c->stream>>>(h.p, c->cx.p, c->F, c->T, c->Fp, c->Tp);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_get_cx(fasst_ctx *c, double *cx) {
+  if (!c || !cx) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  DBuf<double2> h;
+  int st;
+  if ((st = h.alloc((size_t)3 * c->F * c->T))) return st;
+  k_cx_pack<<<dim3(c->ntt, c->nft), 256, 0, c->stream>>>(c->cx.p, h.p, c->F, c->T, c->Fp, c->Tp);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipMemcpyAsync(cx, h.p, h.n * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+}  // extern "C"
+
+namespace fasst {
+static int upload_stft(fasst_ctx *c, const double *X) {
+  int st;
+  if (!c->X.p && (st = c->X.alloc((size_t)2 * c->Tp * c->Fp))) return st;
+  DBuf<double2> h;
+  if ((st = h.alloc((size_t)2 * c->F * c->T))) return st;
+  FASST_HIP(hipMemcpyAsync(h.p, X, h.n * sizeof(double2), hipMemcpyHostToDevice, c->stream));
+  k_ft_to_tf<<<dim3(c->ntt, c->nft, 2), 256, 0, c->stream>>>(h.p, c->X.p, c->F, c->T, c->Fp, c->Tp);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  c->have_X = true;
+  return FASST_OK;
+}
+}  // namespace fasst
+
+extern "C" {
+
+int fasst_set_stft(fasst_ctx *c, const double *X) {
+  if (!c || !X) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  int st = upload_stft(c, X);
+  if (st) return st;
+  k_cx_from_X<<<2048, 256, 0, c->stream>>>(c->X.p, c->cx.p, (size_t)c->Tp * c->Fp);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double *S) {
+  if (!c || !c->configured || !psd || !S) {
+    set_error("fasst_wiener_images: context not configured");
+    return FASST_ERR_SHAPE;
+  }
+  int st;
+  if (X && (st = upload_stft(c, X))) return st;
+  if (!c->have_X) {
+    set_error("fasst_wiener_images: no STFT available (set_audio / set_stft / X argument)");
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(c->device);
+  const int J = c->J;
+  DBuf<double> dpsd, coef;
+  DBuf<int> droff;
+  DBuf<double2> dS, hS;
+  const size_t plane = (size_t)c->Tp * c->Fp;
+  if ((st = dpsd.alloc(c->Fp)) || (st = coef.alloc((size_t)J * 4 * c->Fp)) ||
+      (st = droff.alloc(kMaxJ + 1)) || (st = dS.alloc((size_t)J * 2 * plane)) ||
+      (st = hS.alloc((size_t)J * 2 * c->F * c->T)))
+    return st;
+  FASST_HIP(hipMemcpyAsync(dpsd.p, psd, c->F * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(droff.p, c->roff, (J + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  // W = FB.FW and the per-bin mixing for 'inst'
+  if ((st = build_inst_A(c))) return st;
+  if ((st = launch_w_old(c))) return st;
+  k_mixcoef<<<(c->Fp + 255) / 256, 256, 0, c->stream>>>(c->A.p, coef.p, J, droff.p, c->F, c->Fp);
+  FASST_LAUNCH_CHECK();
+  WArgs w;
+  w.TW = c->TW.p;
+  w.Wkf = c->Wkf.p;
+  w.coef = coef.p;
+  w.psd = dpsd.p;
+  w.X = c->X.p;
+  w.S = dS.p;
+  w.F = c->F;
+  w.T = c->T;
+  w.Fp = c->Fp;
+  w.Tp = c->Tp;
+  w.KP = c->KP;
+  const dim3 grid(c->ntt, c->nft);
+  switch (J) {
+    case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
+    case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
+    case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
+    default: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+  }
+  FASST_LAUNCH_CHECK();
+  k_tf_to_ft<<<dim3(c->ntt, c->nft, J * 2), 256, 0, c->stream>>>(dS.p, hS.p, c->F, c->T, c->Fp, c->Tp);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipMemcpyAsync(S, hS.p, hS.n * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_inv_herm_mat_2d(int device, int n, const double *diag, const double *off,
+                          double *inv_diag, double *inv_off, double *det) {
+  if (n < 0 || (n > 0 && (!diag || !off || !inv_diag || !inv_off || !det))) return FASST_ERR_SHAPE;
+  if (n == 0) return FASST_OK;
+  DeviceGuard g(device);
+  DBuf<double> dd, did, ddet;
+  DBuf<double2> doff, dioff;
+  int st;
+  if ((st = dd.alloc((size_t)2 * n)) || (st = did.alloc((size_t)2 * n)) || (st = ddet.alloc(n)) ||
+      (st = doff.alloc(n)) || (st = dioff.alloc(n)))
+    return st;
+  FASST_HIP(hipMemcpy(dd.p, diag, (size_t)2 * n * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(doff.p, off, (size_t)n * sizeof(double2), hipMemcpyHostToDevice));
+  k_inv_herm<<<std::min((n + 255) / 256, 4096), 256>>>(n, dd.p, doff.p, did.p, dioff.p, ddet.p);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipDeviceSynchronize());
+  FASST_HIP(hipMemcpy(inv_diag, did.p, (size_t)2 * n * sizeof(double), hipMemcpyDeviceToHost));
+  FASST_HIP(hipMemcpy(inv_off, dioff.p, (size_t)n * sizeof(double2), hipMemcpyDeviceToHost));
+  FASST_HIP(hipMemcpy(det, ddet.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+  return FASST_OK;
+}
+
+}  // extern "C"

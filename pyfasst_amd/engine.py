@@ -1,0 +1,143 @@
+"""Thin object wrapper over one device context of libfasst_hip.so.
+
+All compute happens on the GPU; this module only moves NumPy arrays across
+the C ABI (include/fasst_hip.h) and maps status codes to exceptions.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dptr, iptr, lib
+
+
+class Engine(object):
+    """Device state of one FASST model: observation (Cx, STFT) + parameters."""
+
+    def __init__(self, F, T, device=None):
+        self.device = _lib.default_device() if device is None else int(device)
+        self.F, self.T = int(F), int(T)
+        h = ctypes.c_void_p()
+        check(lib.fasst_create(self.device, self.F, self.T, ctypes.byref(h)), "fasst_create")
+        self._h = h
+        self.structure = None
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib.fasst_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def configure(self, ranks, Ks, conv):
+        key = (tuple(int(r) for r in ranks), tuple(int(k) for k in Ks), bool(conv))
+        if key == self.structure:
+            return
+        r = np.ascontiguousarray(ranks, dtype=np.int32)
+        k = np.ascontiguousarray(Ks, dtype=np.int32)
+        check(lib.fasst_configure(self._h, len(r), iptr(r), iptr(k), int(bool(conv))),
+              "fasst_configure")
+        self.structure = key
+
+    # ------------------------------------------------------------ observation
+    def set_audio(self, data, window, nfft, hop):
+        data = np.ascontiguousarray(data, dtype=np.float64)
+        window = np.ascontiguousarray(window, dtype=np.float64)
+        check(lib.fasst_set_audio(self._h, dptr(data), data.shape[0], dptr(window), window.size,
+                                  int(nfft), int(hop)), "fasst_set_audio")
+
+    def mix_psd(self):
+        out = np.empty(self.F)
+        check(lib.fasst_mix_psd(self._h, dptr(out)), "fasst_mix_psd")
+        return out
+
+    def set_cx(self, Cx):
+        Cx = np.ascontiguousarray(Cx, dtype=np.complex128)
+        if Cx.shape != (3, self.F, self.T):
+            raise ValueError("Cx shape %s != (3, %d, %d)" % (Cx.shape, self.F, self.T))
+        check(lib.fasst_set_cx(self._h, dptr(Cx)), "fasst_set_cx")
+
+    def get_cx(self):
+        out = np.empty((3, self.F, self.T), dtype=np.complex128)
+        check(lib.fasst_get_cx(self._h, dptr(out)), "fasst_get_cx")
+        return out
+
+    def set_stft(self, X):
+        X = np.ascontiguousarray(X, dtype=np.complex128)
+        if X.shape != (2, self.F, self.T):
+            raise ValueError("X shape %s != (2, %d, %d)" % (X.shape, self.F, self.T))
+        check(lib.fasst_set_stft(self._h, dptr(X)), "fasst_set_stft")
+
+    # ------------------------------------------------------------ parameters
+    def set_spatial(self, j, params, free):
+        p = np.ascontiguousarray(params, dtype=np.complex128)
+        check(lib.fasst_set_spatial(self._h, int(j), dptr(p), int(bool(free))), "fasst_set_spatial")
+
+    def get_spatial(self, j, shape):
+        out = np.empty(shape, dtype=np.complex128)
+        check(lib.fasst_get_spatial(self._h, int(j), dptr(out)), "fasst_get_spatial")
+        return out
+
+    def set_spectral(self, j, FB, FW, TW, fb_free, tw_free):
+        FB = np.ascontiguousarray(FB, dtype=np.float64)
+        FW = np.ascontiguousarray(FW, dtype=np.float64)
+        TW = np.ascontiguousarray(TW, dtype=np.float64)
+        check(lib.fasst_set_spectral(self._h, int(j), dptr(FB), dptr(FW), dptr(TW),
+                                     int(bool(fb_free)), int(bool(tw_free))), "fasst_set_spectral")
+
+    def get_spectral(self, j, K):
+        FB = np.empty((self.F, K))
+        FW = np.empty((K, K))
+        TW = np.empty((K, self.T))
+        check(lib.fasst_get_spectral(self._h, int(j), dptr(FB), dptr(FW), dptr(TW)),
+              "fasst_get_spectral")
+        return FB, FW, TW
+
+    # ------------------------------------------------------------ compute
+    def renormalize(self):
+        mask = ctypes.c_int(0)
+        check(lib.fasst_renormalize(self._h, ctypes.byref(mask)), "fasst_renormalize")
+        return mask.value
+
+    def run(self, psd_rows, omega):
+        """Run len(psd_rows) GEM iterations.  Returns (logliks, done, restart_mask)."""
+        psd_rows = np.ascontiguousarray(psd_rows, dtype=np.float64)
+        n = psd_rows.shape[0]
+        if n and psd_rows.shape[1] != self.F:
+            raise ValueError("psd rows must have F=%d columns" % self.F)
+        ll = np.zeros(max(n, 1))
+        mask = ctypes.c_int(0)
+        done = ctypes.c_int(0)
+        st = lib.fasst_run(self._h, n, dptr(psd_rows) if n else None, float(omega), dptr(ll),
+                           ctypes.byref(mask), ctypes.byref(done))
+        if st == _lib.FASST_TW_RESTART:
+            return ll[:done.value], done.value, mask.value
+        check(st, "fasst_run")
+        return ll[:n], n, 0
+
+    def set_profiling(self, on=True):
+        check(lib.fasst_set_profiling(self._h, int(bool(on))), "fasst_set_profiling")
+
+    def kernel_times(self):
+        """{kernel name: (mean ms per launch, launches)} over the profiled iterations."""
+        nk = 32
+        ms = np.zeros(nk)
+        cnt = (ctypes.c_long * nk)()
+        n = lib.fasst_kernel_times(self._h, dptr(ms), cnt, nk)
+        return {lib.fasst_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(n) if cnt[i]}
+
+    def wiener_images(self, psd, X=None):
+        psd = np.ascontiguousarray(psd, dtype=np.float64)
+        J = len(self.structure[0])
+        out = np.empty((J, 2, self.F, self.T), dtype=np.complex128)
+        xp = None
+        if X is not None:
+            X = np.ascontiguousarray(X, dtype=np.complex128)
+            xp = dptr(X)
+        check(lib.fasst_wiener_images(self._h, dptr(psd), xp, dptr(out)), "fasst_wiener_images")
+        return out

@@ -1,0 +1,46 @@
+"""Shared test helpers (test infrastructure only)."""
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+# golden case -> (J, K, spatial_rank, conv, ctor kwargs); mirrors tests/golden/make_golden.py
+CASES = {
+    "em_inst": (2, 4, 1, False, dict(iter_num=6, wlen=256, hopsize=128)),
+    "em_inst_noann": (3, 5, 2, False, dict(iter_num=4, wlen=128, hopsize=64,
+                                           sim_ann_opt='no_ann', nmfUpdateCoeff=0.7)),
+    "em_conv": (3, 8, 2, True, dict(iter_num=5, wlen=256, hopsize=64)),
+    "em_conv_j4": (4, 16, 2, True, dict(iter_num=4, wlen=256, hopsize=64)),
+    "em_conv_j1": (1, 3, [2], True, dict(iter_num=3, wlen=128, hopsize=32)),
+}
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+def rel(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    den = np.max(np.abs(b))
+    return float(np.max(np.abs(a - b)) / (den if den > 0 else 1.0))
+
+
+def oracle_model_from_golden(g, case):
+    """Oracle model on the golden wav (oracle STFT), initialised like the reference."""
+    import fasst_ref as R
+    J, K, rank, conv, kw = CASES[case]
+    x, _ = R.read_scaled(g['wav'])
+    wlen, hop = kw['wlen'], kw['hopsize']
+    w = np.hanning(wlen)
+    X = [R.stft(x[:, c], w, hop, wlen) for c in range(2)]
+    okw = {k: v for k, v in kw.items() if k in ('iter_num', 'sim_ann_opt', 'nmfUpdateCoeff')}
+    m = R.RefFASST(**okw)
+    m.set_transform(X)
+    np.random.seed(0)
+    R.init_nmf_inst(m, J, K, rank)
+    if conv:
+        R.make_convolutive(m)
+    return m, X

@@ -1,0 +1,62 @@
+"""The CPU oracle (oracle/fasst_ref.py) against the reference's own outputs.
+
+Golden vectors were produced by running the reference itself
+(tests/golden/make_golden.py); inv_herm.npz holds the known-answer data of
+the reference test pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64.
+"""
+import numpy as np
+import pytest
+
+import fasst_ref as R
+from helpers import CASES, load, oracle_model_from_golden, rel
+
+
+def test_inv_herm_known_answer():
+    g = load("inv_herm")
+    d, o, det = R.inv_herm_mat_2d(g['sigma_x_diag'], g['sigma_x_off'])
+    # the reference test's own assertions (A A^-1 = I to 6 decimals)
+    np.testing.assert_array_almost_equal(d[0] * g['sigma_x_diag'][0] + g['sigma_x_off'] * np.conj(o),
+                                         np.ones_like(o))
+    np.testing.assert_array_almost_equal(d[0] * np.conj(g['sigma_x_off']) +
+                                         g['sigma_x_diag'][1] * np.conj(o), np.zeros_like(o))
+    np.testing.assert_array_equal(d, g['inv_diag_run'])
+    np.testing.assert_array_equal(o, g['inv_off_run'])
+    # (the test file's inv_*_ref literals are not asserted by the reference
+    # test itself: its inputs are printed to 8 digits and near-singular)
+
+
+def test_stft_istft_golden():
+    g = load("stft")
+    for nfft, hop in ((256, 64), (512, 128), (1024, 256)):
+        X = R.stft(g['x'], np.hanning(nfft), hop, nfft)
+        np.testing.assert_array_equal(X, g['X_%d_%d' % (nfft, hop)])
+        y = R.istft(X, np.hanning(nfft), np.hanning(nfft), hop, nfft)[:g['x'].size]
+        np.testing.assert_array_equal(y, g['y_%d_%d' % (nfft, hop)])
+
+
+def test_nmf_golden():
+    g = load("nmf")
+    rng = np.random.RandomState(1)
+    W, H = R.nmf_decomposition(g['SX'], nbComps=6, niter=7, rng=rng)
+    np.testing.assert_array_equal(W, g['W'])
+    np.testing.assert_array_equal(H, g['H'])
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_em_golden(case):
+    g = load(case)
+    m, X = oracle_model_from_golden(g, case)
+    J = CASES[case][0]
+    np.testing.assert_array_equal(m.Cx, g['Cx'])
+    for j in range(J):
+        np.testing.assert_array_equal(np.array(m.spat_comps[j]['params']), g['init_params_%d' % j])
+        np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FB'], g['init_FB_%d' % j])
+        np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['init_TW_%d' % j])
+    ll = m.estim_param_a_post_model()
+    np.testing.assert_array_equal(ll, g['logliks'])
+    for j in range(J):
+        np.testing.assert_array_equal(np.array(m.spat_comps[j]['params']), g['final_params_%d' % j])
+        np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FB'], g['final_FB_%d' % j])
+        np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['final_TW_%d' % j])
+    S = m.separated_images(X)
+    assert rel(np.abs(S), np.abs(g['images'])) == 0.0
