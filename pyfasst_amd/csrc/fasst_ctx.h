@@ -34,7 +34,8 @@ struct fasst_ctx {
   fasst::DBuf<double2> A, Pinst;
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
-  fasst::DBuf<double> epart, llpart, bnum, bden, psd, ll;
+  fasst::DBuf<double> epart, llpart, bnum, bden, psd, ll, hsum, rscal, rtpart;
+  int nchunk_r = 1;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart
   int *h_flags = nullptr;        // pinned host mirror
@@ -43,6 +44,7 @@ struct fasst_ctx {
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
   static constexpr int kNK = 11;
   int prof = 0;
+  int ablate = 0;  // FASST_ABLATE (profiling builds of the E-step; never in the product)
   hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};
   int used[kNK] = {0};
   double prof_ms[kNK] = {0};

@@ -65,20 +65,28 @@ __global__ void k_w_from_fb(const double *__restrict__ FB, const double *__restr
   }
 }
 
-// FWHt[j][t][k] = sum_q FW[j][k][q] TW[j][q][t]
-__global__ void k_fwh_t(const double *__restrict__ FW, const double *__restrict__ TW,
-                        double *__restrict__ FWHt, int J, int Tp, int KP) {
-  const size_t n = (size_t)J * Tp * KP;
-  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    const int k = idx % KP;
-    const int t = (idx / KP) % Tp;
-    const int j = idx / ((size_t)Tp * KP);
-    const double *fw = FW + ((size_t)j * KP + k) * KP;
-    const double *tw = TW + (size_t)j * KP * Tp + t;
+// FWHt[j][t][k] = sum_q FW[j][k][q] TW[j][q][t]; one block per (64-frame
+// tile, source): FW and the TW tile staged in LDS, coalesced [t][k] writes.
+__global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
+                                               const double *__restrict__ TW,
+                                               double *__restrict__ FWHt, int J, int Tp, int KP) {
+  extern __shared__ __attribute__((aligned(16))) double s_f[];
+  double *s_fw = s_f;             // [KP][KP]
+  double *s_tw = s_f + KP * KP;   // [KP][64]
+  const int j = blockIdx.y, t0 = blockIdx.x * 64;
+  const int tn = min(64, Tp - t0);
+  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
+    s_fw[idx] = FW[(size_t)j * KP * KP + idx];
+  for (int idx = threadIdx.x; idx < KP * 64; idx += blockDim.x) {
+    const int q = idx >> 6, tl = idx & 63;
+    s_tw[idx] = tl < tn ? TW[((size_t)j * KP + q) * Tp + t0 + tl] : 0.0;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < tn * KP; idx += blockDim.x) {
+    const int tl = idx / KP, k = idx % KP;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += fw[q] * tw[(size_t)q * Tp];
-    FWHt[idx] = s;
+    for (int q = 0; q < KP; ++q) s += s_fw[k * KP + q] * s_tw[q * 64 + tl];
+    FWHt[((size_t)j * Tp + t0 + tl) * KP + k] = s;
   }
 }
 
@@ -110,10 +118,21 @@ struct EArgs {
 // Block: 4 waves on one 16-bin tile; wave w walks frame tiles w, w+4, ... of
 // the block's chunk.  Each lane owns ONE bin (f = f0 + lane%16) and 4 frames
 // per tile, so all per-bin statistics stay in registers across the t-loop.
-template <int J>
-__global__ __launch_bounds__(256) void k_estep(const EArgs a) {
+// The E-step is split in two launches so that each keeps half of the per-bin
+// accumulators live (occupancy):
+//   PART 1: pair statistics sum_t V_j1 V_j2 N (4 per pair), loglik, hat_W
+//   PART 2: cross statistics sum_t V_j Cx S (8 per source)
+// NKS = KP/4 MFMA k-steps; RKU = 1 or 2: every source has that rank (no
+// predication), 0: general ranks <= kMaxR.  AB = ablation bits (profiling
+// builds only, 0 in the product).
+template <int J, int NKS, int RKU, int PART, int AB>
+__global__ __launch_bounds__(256, 2) void k_estep(const EArgs a) {
   constexpr int NP = J * (J + 1) / 2;
-  constexpr int NACC = 4 * NP + 9 * J;
+  constexpr int NACC = PART == 1 ? 4 * NP : 8 * J;
+  constexpr int UOFF = PART == 1 ? 0 : 4 * NP;   // column offset in the partial rows
+  constexpr int NTOT = 4 * NP + 8 * J;
+  constexpr int KP = 4 * NKS;
+  constexpr int RK = RKU ? RKU : kMaxR;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *s_cr = smem;                     // [kMaxR][4][16]
   double *s_cj = s_cr + kMaxR * 4 * 16;    // [J][4][16]
@@ -126,7 +145,7 @@ __global__ __launch_bounds__(256) void k_estep(const EArgs a) {
   const int f0 = blockIdx.x * 16;
   const int f = f0 + fl;
 
-  for (int idx = tid; idx < J * a.KP * 16; idx += 256) {
+  for (int idx = tid; idx < J * KP * 16; idx += 256) {
     const int ff = idx & 15, jk = idx >> 4;
     s_w[idx] = a.Wkf[(size_t)jk * a.Fp + f0 + ff];
   }
@@ -144,8 +163,8 @@ __global__ __launch_bounds__(256) void k_estep(const EArgs a) {
         const double ci = a0.y * a1.x - a0.x * a1.y;  // Im a0 conj(a1)
         s_cr[(r * 4 + 0) * 16 + tid] = aa;
         s_cr[(r * 4 + 1) * 16 + tid] = bb;
-        s_cr[(r * 4 + 2) * 16 + tid] = cr;
-        s_cr[(r * 4 + 3) * 16 + tid] = ci;
+        s_cr[(r * 4 + 2) * 16 + tid] = 2.0 * cr;
+        s_cr[(r * 4 + 3) * 16 + tid] = 2.0 * ci;
         al += aa;
         be += bb;
         gr += cr;
@@ -159,35 +178,33 @@ __global__ __launch_bounds__(256) void k_estep(const EArgs a) {
   }
   __syncthreads();
 
-  double cal[J], cbe[J], cgr[J], cgi[J];
+  int rk[J], r0[J];
+  double inv_rk[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    cal[j] = s_cj[(j * 4 + 0) * 16 + fl];
-    cbe[j] = s_cj[(j * 4 + 1) * 16 + fl];
-    cgr[j] = s_cj[(j * 4 + 2) * 16 + fl];
-    cgi[j] = s_cj[(j * 4 + 3) * 16 + fl];
+    r0[j] = RKU ? RKU * j : a.roff[j];
+    rk[j] = RKU ? RKU : a.roff[j + 1] - a.roff[j];
+    inv_rk[j] = 1.0 / (double)rk[j];
   }
   const double psd = a.psd[f];
   const bool fvalid = f < a.F;
 
-  double sn[NP][4], q[J][8], sv[J];
-  double ll = 0.0;
+  double acc[NACC];
 #pragma unroll
-  for (int p = 0; p < NP; ++p)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) sn[p][u] = 0.0;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    sv[j] = 0.0;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) q[j][u] = 0.0;
-  }
+  for (int u = 0; u < NACC; ++u) acc[u] = 0.0;
+  // loglik: sum log(det*pi) is accumulated as a mantissa product lm in [0.5,1)
+  // times 2^lev (one log() per lane at the end instead of one per point);
+  // non-positive / non-finite terms map to -inf / NaN / inf like log().
+  double ll = 0.0, lm = 1.0, lev = 0.0, lspec = 0.0;
 
   const int tb = blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
-  const int nks = a.KP >> 2;
   for (int tt = tb + wv; tt < te; tt += 4) {
     const int t0 = tt * 16;
+    // the W tile and mixing coefficients are loop-invariant LDS data: launder
+    // the offset so they are re-read per tile instead of pinning ~96 VGPRs
+    int lofs = 0;
+    asm volatile("" : "+v"(lofs));
     double c00[4], c11[4], cre[4], cim[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -201,11 +218,13 @@ __global__ __launch_bounds__(256) void k_estep(const EArgs a) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       v[j] = d4{0.0, 0.0, 0.0, 0.0};
-      const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
-      const double *sw = s_w + (j * a.KP + tq) * 16 + fl;
-      for (int s = 0; s < nks; ++s)
+      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
+      const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s)
         v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], sw[4 * s * 16], v[j]);
     }
+    const double *cj = s_cj + lofs + fl;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int t = t0 + tq + 4 * i;
@@ -215,10 +234,10 @@ __global__ __launch_bounds__(256) void k_estep(const EArgs a) {
       double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        d0 += cal[j] * V[j];
-        d1 += cbe[j] * V[j];
-        ore += cgr[j] * V[j];
-        oim += cgi[j] * V[j];
+        d0 += cj[(j * 4 + 0) * 16] * V[j];
+        d1 += cj[(j * 4 + 1) * 16] * V[j];
+        ore += cj[(j * 4 + 2) * 16] * V[j];
+        oim += cj[(j * 4 + 3) * 16] * V[j];
       }
       // inv_herm_mat_2d (signalTools.py:177-194)
       double det = d0 * d1 - (ore * ore + oim * oim);
@@ -228,90 +247,130 @@ __global__ __launch_bounds__(256) void k_estep(const EArgs a) {
       const double rd = 1.0 / det;
       const double i0 = d1 * rd, i1 = d0 * rd, ior = -ore * rd, ioi = -oim * rd;
       const double x00 = c00[i], x11 = c11[i], xr = cre[i], xi = cim[i];
-      if (fvalid && t < a.T)
-        ll += log(det * M_PI) + i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
       // P = Cx S
       const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
       const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
       const double p10r = xr * i0 + x11 * ior, p10i = -xi * i0 - x11 * ioi;
       const double p11r = xr * ior + xi * ioi + x11 * i1, p11i = xr * ioi - xi * ior;
+      if (PART == 2) {
+        if (!(AB & 4)) {
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            acc[8 * j + 0] += V[j] * p00r;
+            acc[8 * j + 1] += V[j] * p00i;
+            acc[8 * j + 2] += V[j] * p01r;
+            acc[8 * j + 3] += V[j] * p01i;
+            acc[8 * j + 4] += V[j] * p10r;
+            acc[8 * j + 5] += V[j] * p10i;
+            acc[8 * j + 6] += V[j] * p11r;
+            acc[8 * j + 7] += V[j] * p11i;
+          }
+        }
+        continue;
+      }
+      if (fvalid && t < a.T) {
+        const double x = det * M_PI;
+        if (AB & 1) {
+          ll += x;
+        } else if (x > 0.0 && x < INFINITY) {
+          const unsigned long long b = __double_as_longlong(x);
+          lev += (double)((int)((b >> 52) & 0x7ff) - 1022);
+          lm *= __longlong_as_double((b & 0x800fffffffffffffULL) | 0x3fe0000000000000ULL);
+        } else {
+          lspec += x == 0.0 ? -INFINITY : (x == INFINITY ? INFINITY : NAN);
+        }
+        ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
+      }
       // N = S Cx S - S = P^H S - S
       const double n00 = p00r * i0 + (p10r * ior - p10i * ioi) - i0;
       const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
       const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
       const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
-      int p = 0;
+      if (!(AB & 4)) {
+        int p = 0;
 #pragma unroll
-      for (int j1 = 0; j1 < J; ++j1) {
+        for (int j1 = 0; j1 < J; ++j1) {
 #pragma unroll
-        for (int j2 = j1; j2 < J; ++j2, ++p) {
-          const double vv = V[j1] * V[j2];
-          sn[p][0] += vv * n00;
-          sn[p][1] += vv * n11;
-          sn[p][2] += vv * n01r;
-          sn[p][3] += vv * n01i;
+          for (int j2 = j1; j2 < J; ++j2, ++p) {
+            const double vv = V[j1] * V[j2];
+            acc[4 * p + 0] += vv * n00;
+            acc[4 * p + 1] += vv * n11;
+            acc[4 * p + 2] += vv * n01r;
+            acc[4 * p + 3] += vv * n01i;
+          }
         }
-      }
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        q[j][0] += V[j] * p00r;
-        q[j][1] += V[j] * p00i;
-        q[j][2] += V[j] * p01r;
-        q[j][3] += V[j] * p01i;
-        q[j][4] += V[j] * p10r;
-        q[j][5] += V[j] * p10i;
-        q[j][6] += V[j] * p11r;
-        q[j][7] += V[j] * p11i;
-        sv[j] += V[j];
       }
       // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414)
+      if (!(AB & 2)) {
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        double acc = 0.0;
-        const double v2 = V[j] * V[j];
-        for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
-          const double qa = s_cr[(r * 4 + 0) * 16 + fl] * n00 + s_cr[(r * 4 + 1) * 16 + fl] * n11 +
-                            2.0 * (s_cr[(r * 4 + 2) * 16 + fl] * n01r +
-                                   s_cr[(r * 4 + 3) * 16 + fl] * n01i);
-          acc += fabs(v2 * qa + V[j]);
+        for (int j = 0; j < J; ++j) {
+          double hw = 0.0;
+          const double v2 = V[j] * V[j];
+#pragma unroll
+          for (int qq = 0; qq < RK; ++qq) {
+            if (RKU || qq < rk[j]) {
+              const double *cr = s_cr + lofs + (r0[j] + qq) * 64 + fl;
+              const double qa = cr[0] * n00 + cr[16] * n11 + (cr[32] * n01r + cr[48] * n01i);
+              hw += fabs(v2 * qa + V[j]);
+            }
+          }
+          a.hatW[((size_t)j * a.Tp + t) * a.Fp + f] = RKU == 1 ? hw : hw * inv_rk[j];
         }
-        a.hatW[((size_t)j * a.Tp + t) * a.Fp + f] = acc / (double)(a.roff[j + 1] - a.roff[j]);
+      } else {
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) sum += V[j] * n00;
+        a.hatW[(size_t)t * a.Fp + f] = sum;
       }
     }
+    if (PART == 1) {  // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
+      const unsigned long long b = __double_as_longlong(lm);
+      lev += (double)((int)((b >> 52) & 0x7ff) - 1022);
+      lm = __longlong_as_double((b & 0x800fffffffffffffULL) | 0x3fe0000000000000ULL);
+    }
   }
+  if (PART == 1) ll += (log(lm) + lev * M_LN2) + lspec;
 
   // reduce the 4 lanes sharing a bin, then the 4 waves, then write the chunk partial
   __syncthreads();  // s_red aliases s_w: every wave must be done with its last tile
   double *red = s_red + wv * NACC * 16;
-  auto put = [&](int idx, double x) {
+#pragma unroll
+  for (int u = 0; u < NACC; ++u) {
+    double x = acc[u];
     x += __shfl_xor(x, 16, 64);
     x += __shfl_xor(x, 32, 64);
-    if (tq == 0) red[idx * 16 + fl] = x;
-  };
-  {
-    int idx = 0;
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) put(idx++, sn[p][u]);
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-#pragma unroll
-      for (int u = 0; u < 8; ++u) put(idx++, q[j][u]);
-#pragma unroll
-    for (int j = 0; j < J; ++j) put(idx++, sv[j]);
+    if (tq == 0) red[u * 16 + fl] = x;
   }
+  if (PART == 1) {
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) ll += __shfl_xor(ll, m, 64);
-  if (lane == 0) s_ll[wv] = ll;
+    for (int m = 1; m < 64; m <<= 1) ll += __shfl_xor(ll, m, 64);
+    if (lane == 0) s_ll[wv] = ll;
+  }
   __syncthreads();
   for (int idx = tid; idx < NACC * 16; idx += 256) {
     const int u = idx >> 4, ff = idx & 15;
     const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
                      s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
-    a.part[((size_t)blockIdx.y * a.Fp + f0 + ff) * NACC + u] = x;
+    a.part[((size_t)blockIdx.y * a.Fp + f0 + ff) * NTOT + UOFF + u] = x;
   }
-  if (tid == 0) a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+  if (PART == 1 && tid == 0)
+    a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+}
+
+// sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
+__global__ void k_tw_rowsum(const double *__restrict__ TW, double *__restrict__ hsum, int T,
+                            int Tp) {
+  __shared__ double s[256];
+  const double *row = TW + (size_t)blockIdx.x * Tp;
+  double x = 0.0;
+  for (int t = threadIdx.x; t < T; t += 256) x += row[t];
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) hsum[blockIdx.x] = s[0];
 }
 
 __global__ void k_loglik(const double *__restrict__ llpart, int n, double *__restrict__ out,
@@ -331,10 +390,12 @@ __global__ void k_loglik(const double *__restrict__ llpart, int n, double *__res
 // ---------------------------------------------------------------- mixing
 struct MArgs {
   const double *part;  // [nchunk][Fp][NACC]
+  const double *Wkf;   // [J][KP][Fp]   (W before the spectral update)
+  const double *hsum;  // [J][KP]       sum_t TW
   double2 *A;          // [R][2][Fp]
   double2 *rss, *rxs;  // inst: [Fp][R][R], [Fp][2][R]
   int *flags;
-  int F, Fp, J, R, nchunk, nacc, conv_update;
+  int F, Fp, J, R, nchunk, nacc, conv_update, KP;
   double invT;
   int jr[kMaxR];
 };
@@ -362,115 +423,123 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
   return make_double2((a.x * r + a.y) / d, (a.y * r - a.x) / d);
 }
 
-// One thread per bin: sufficient statistics -> hat_Rss, hat_Rxs (:698-755),
-// then for 'conv' the per-bin LAPACK-style solve of hat_Rss^T X = hat_Rxs^T
-// (:854-863); for 'inst' the per-bin statistics are stored for k_mix_inst.
-__global__ void k_mix(const MArgs a) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= a.F) return;
+// One wave per bin f: sufficient statistics -> hat_Rss, hat_Rxs (:698-755),
+// hermitised (:734-740); for 'conv' the per-bin solve hat_Rss^T X = hat_Rxs^T
+// (:854-863) by LU with partial pivoting on |re|+|im| (LAPACK zgesv), the
+// matrix entries spread over the lanes; for 'inst' the per-bin statistics are
+// stored for k_mix_inst.
+__global__ __launch_bounds__(64) void k_mix(const MArgs a) {
+  __shared__ double s_acc[4 * 10 + 8 * kMaxJ];
+  __shared__ double2 s_A[kMaxR][2];
+  __shared__ double2 s_L[kMaxR][kMaxR + 2];   // [M^T | hat_Rxs^T]
+  __shared__ double2 s_H[kMaxR][kMaxR];
+  __shared__ double2 s_mult[kMaxR];
+  __shared__ double s_sv[kMaxJ];
+  const int f = blockIdx.x, lane = threadIdx.x;
   const int J = a.J, R = a.R, NACC = a.nacc;
   const int NP = J * (J + 1) / 2;
-  double acc[4 * 10 + 9 * kMaxJ];
-  for (int u = 0; u < NACC; ++u) acc[u] = 0.0;
-  for (int c = 0; c < a.nchunk; ++c) {
-    const double *src = a.part + ((size_t)c * a.Fp + f) * NACC;
-    for (int u = 0; u < NACC; ++u) acc[u] += src[u];
+  for (int u = lane; u < NACC; u += 64) {  // NACC = 72 > 64 lanes for J = 4
+    double x = 0.0;
+    for (int c = 0; c < a.nchunk; ++c) x += a.part[((size_t)c * a.Fp + f) * NACC + u];
+    s_acc[u] = x;
   }
-  double2 Am[kMaxR][2];
-  for (int r = 0; r < R; ++r) {
-    Am[r][0] = a.A[(size_t)(2 * r) * a.Fp + f];
-    Am[r][1] = a.A[(size_t)(2 * r + 1) * a.Fp + f];
+  if (lane < 2 * R) s_A[lane >> 1][lane & 1] = a.A[(size_t)lane * a.Fp + f];
+  if (lane < J) {  // sum_t V_j(f, t) = sum_k W_j(f, k) sum_t TW_j(k, t)
+    double sv = 0.0;
+    for (int k = 0; k < a.KP; ++k)
+      sv += a.Wkf[((size_t)lane * a.KP + k) * a.Fp + f] * a.hsum[lane * a.KP + k];
+    s_sv[lane] = sv;
   }
-  double2 M[kMaxR][kMaxR];
-  for (int r1 = 0; r1 < R; ++r1) {
-    for (int r2 = 0; r2 < R; ++r2) {
-      int j1 = a.jr[r1], j2 = a.jr[r2];
-      const int lo = min(j1, j2), hi = max(j1, j2);
-      const int p = lo * J - lo * (lo - 1) / 2 + (hi - lo);
-      const double n00 = acc[4 * p], n11 = acc[4 * p + 1];
-      const double2 n01 = make_double2(acc[4 * p + 2], acc[4 * p + 3]);
-      // a_r1^H Nsum a_r2
-      const double2 c10 = cconj(Am[r1][0]), c11 = cconj(Am[r1][1]);
-      double2 v = cscale(cmul(c10, Am[r2][0]), n00);
-      v = cadd(v, cmul(cmul(c10, n01), Am[r2][1]));
-      v = cadd(v, cmul(cmul(c11, cconj(n01)), Am[r2][0]));
-      v = cadd(v, cscale(cmul(c11, Am[r2][1]), n11));
-      v = cscale(v, a.invT);
-      if (r1 == r2) v.x += acc[4 * NP + 8 * J + j1] * a.invT;
-      M[r1][r2] = v;
-    }
+  __syncthreads();
+  const int r1 = lane / R, r2 = lane % R;
+  const bool ent = lane < R * R;
+  if (ent) {
+    const int j1 = a.jr[r1], j2 = a.jr[r2];
+    const int lo = min(j1, j2), hi = max(j1, j2);
+    const int p = lo * J - lo * (lo - 1) / 2 + (hi - lo);
+    const double n00 = s_acc[4 * p], n11 = s_acc[4 * p + 1];
+    const double2 n01 = make_double2(s_acc[4 * p + 2], s_acc[4 * p + 3]);
+    const double2 c10 = cconj(s_A[r1][0]), c11 = cconj(s_A[r1][1]);
+    double2 v = cscale(cmul(c10, s_A[r2][0]), n00);               // a_r1^H Nsum a_r2
+    v = cadd(v, cmul(cmul(c10, n01), s_A[r2][1]));
+    v = cadd(v, cmul(cmul(c11, cconj(n01)), s_A[r2][0]));
+    v = cadd(v, cscale(cmul(c11, s_A[r2][1]), n11));
+    v = cscale(v, a.invT);
+    if (r1 == r2) v.x += s_sv[j1] * a.invT;
+    s_H[r1][r2] = v;
   }
-  // hermitise (:734-740)
-  for (int r1 = 0; r1 < R; ++r1)
-    for (int r2 = r1; r2 < R; ++r2) {
-      const double2 x = M[r1][r2], y = M[r2][r1];
-      M[r1][r2] = cscale(cadd(x, cconj(y)), 0.5);
-      M[r2][r1] = cscale(cadd(y, cconj(x)), 0.5);
-    }
-  double2 B[kMaxR][2];  // hat_Rxs^T
-  for (int r = 0; r < R; ++r) {
-    const double *qq = acc + 4 * NP + 8 * a.jr[r];
-    for (int c = 0; c < 2; ++c) {
-      const double2 q0 = make_double2(qq[4 * c + 0], qq[4 * c + 1]);
-      const double2 q1 = make_double2(qq[4 * c + 2], qq[4 * c + 3]);
-      B[r][c] = cscale(cadd(cmul(q0, Am[r][0]), cmul(q1, Am[r][1])), a.invT);
-    }
+  __syncthreads();
+  double2 h = make_double2(0.0, 0.0);
+  if (ent) {
+    const double2 x = s_H[r1][r2], y = s_H[r2][r1];
+    h = cscale(cadd(x, cconj(y)), 0.5);
+  }
+  if (lane < 2 * R) {  // hat_Rxs[f][c][r] = sum_c' Q_j[c][c'] A_r,c' / T
+    const int r = lane >> 1, c = lane & 1;
+    const double *qq = s_acc + 4 * NP + 8 * a.jr[r];
+    const double2 q0 = make_double2(qq[4 * c + 0], qq[4 * c + 1]);
+    const double2 q1 = make_double2(qq[4 * c + 2], qq[4 * c + 3]);
+    s_L[r][R + c] = cscale(cadd(cmul(q0, s_A[r][0]), cmul(q1, s_A[r][1])), a.invT);
   }
   if (!a.conv_update) {
+    __syncthreads();
     if (a.rss) {
-      for (int r1 = 0; r1 < R; ++r1)
-        for (int r2 = 0; r2 < R; ++r2) a.rss[((size_t)f * R + r1) * R + r2] = M[r1][r2];
-      for (int c = 0; c < 2; ++c)
-        for (int r = 0; r < R; ++r) a.rxs[((size_t)f * 2 + c) * R + r] = B[r][c];
+      if (ent) a.rss[((size_t)f * R + r1) * R + r2] = h;
+      if (lane < 2 * R) {
+        const int r = lane >> 1, c = lane & 1;
+        a.rxs[((size_t)f * 2 + c) * R + r] = s_L[r][R + c];
+      }
     }
     return;
   }
-  // solve M^T X = B (LU with partial pivoting on |re|+|im|, as LAPACK zgesv)
-  double2 L[kMaxR][kMaxR];
-  for (int r1 = 0; r1 < R; ++r1)
-    for (int r2 = 0; r2 < R; ++r2) L[r1][r2] = M[r2][r1];
+  if (ent) s_L[r2][r1] = h;  // L = hermitised(hat_Rss)^T
+  __syncthreads();
+  const int W = R + 2;
   for (int k = 0; k < R; ++k) {
-    int piv = k;
-    double best = fabs(L[k][k].x) + fabs(L[k][k].y);
-    for (int i = k + 1; i < R; ++i) {
-      const double m = fabs(L[i][k].x) + fabs(L[i][k].y);
-      if (m > best) {
-        best = m;
-        piv = i;
+    // pivot: first row i >= k maximising |re|+|im| of L[i][k]
+    double m = -1.0;
+    int mi = R;
+    if (lane >= k && lane < R) {
+      m = fabs(s_L[lane][k].x) + fabs(s_L[lane][k].y);
+      mi = lane;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double om = __shfl_xor(m, off, 64);
+      const int oi = __shfl_xor(mi, off, 64);
+      if (om > m || (om == m && oi < mi)) {
+        m = om;
+        mi = oi;
       }
     }
-    if (best == 0.0) {
-      atomicOr(a.flags, 1);
+    if (m == 0.0) {
+      if (lane == 0) atomicOr(a.flags, 1);
       return;
     }
-    if (piv != k) {
-      for (int c = 0; c < R; ++c) {
-        const double2 tmp = L[k][c];
-        L[k][c] = L[piv][c];
-        L[piv][c] = tmp;
-      }
-      for (int c = 0; c < 2; ++c) {
-        const double2 tmp = B[k][c];
-        B[k][c] = B[piv][c];
-        B[piv][c] = tmp;
-      }
+    if (mi != k && lane < W) {
+      const double2 t = s_L[k][lane];
+      s_L[k][lane] = s_L[mi][lane];
+      s_L[mi][lane] = t;
     }
-    const double2 rinv = cdiv(make_double2(1.0, 0.0), L[k][k]);
-    for (int i = k + 1; i < R; ++i) {
-      const double2 l = cmul(L[i][k], rinv);
-      for (int c = k + 1; c < R; ++c) L[i][c] = csub(L[i][c], cmul(l, L[k][c]));
-      for (int c = 0; c < 2; ++c) B[i][c] = csub(B[i][c], cmul(l, B[k][c]));
+    __syncthreads();
+    if (lane > k && lane < R) s_mult[lane] = cmul(s_L[lane][k], cdiv(make_double2(1.0, 0.0), s_L[k][k]));
+    __syncthreads();
+    const int nr = R - k - 1, nc = W - k - 1;
+    if (lane < nr * nc) {
+      const int i = k + 1 + lane / nc, c = k + 1 + lane % nc;
+      s_L[i][c] = csub(s_L[i][c], cmul(s_mult[i], s_L[k][c]));
     }
+    __syncthreads();
   }
   for (int i = R - 1; i >= 0; --i) {
-    for (int c = 0; c < 2; ++c) {
-      double2 x = B[i][c];
-      for (int q = i + 1; q < R; ++q) x = csub(x, cmul(L[i][q], B[q][c]));
-      B[i][c] = cdiv(x, L[i][i]);
+    if (lane < 2) {
+      double2 x = s_L[i][R + lane];
+      for (int q = i + 1; q < R; ++q) x = csub(x, cmul(s_L[i][q], s_L[q][R + lane]));
+      s_L[i][R + lane] = cdiv(x, s_L[i][i]);
     }
+    __syncthreads();
   }
-  for (int r = 0; r < R; ++r)
-    for (int c = 0; c < 2; ++c) a.A[(size_t)(2 * r + c) * a.Fp + f] = B[r][c];
+  if (lane < 2 * R) a.A[(size_t)lane * a.Fp + f] = s_L[lane >> 1][R + (lane & 1)];
 }
 
 // 'inst' update (:808-839): f-means of the statistics, real R_u x R_u solve.
@@ -739,8 +808,10 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
 struct RArgs {
   double2 *A, *Pinst;
   double *FB, *FW, *TW;
+  double *scal;   // [J][2 + 2*KP]: e_j, -, w_j[KP], w2_j[KP]
+  double *tpart;  // [J][nchunk] partial sums of the rescaled TW
   int *flags;
-  int F, T, Fp, Tp, KP, conv;
+  int F, T, Fp, Tp, KP, conv, nchunk, tpc;
   int K[kMaxJ], roff[kMaxJ + 1];
 };
 
@@ -756,97 +827,114 @@ __device__ double block_sum(double x, double *s) {
   return r;
 }
 
-// One 1024-thread block per source (audioModel.py:1991-2037).
-__global__ __launch_bounds__(1024) void k_renorm(const RArgs a) {
-  __shared__ double s_red[1024];
-  __shared__ double s_w[kMaxKP];
-  const int j = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+__device__ double spatial_energy(const RArgs &a, int j, double *s_red) {
   const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
-  const int K = a.K[j], KP = a.KP;
-  // spatial energy: mean |params|^2
   double e = 0.0;
   if (a.conv) {
     const int n = nr * 2 * a.F;
-    for (int idx = tid; idx < n; idx += nt) {
+    for (int idx = threadIdx.x; idx < n; idx += blockDim.x) {
       const int f = idx % a.F, rc = idx / a.F;
       const double2 x = a.A[(size_t)(2 * r0 + rc) * a.Fp + f];
       e += x.x * x.x + x.y * x.y;
     }
-    e = block_sum(e, s_red) / (double)n;
-  } else {
-    for (int idx = tid; idx < nr * 2; idx += nt) {
-      const double2 x = a.Pinst[2 * r0 + idx];
-      e += x.x * x.x + x.y * x.y;
-    }
-    e = block_sum(e, s_red) / (double)(nr * 2);
+    return block_sum(e, s_red) / (double)n;
   }
-  const double se = sqrt(e);
-  if (a.conv) {
-    const int n = nr * 2 * a.F;
-    for (int idx = tid; idx < n; idx += nt) {
-      const int f = idx % a.F, rc = idx / a.F;
-      double2 *p = a.A + (size_t)(2 * r0 + rc) * a.Fp + f;
+  for (int idx = threadIdx.x; idx < nr * 2; idx += blockDim.x) {
+    const double2 x = a.Pinst[2 * r0 + idx];
+    e += x.x * x.x + x.y * x.y;
+  }
+  return block_sum(e, s_red) / (double)(nr * 2);
+}
+
+// renormalize_parameters (audioModel.py:1991-2037), stage 1: one 256-thread
+// block per (source j, NMF column k): e_j = mean|params_j|^2 (recomputed per
+// block, it is tiny), FB[:,k] *= e_j, w = max_f FB[:,k] (0 -> 1), FB[:,k] /= w.
+__global__ __launch_bounds__(256) void k_renorm_fb(const RArgs a) {
+  __shared__ double s_red[256];
+  const int j = blockIdx.y, k = blockIdx.x;
+  const double e = spatial_energy(a, j, s_red);
+  if (k >= a.K[j]) return;
+  double *col = a.FB + (size_t)j * a.Fp * a.KP + k;
+  double m = -INFINITY;
+  for (int f = threadIdx.x; f < a.F; f += blockDim.x) {
+    const double x = col[(size_t)f * a.KP] * e;
+    col[(size_t)f * a.KP] = x;
+    m = fmax(m, x);
+  }
+  s_red[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  const double wk = s_red[0] == 0.0 ? 1.0 : s_red[0];
+  for (int f = threadIdx.x; f < a.F; f += blockDim.x) col[(size_t)f * a.KP] /= wk;
+  if (threadIdx.x == 0) {
+    double *sc = a.scal + (size_t)j * (2 + 2 * a.KP);
+    sc[2 + k] = wk;
+    if (k == 0) sc[0] = e;
+  }
+}
+
+// stage 2: one block per (source, frame chunk): FW *= w (rows), w2 = mean
+// over rows, FW /= w2 (chunk 0 writes FW, the others recompute w2), TW[:,
+// chunk] *= w2, params /= sqrt(e) (chunk 0), partial sum of TW.
+__global__ __launch_bounds__(256) void k_renorm_tw(const RArgs a) {
+  __shared__ double s_red[256];
+  __shared__ double s_w2[kMaxKP];
+  const int j = blockIdx.y, chunk = blockIdx.x;
+  const int K = a.K[j], KP = a.KP;
+  const double *sc = a.scal + (size_t)j * (2 + 2 * KP);
+  double *FW = a.FW + (size_t)j * KP * KP;
+  if (threadIdx.x < K) {
+    const int c = threadIdx.x;
+    double s = 0.0;
+    for (int r = 0; r < K; ++r) s += FW[r * KP + c] * sc[2 + r];
+    s /= (double)K;
+    s_w2[c] = s == 0.0 ? 1.0 : s;
+  }
+  __syncthreads();
+  if (chunk == 0) {
+    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+      const int r = idx / K, c = idx % K;
+      FW[r * KP + c] = (FW[r * KP + c] * sc[2 + r]) / s_w2[c];
+    }
+    const double se = sqrt(sc[0]);
+    const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+    if (a.conv) {
+      for (int idx = threadIdx.x; idx < nr * 2 * a.F; idx += blockDim.x) {
+        const int f = idx % a.F, rc = idx / a.F;
+        double2 *p = a.A + (size_t)(2 * r0 + rc) * a.Fp + f;
+        *p = make_double2(p->x / se, p->y / se);
+      }
+    } else if (threadIdx.x < nr * 2) {
+      double2 *p = a.Pinst + 2 * r0 + threadIdx.x;
       *p = make_double2(p->x / se, p->y / se);
     }
-  } else if (tid < nr * 2) {
-    double2 *p = a.Pinst + 2 * r0 + tid;
-    *p = make_double2(p->x / se, p->y / se);
-  }
-  // FB *= e ; w = max_f FB ; FB /= w ; FW *= w[:,None]
-  double *FB = a.FB + (size_t)j * a.Fp * KP;
-  const int groups = nt / KP;
-  {
-    const int k = tid % KP, g = tid / KP;
-    double m = -INFINITY;
-    if (g < groups && k < K)
-      for (int f = g; f < a.F; f += groups) {
-        double *p = FB + (size_t)f * KP + k;
-        const double x = *p * e;
-        *p = x;
-        m = fmax(m, x);
-      }
-    s_red[tid] = m;
-  }
-  __syncthreads();
-  if (tid < K) {
-    double m = -INFINITY;
-    for (int g = 0; g < groups; ++g) m = fmax(m, s_red[g * KP + tid]);
-    s_w[tid] = m == 0.0 ? 1.0 : m;
-  }
-  __syncthreads();
-  for (int idx = tid; idx < a.F * K; idx += nt) {
-    const int f = idx / K, k = idx % K;
-    FB[(size_t)f * KP + k] /= s_w[k];
-  }
-  double *FW = a.FW + (size_t)j * KP * KP;
-  for (int idx = tid; idx < K * K; idx += nt) {
-    const int r = idx / K, c = idx % K;
-    FW[r * KP + c] *= s_w[r];
-  }
-  __syncthreads();
-  // w2 = FW.mean(axis=0) ; FW /= w2 ; TW *= w2[:,None]
-  if (tid < K) {
-    double s = 0.0;
-    for (int r = 0; r < K; ++r) s += FW[r * KP + tid];
-    s /= (double)K;
-    s_w[tid] = s == 0.0 ? 1.0 : s;
-  }
-  __syncthreads();
-  for (int idx = tid; idx < K * K; idx += nt) {
-    const int r = idx / K, c = idx % K;
-    FW[r * KP + c] /= s_w[c];
   }
   double *TW = a.TW + (size_t)j * KP * a.Tp;
+  const int t0 = chunk * a.tpc, t1 = min(t0 + a.tpc, a.T);
+  const int w = t1 - t0;
   double tsum = 0.0;
-  for (int idx = tid; idx < K * a.T; idx += nt) {
-    const int k = idx / a.T, t = idx % a.T;
-    double *p = TW + (size_t)k * a.Tp + t;
-    const double x = *p * s_w[k];
-    *p = x;
-    tsum += x;
-  }
+  if (w > 0)
+    for (int idx = threadIdx.x; idx < K * w; idx += blockDim.x) {
+      const int k = idx / w, t = t0 + idx % w;
+      double *p = TW + (size_t)k * a.Tp + t;
+      const double x = *p * s_w2[k];
+      *p = x;
+      tsum += x;
+    }
   tsum = block_sum(tsum, s_red);
-  if (tid == 0) a.flags[1 + j] = tsum < kEps ? 1 : 0;
+  if (threadIdx.x == 0) a.tpart[(size_t)j * a.nchunk + chunk] = tsum;
+}
+
+// stage 3: sum(TW_j) < eps -> host-side random restart (audioModel.py:2023)
+__global__ void k_renorm_flags(const RArgs a, int J) {
+  const int j = threadIdx.x;
+  if (j >= J) return;
+  double s = 0.0;
+  for (int c = 0; c < a.nchunk; ++c) s += a.tpart[(size_t)j * a.nchunk + c];
+  a.flags[1 + j] = s < kEps ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- host side
@@ -908,7 +996,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   c->J = J;
   c->R = R;
   c->conv = conv;
-  c->KP = round_up(kmax, 16);
+  c->KP = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : 64);
   c->roff[0] = 0;
   for (int j = 0; j < J; ++j) {
     c->rank[j] = rank[j];
@@ -926,7 +1014,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
     c->tpc_b /= 2;
   c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
   const int NP = J * (J + 1) / 2;
-  c->nacc = 4 * NP + 9 * J;
+  c->nacc = 4 * NP + 8 * J;
   int st;
 #define ALLOC(buf, n) \
   if ((st = c->buf.alloc(n)) != FASST_OK) return st
@@ -947,6 +1035,10 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
   ALLOC(flags, 1 + kMaxJ);
+  ALLOC(hsum, (size_t)J * KP);
+  c->nchunk_r = std::max(1, std::min(64, (c->T + 255) / 256));
+  ALLOC(rscal, (size_t)J * (2 + 2 * KP));
+  ALLOC(rtpart, (size_t)J * c->nchunk_r);
 #undef ALLOC
   c->configured = 1;
   return FASST_OK;
@@ -978,6 +1070,8 @@ static int launch_renorm(fasst_ctx *c) {
   r.FB = c->FB.p;
   r.FW = c->FW.p;
   r.TW = c->TW.p;
+  r.scal = c->rscal.p;
+  r.tpart = c->rtpart.p;
   r.flags = c->flags.p;
   r.F = c->F;
   r.T = c->T;
@@ -985,25 +1079,65 @@ static int launch_renorm(fasst_ctx *c) {
   r.Tp = c->Tp;
   r.KP = c->KP;
   r.conv = c->conv;
+  r.nchunk = c->nchunk_r;
+  r.tpc = (c->T + c->nchunk_r - 1) / c->nchunk_r;
   for (int j = 0; j < kMaxJ; ++j) r.K[j] = j < c->J ? c->K[j] : 0;
   for (int j = 0; j <= kMaxJ; ++j) r.roff[j] = j <= c->J ? c->roff[j] : c->R;
   prof_begin(c, KREN);
-  k_renorm<<<c->J, 1024, 0, c->stream>>>(r);
+  k_renorm_fb<<<dim3(c->KP, c->J), 256, 0, c->stream>>>(r);
+  k_renorm_tw<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
+  k_renorm_flags<<<1, 64, 0, c->stream>>>(r, c->J);
   prof_end(c, KREN);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
 }
 
-template <int J>
-static void launch_estep(fasst_ctx *c, const EArgs &e) {
-  const size_t smem =
-      (size_t)(kMaxR * 4 * 16 + J * 4 * 16 + 4 +
-               std::max(J * c->KP * 16, 4 * (4 * (J * (J + 1) / 2) + 9 * J) * 16)) *
-      sizeof(double);
+template <int J, int NKS, int RKU, int AB>
+static void launch_estep_t(fasst_ctx *c, const EArgs &e) {
+  constexpr int NP = J * (J + 1) / 2;
+  const size_t base = (size_t)(kMaxR * 4 * 16 + J * 4 * 16 + 4);
+  const size_t sm1 = (base + std::max(J * 4 * NKS * 16, 4 * (4 * NP) * 16)) * sizeof(double);
+  const size_t sm2 = (base + std::max(J * 4 * NKS * 16, 4 * (8 * J) * 16)) * sizeof(double);
   dim3 grid(c->nft, c->nchunk_e);
   prof_begin(c, KESTEP);
-  k_estep<J><<<grid, 256, smem, c->stream>>>(e);
+  k_estep<J, NKS, RKU, 1, AB><<<grid, 256, sm1, c->stream>>>(e);
+  k_estep<J, NKS, RKU, 2, AB><<<grid, 256, sm2, c->stream>>>(e);
   prof_end(c, KESTEP);
+}
+
+template <int J, int NKS>
+static void launch_estep_r(fasst_ctx *c, const EArgs &e) {
+  bool all1 = true, all2 = true;
+  for (int j = 0; j < J; ++j) {
+    all1 &= c->rank[j] == 1;
+    all2 &= c->rank[j] == 2;
+  }
+  if (all1)
+    launch_estep_t<J, NKS, 1, 0>(c, e);
+  else if (all2)
+    launch_estep_t<J, NKS, 2, 0>(c, e);
+  else
+    launch_estep_t<J, NKS, 0, 0>(c, e);
+}
+
+template <int J>
+static void launch_estep(fasst_ctx *c, const EArgs &e) {
+  bool all2 = true;
+  for (int j = 0; j < J; ++j) all2 &= c->rank[j] == 2;
+  if (J == 4 && c->KP == 32 && all2 && c->ablate) {  // profiling builds only
+    switch (c->ablate) {
+      case 1: launch_estep_t<4, 8, 2, 1>(c, e); return;
+      case 2: launch_estep_t<4, 8, 2, 2>(c, e); return;
+      case 4: launch_estep_t<4, 8, 2, 4>(c, e); return;
+      case 7: launch_estep_t<4, 8, 2, 7>(c, e); return;
+      default: break;
+    }
+  }
+  switch (c->KP) {
+    case 16: launch_estep_r<J, 4>(c, e); break;
+    case 32: launch_estep_r<J, 8>(c, e); break;
+    default: launch_estep_r<J, 16>(c, e); break;
+  }
 }
 
 template <int NKC>
@@ -1025,8 +1159,8 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   int st = launch_w_old(c);
   if (st) return st;
   prof_begin(c, KFWH);
-  k_fwh_t<<<launch_grid((size_t)J * c->Tp * c->KP), 256, 0, c->stream>>>(c->FW.p, c->TW.p,
-                                                                        c->FWHt.p, J, c->Tp, c->KP);
+  k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, (size_t)(c->KP * c->KP + c->KP * 64) * sizeof(double),
+            c->stream>>>(c->FW.p, c->TW.p, c->FWHt.p, J, c->Tp, c->KP);
   prof_end(c, KFWH);
   st = build_inst_A(c);
   if (st) return st;
@@ -1059,6 +1193,8 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     default: launch_estep<4>(c, e); break;
   }
   FASST_LAUNCH_CHECK();
+  k_tw_rowsum<<<J * c->KP, 256, 0, c->stream>>>(c->TW.p, c->hsum.p, c->T, c->Tp);
+  FASST_LAUNCH_CHECK();
   prof_begin(c, KLL);
   k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
                                      1.0 / ((double)c->F * (double)c->T));
@@ -1073,6 +1209,9 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   if (any_free) {
     MArgs m;
     m.part = c->epart.p;
+    m.Wkf = c->Wkf.p;
+    m.hsum = c->hsum.p;
+    m.KP = c->KP;
     m.A = c->A.p;
     m.rss = c->rss.p;
     m.rxs = c->rxs.p;
@@ -1088,7 +1227,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     for (int j = 0; j < J; ++j)
       for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
     prof_begin(c, KMIX);
-    k_mix<<<(c->F + 63) / 64, 64, 0, c->stream>>>(m);
+    k_mix<<<c->F, 64, 0, c->stream>>>(m);
     prof_end(c, KMIX);
     FASST_LAUNCH_CHECK();
     if (!c->conv) {
@@ -1221,6 +1360,7 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->nft = c->Fp / kTile;
   c->ntt = c->Tp / kTile;
   int st = FASST_OK;
+  if (const char *ab = getenv("FASST_ABLATE")) c->ablate = atoi(ab);  // profiling only
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     set_error("hipStreamCreate failed");
     st = FASST_ERR_DEVICE;
@@ -1271,6 +1411,9 @@ int fasst_destroy(fasst_ctx *c) {
     c->rss.release();
     c->rxs.release();
     c->flags.release();
+    c->hsum.release();
+    c->rscal.release();
+    c->rtpart.release();
     for (int i = 0; i < fasst_ctx::kNK; ++i) {
       if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
       if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -1429,7 +1572,7 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
                              hipMemcpyDeviceToHost, c->stream));
     FASST_HIP(hipStreamSynchronize(c->stream));
     prof_collect(c);
-    if (c->h_flags[0]) {
+    if (c->h_flags[0] && !c->ablate) {
       set_error("Singular Matrix");
       return FASST_ERR_SINGULAR;
     }

@@ -1,0 +1,17 @@
+#!/bin/bash
+# rocprofv3 passes for the bench workload: kernel trace + stats, then one PMC
+# pass per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass).
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+OUT="$R/gpurun_out/${PROF_TAG:-prof}"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+ARGS="--steps ${STEPS:-10} --warmup 2 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+  -- python3 "$R/bench.py" $ARGS > "$OUT/bench_trace.log" 2>&1
+rc=$?; echo "trace rc=$rc"; tail -2 "$OUT/bench_trace.log"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
+  -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_fetch.log" 2>&1
+rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
+  -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_write.log" 2>&1
+rc=$?; echo "write rc=$rc"; exit $rc
