@@ -158,13 +158,24 @@ def main():
         work = kernel_work(m.nbFreqsSigRepr, m.nbFramesSigRepr, J_SRC, R, K_NMF)
         dom = max(times, key=lambda k: times[k][0])
         rl = None
+        pmc = None
+        pmc_path = os.environ.get("FASST_PMC_JSON", os.path.join(ROOT, "profiles", "r1_bench.json"))
+        if os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))["kernels"]
+            except Exception:
+                pmc = None
         if dom in work:
             sec = times[dom][0] * 1e-3
             achieved = work[dom]["flops"] / sec / 1e12
+            traffic = None
+            if pmc and dom in pmc and pmc[dom].get("hbm_bytes_per_launch"):
+                traffic = pmc[dom]["hbm_bytes_per_launch"]
             rl = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_MFMA_PEAK / 1e12,
                   "unit": "TFLOP/s", "frac": round(achieved * 1e12 / FP64_MFMA_PEAK, 4),
-                  "traffic": None, "kernel": dom, "kernel_ms": round(times[dom][0], 4),
-                  "dtype": "f64"}
+                  "traffic": traffic, "kernel": dom, "kernel_ms": round(times[dom][0], 4),
+                  "dtype": "f64", "algorithmic_bytes": work[dom]["bytes"],
+                  "traffic_source": os.path.relpath(pmc_path, ROOT) if traffic else None}
         out = {
             "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",
             "value": round(world * args.steps / dt, 4),
