@@ -95,6 +95,31 @@ def cpu_baseline(T_sample=1000):
                                            T_FRAMES, cores)}
 
 
+def rank_setup(env=None):
+    """(world, rank, local_rank, data_seed, device) of this process: one clip per
+    GPU, data seed = global rank, device = local rank (torchrun env vars)."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", "0"))
+    return world, rank, local, rank, local
+
+
+def max_over_ranks(dt, dist=None, device="cpu"):
+    """Wall time of the slowest rank (the whole job's time)."""
+    if dist is None:
+        return dt
+    import torch
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_value(world, steps, dt_max):
+    """Whole-job throughput: iterations of all clips / slowest rank's time."""
+    return world * steps / dt_max
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,9 +129,7 @@ def main():
     ap.add_argument("--T", type=int, default=T_FRAMES)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local, seed, device = rank_setup()
     dist = None
     if world > 1:
         import torch
@@ -114,7 +137,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
 
-    m = build_model(seed=rank, device=local, T=args.T)
+    m = build_model(seed=seed, device=device, T=args.T)
     eng = m._engine
     order, Ks, conv = m._upload()
     rows_w = psd_schedule(m, max(args.warmup, 1))
@@ -140,12 +163,7 @@ def main():
             m._restart_tw(mask, order)
             order, Ks, conv = m._upload()
     barrier_sync()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda:%d" % local)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(time.perf_counter() - t0, dist, "cuda:%d" % local)
 
     # per-kernel HIP-event timing on the engine's stream (separate, untimed pass)
     eng.set_profiling(True)
@@ -178,7 +196,7 @@ def main():
                   "traffic_source": os.path.relpath(pmc_path, ROOT) if traffic else None}
         out = {
             "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",
-            "value": round(world * args.steps / dt, 4),
+            "value": round(job_value(world, args.steps, dt), 4),
             "unit": "EM it/s",
             "n_gpus": world,
             "steps": args.steps,
