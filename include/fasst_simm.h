@@ -1,0 +1,68 @@
+/*
+ * fasst_simm.h -- C ABI of the SIMM source/filter engine (libfasst_hip.so).
+ *
+ * Replaces the multiplicative-update loops of the reference's
+ * SeparateLeadStereo/SIMM/SIMM.py:
+ *   Stereo_SIMM (SIMM.py:397-943)  -> simm_create(stereo=1) + simm_run
+ *   SIMM        (SIMM.py:46-395)   -> simm_create(stereo=0) + simm_run
+ * The random initialisation stays on the host (it draws from NumPy's global
+ * stream in the reference, SIMM.py:200-255 / :525-576), so the Python host
+ * side (pyfasst_amd/SeparateLeadStereo/SIMM/SIMM.py) reproduces it exactly
+ * and hands the initial parameters over with simm_set_params.
+ *
+ * Conventions are those of fasst_hip.h: float64, C order, host arrays copied
+ * in and out, status codes FASST_*, message in fasst_last_error().
+ *   SXR, SXL : [F][N]   power spectrograms (mono: SXR only, SXL NULL)
+ *   WF0      : [F][NF0] source comb dictionary
+ *   WGAMMA   : [F][P]   smooth filter atoms
+ *   HGAMMA [P][K], HPHI [K][N], HF0 [NF0][N], HM [R][N], WM [F][R]
+ *   alpha [2] = (alphaR, alphaL), betaR/betaL [R] (the diagonals the
+ *   reference returns as np.diag matrices, SIMM.py:943)
+ */
+#ifndef FASST_SIMM_H
+#define FASST_SIMM_H
+
+#include "fasst_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct simm_ctx simm_ctx;
+
+/* sizes of SIMM.py:498-504 / :147-153; K <= 8, P*K <= 512.  Mono needs
+ * R == 1 or R == N (quirk N7, SIMM.py:388), else FASST_ERR_SHAPE.        */
+int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int stereo,
+                simm_ctx **out);
+int simm_destroy(simm_ctx *ctx);
+
+/* the data to be fitted and the fixed dictionaries (SIMM.py:397-403) */
+int simm_set_data(simm_ctx *ctx, const double *SXR, const double *SXL, const double *WF0,
+                  const double *WGAMMA);
+
+/* initial parameters (SIMM.py:525-576); alpha and betaR are read for stereo
+ * only (alpha = (0.5, 0.5) in the reference, betaL = 1 - betaR, :575-576).
+ * Builds WPHI, SF0, SPHI and the model spectrograms (:578-585).           */
+int simm_set_params(simm_ctx *ctx, const double *HGAMMA, const double *HPHI, const double *HF0,
+                    const double *HM, const double *WM, const double *alpha,
+                    const double *betaR);
+
+/* n_iter iterations of the reference loop body (:613-941 / :278-393);
+ * omega = updateRulePower; update_hgamma = updateHGAMMA (stereo only).
+ * reco_err (may be NULL): [2*n_iter] Itakura-Saito errors after the HF0 and
+ * the HPHI update of each iteration (computeError=True, :676-683, :721-728). */
+int simm_run(simm_ctx *ctx, int n_iter, double omega, int update_hgamma, double *reco_err);
+
+/* ISDistortion(SXR, hatSXR) [+ ISDistortion(SXL, hatSXL)] of the current
+ * model (SIMM.py:34-44, :602-603)                                          */
+int simm_reco_error(simm_ctx *ctx, double *out);
+
+/* current parameters; any pointer may be NULL (alpha/beta: stereo only) */
+int simm_get_params(simm_ctx *ctx, double *HGAMMA, double *HPHI, double *HF0, double *HM,
+                    double *WM, double *alpha, double *betaR, double *betaL);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FASST_SIMM_H */

@@ -1,4 +1,5 @@
-"""ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h).
+"""ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h and
+include/fasst_simm.h).
 
 The product path has no CPU fallback: if the HIP library is missing this
 module raises at import time, and every compute call raises if the device
@@ -32,7 +33,7 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
 
-# name -> (restype, argtypes); must match include/fasst_hip.h exactly
+# name -> (restype, argtypes); must match include/*.h exactly
 SIGNATURES = {
     "fasst_last_error": (ctypes.c_char_p, []),
     "fasst_device_count": (ctypes.c_int, [_ip]),
@@ -62,6 +63,14 @@ SIGNATURES = {
     "fasst_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
     "fasst_inv_herm_mat_2d": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp,
                                              _dp]),
+    # include/fasst_simm.h
+    "simm_create": (ctypes.c_int, [ctypes.c_int] * 8 + [ctypes.POINTER(_vp)]),
+    "simm_destroy": (ctypes.c_int, [_vp]),
+    "simm_set_data": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp]),
+    "simm_set_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    "simm_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_int, _dp]),
+    "simm_reco_error": (ctypes.c_int, [_vp, _dp]),
+    "simm_get_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -1,0 +1,904 @@
+// SIMM source/filter multiplicative updates on MI355X (gfx950), FP64.
+//
+// Restates SeparateLeadStereo/SIMM/SIMM.py: Stereo_SIMM (:397-943) and SIMM
+// (:46-395).  The per-iteration update order is the reference's: HF0, HPHI,
+// HM, HGAMMA, WM, (stereo) alpha, beta, each followed by the model refresh
+//   hatSX_R = max(WM diag(bR^2) HM + aR^2 SF0*SPHI, eps)
+//   hatSX_L = max(aL^2 SF0*SPHI + WM diag(bL^2) HM, eps).
+// The F x NF0 x N products (WF0^T X, WF0 HF0) run on the FP64 MFMA GEMM of
+// fasst_gemm.h; elementwise ratios, skinny products (K = 4 filters) and the
+// renormalisations are fused VALU kernels.  One deliberate shortcut: after
+// HPHI / HGAMMA renormalise the columns of HF0 (HF0 *= s), SF0 = WF0 HF0 is
+// updated as SF0 *= s (the same linear map; the reference recomputes the
+// GEMM) -- it saves two F x NF0 x N GEMMs per iteration.
+#include "fasst_gemm.h"
+
+#include <cmath>
+
+#include "../../include/fasst_simm.h"
+
+namespace fasst {
+
+constexpr double kSimmEps = 1e-20;  // SIMM.py:150, :506
+
+// ------------------------------------------------------------------ GEMM host
+__global__ void k_gemm_reduce(const double *__restrict__ part, int nz, size_t slab,
+                              double *__restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int z = 0; z < nz; ++z) s += part[z * slab + i];
+    out[i] = s;
+  }
+}
+
+GemmPlan gemm_plan(int M, int N, int K) {
+  GemmPlan p;
+  const long tiles = (long)((M + kGBM - 1) / kGBM) * ((N + kGBN - 1) / kGBN);
+  int nz = 1;
+  while (tiles * nz < 512 && K / (nz * 2) >= 256) nz *= 2;
+  p.nz = nz;
+  p.kchunk = ((K + nz - 1) / nz + kGBK - 1) / kGBK * kGBK;
+  p.nz = (K + p.kchunk - 1) / p.kchunk;
+  if (p.nz < 1) p.nz = 1;
+  return p;
+}
+
+template <bool TA, bool TB, int NB>
+int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ldb, double *const *C,
+         int ldc, int M, int N, int K, double *work) {
+  GemmPlan p = gemm_plan(M, N, K);
+  GemmArgs g;
+  g.A = A;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.kchunk = p.kchunk;
+  if (p.nz == 1 || !work) {
+    g.kchunk = K;
+    g.ldc = ldc;
+    g.slab = 0;
+    for (int b = 0; b < NB; ++b) {
+      g.B[b] = B[b];
+      g.C[b] = C[b];
+    }
+    dim3 grid((N + kGBN - 1) / kGBN, (M + kGBM - 1) / kGBM, 1);
+    k_gemm<TA, TB, NB><<<grid, 256, 0, s>>>(g);
+    FASST_LAUNCH_CHECK();
+    return FASST_OK;
+  }
+  // split-K into work slabs laid out [NB][nz][M][N] (ldc = N)
+  const size_t slab = (size_t)M * N;
+  g.ldc = N;
+  g.slab = slab;
+  for (int b = 0; b < NB; ++b) {
+    g.B[b] = B[b];
+    g.C[b] = work + (size_t)b * p.nz * slab;
+  }
+  dim3 grid((N + kGBN - 1) / kGBN, (M + kGBM - 1) / kGBM, p.nz);
+  k_gemm<TA, TB, NB><<<grid, 256, 0, s>>>(g);
+  FASST_LAUNCH_CHECK();
+  for (int b = 0; b < NB; ++b) {
+    if (ldc == N) {
+      k_gemm_reduce<<<(int)std::min<size_t>((slab + 255) / 256, 4096), 256, 0, s>>>(
+          work + (size_t)b * p.nz * slab, p.nz, slab, C[b], slab);
+    } else {
+      return FASST_ERR_SHAPE;  // split-K outputs must be dense
+    }
+    FASST_LAUNCH_CHECK();
+  }
+  return FASST_OK;
+}
+
+size_t gemm_workspace(int M, int N, int K, int NB) {
+  GemmPlan p = gemm_plan(M, N, K);
+  return p.nz > 1 ? (size_t)NB * p.nz * M * N : 0;
+}
+
+// ------------------------------------------------------------------ kernels
+#define GRID_STRIDE(i, n)                                                          \
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)(n); \
+       i += (size_t)gridDim.x * blockDim.x)
+
+static inline int egrid(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 8192); }
+
+// ratio^omega with the reference's `** omega` (omega == 1 is exact)
+__device__ __forceinline__ double powo(double x, double omega) {
+  return omega == 1.0 ? x : pow(x, omega);
+}
+
+// HF0 / HPHI / HGAMMA ratios, stereo (SIMM.py:623-630, :688-694):
+//   com = aR2*Z/max(hR), den = aL2*Z/max(hL), num = com*SXR/max(hR) + den*SXL/max(hL), den += com
+// mono (SIMM.py:282-283): den = Z/max(hat), num = (den*SX)/max(hat)
+__global__ void k_simm_numden(const double *__restrict__ Z, const double *__restrict__ hR,
+                              const double *__restrict__ hL, const double *__restrict__ SXR,
+                              const double *__restrict__ SXL, const double *__restrict__ alpha,
+                              double *__restrict__ num, double *__restrict__ den, size_t n,
+                              int stereo) {
+  if (stereo) {
+    const double aR2 = alpha[0] * alpha[0], aL2 = alpha[1] * alpha[1];
+    GRID_STRIDE(i, n) {
+      const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
+      const double com = aR2 * Z[i] / mr;
+      const double d = aL2 * Z[i] / ml;
+      num[i] = com * SXR[i] / mr + d * SXL[i] / ml;
+      den[i] = d + com;
+    }
+  } else {
+    GRID_STRIDE(i, n) {
+      const double m = fmax(hR[i], kSimmEps);
+      const double d = Z[i] / m;
+      den[i] = d;
+      num[i] = (d * SXR[i]) / m;
+    }
+  }
+}
+
+// X *= (num / max(den, eps))^omega ; optional floor max(X, eps) (mono HM)
+__global__ void k_mu_apply(double *__restrict__ X, const double *__restrict__ num,
+                           const double *__restrict__ den, size_t n, double omega, int floor_eps) {
+  GRID_STRIDE(i, n) {
+    double x = X[i] * powo(num[i] / fmax(den[i], kSimmEps), omega);
+    if (floor_eps) x = fmax(x, kSimmEps);
+    X[i] = x;
+  }
+}
+
+// HM (stereo, :747-758): HM *= ((nR + nL) / max(dR + dL, eps))^omega with
+// nR = (WM bR^2)^T XR etc. given as unscaled products P_* = WM^T X_*.
+__global__ void k_hm_apply(double *__restrict__ HM, const double *__restrict__ PnR,
+                           const double *__restrict__ PdR, const double *__restrict__ PnL,
+                           const double *__restrict__ PdL, const double *__restrict__ bR,
+                           const double *__restrict__ bL, int R, int N, double omega) {
+  GRID_STRIDE(i, (size_t)R * N) {
+    const int r = i / N;
+    const double br = bR[r] * bR[r], bl = bL[r] * bL[r];
+    const double num = br * PnR[i] + bl * PnL[i];
+    const double den = br * PdR[i] + bl * PdL[i];
+    HM[i] *= powo(num / fmax(den, kSimmEps), omega);
+  }
+}
+
+// hat refresh: optional SF0 column scale, optional SPHI = WPHI HPHI (K small)
+__global__ void k_simm_refresh(double *__restrict__ SF0, double *__restrict__ SPHI,
+                               const double *__restrict__ WPHI, const double *__restrict__ HPHI,
+                               const double *__restrict__ colscale, const double *__restrict__ SMR,
+                               const double *__restrict__ SML, const double *__restrict__ alpha,
+                               double *__restrict__ hR, double *__restrict__ hL, int F, int N,
+                               int K, int stereo, int recompute_sphi) {
+  const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
+  const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
+  GRID_STRIDE(i, (size_t)F * N) {
+    const int f = i / N, n = i % N;
+    double sf = SF0[i];
+    if (colscale) {
+      sf *= colscale[n];
+      SF0[i] = sf;
+    }
+    double sp;
+    if (recompute_sphi) {
+      sp = 0.0;
+      for (int k = 0; k < K; ++k) sp += WPHI[f * K + k] * HPHI[(size_t)k * N + n];
+      SPHI[i] = sp;
+    } else {
+      sp = SPHI[i];
+    }
+    const double l = sf * sp;
+    if (stereo) {
+      hR[i] = fmax(SMR[i] + aR2 * l, kSimmEps);
+      hL[i] = fmax(l * aL2 + SML[i], kSimmEps);
+    } else {
+      hR[i] = fmax(l + SMR[i], kSimmEps);
+    }
+  }
+}
+
+// stereo: X = SX/max(h^2, eps), Y = 1/max(h, eps)             (:747-753)
+// mono:   Y = 1/max(h, eps), X = (Y*SX)/max(h, eps)               (:318-321)
+__global__ void k_simm_xy(const double *__restrict__ h, const double *__restrict__ SX,
+                          double *__restrict__ X, double *__restrict__ Y, size_t n, int stereo) {
+  GRID_STRIDE(i, n) {
+    const double hv = h[i];
+    const double y = 1.0 / fmax(hv, kSimmEps);
+    X[i] = stereo ? SX[i] / fmax(hv * hv, kSimmEps) : (y * SX[i]) / fmax(hv, kSimmEps);
+    Y[i] = y;
+  }
+}
+
+// HPHI numerator/denominator: out[m][n] = sum_f WPHI[f][m] * {num,den}(f, n),
+// num/den built on the fly from Z = SF0 (:688-694).  Block: 256 frames x one
+// f-chunk; partials [chunk][2][K][N].
+__global__ __launch_bounds__(256) void k_hphi_partial(
+    const double *__restrict__ Z, const double *__restrict__ hR, const double *__restrict__ hL,
+    const double *__restrict__ SXR, const double *__restrict__ SXL,
+    const double *__restrict__ alpha, const double *__restrict__ WPHI, double *__restrict__ part,
+    int F, int N, int K, int fchunk, int stereo) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  const int fb = c * fchunk, fe = min(F, fb + fchunk);
+  double sn[8], sd[8];
+  for (int k = 0; k < 8; ++k) sn[k] = sd[k] = 0.0;
+  if (n < N) {
+    const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
+    const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
+    for (int f = fb; f < fe; ++f) {
+      const size_t i = (size_t)f * N + n;
+      double num, den;
+      if (stereo) {
+        const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
+        const double com = aR2 * Z[i] / mr;
+        const double d = aL2 * Z[i] / ml;
+        num = com * SXR[i];
+        num /= mr;
+        num += d * SXL[i] / ml;
+        den = d + com;
+      } else {
+        const double m = fmax(hR[i], kSimmEps);
+        den = Z[i] / m;
+        num = (den * SXR[i]) / m;
+      }
+      for (int k = 0; k < K; ++k) {
+        const double w = WPHI[f * K + k];
+        sn[k] += w * num;
+        sd[k] += w * den;
+      }
+    }
+    for (int k = 0; k < K; ++k) {
+      part[(((size_t)c * 2 + 0) * K + k) * N + n] = sn[k];
+      part[(((size_t)c * 2 + 1) * K + k) * N + n] = sd[k];
+    }
+  }
+}
+
+// HPHI *= (num/max(den,eps))^omega; s = column sums; HPHI[:, s>0] /= s
+__global__ void k_hphi_update(double *__restrict__ HPHI, const double *__restrict__ part,
+                              int nchunk, double *__restrict__ s_out, int K, int N,
+                              double omega) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int k = 0; k < K; ++k) {
+    double num = 0.0, den = 0.0;
+    for (int c = 0; c < nchunk; ++c) {
+      num += part[(((size_t)c * 2 + 0) * K + k) * N + n];
+      den += part[(((size_t)c * 2 + 1) * K + k) * N + n];
+    }
+    double h = HPHI[(size_t)k * N + n] * powo(num / fmax(den, kSimmEps), omega);
+    HPHI[(size_t)k * N + n] = h;
+    s += h;
+  }
+  if (s > 0)
+    for (int k = 0; k < K; ++k) HPHI[(size_t)k * N + n] /= s;
+  s_out[n] = s;
+}
+
+// X[r][n] *= s[n] over R rows (column scale)
+__global__ void k_colscale(double *__restrict__ X, const double *__restrict__ s, int R, int N) {
+  GRID_STRIDE(i, (size_t)R * N) X[i] *= s[i % N];
+}
+
+// HGAMMA numerator/denominator rows: out[f][k] = sum_n {num,den}(f, n) HPHI[k][n]
+// (np.dot(tempNumFbyN, HPHI.T), :802); one block per bin f.
+__global__ __launch_bounds__(256) void k_hgamma_rows(
+    const double *__restrict__ Z, const double *__restrict__ hR, const double *__restrict__ hL,
+    const double *__restrict__ SXR, const double *__restrict__ SXL,
+    const double *__restrict__ alpha, const double *__restrict__ HPHI, double *__restrict__ out,
+    int N, int K, int stereo) {
+  __shared__ double s_red[256];
+  const int f = blockIdx.x;
+  double sn[8], sd[8];
+  for (int k = 0; k < 8; ++k) sn[k] = sd[k] = 0.0;
+  const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
+  const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const size_t i = (size_t)f * N + n;
+    double num, den;
+    if (stereo) {
+      const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
+      const double com = aR2 * Z[i] / mr;
+      const double d = aL2 * Z[i] / ml;
+      num = com * SXR[i];
+      num /= mr;
+      num += d * SXL[i] / ml;
+      den = d + com;
+    } else {
+      const double m = fmax(hR[i], kSimmEps);
+      den = Z[i] / m;
+      num = (den * SXR[i]) / m;
+    }
+    for (int k = 0; k < K; ++k) {
+      const double h = HPHI[(size_t)k * N + n];
+      sn[k] += num * h;
+      sd[k] += den * h;
+    }
+  }
+  for (int q = 0; q < 2 * K; ++q) {
+    s_red[threadIdx.x] = q < K ? sn[q] : sd[q - K];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[(size_t)f * 2 * K + q] = s_red[0];
+    __syncthreads();
+  }
+}
+
+// HGAMMA update + renormalisations (:802-812 / :335-343), one block:
+// HGAMMA *= (WGAMMA^T numH / max(WGAMMA^T denH, eps))^omega, column-normalise,
+// WPHI = WGAMMA HGAMMA; the HPHI row scale by sumHGAMMA is returned in sg.
+__global__ void k_hgamma_update(double *__restrict__ HGAMMA, const double *__restrict__ WGAMMA,
+                                const double *__restrict__ rows, double *__restrict__ WPHI,
+                                double *__restrict__ sg, int F, int P, int K, double omega) {
+  __shared__ double s_h[64 * 8];
+  for (int idx = threadIdx.x; idx < P * K; idx += blockDim.x) {
+    const int p = idx / K, k = idx % K;
+    double num = 0.0, den = 0.0;
+    for (int f = 0; f < F; ++f) {
+      const double w = WGAMMA[f * P + p];
+      num += w * rows[(size_t)f * 2 * K + k];
+      den += w * rows[(size_t)f * 2 * K + K + k];
+    }
+    s_h[idx] = HGAMMA[idx] * powo(num / fmax(den, kSimmEps), omega);
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    double s = 0.0;
+    for (int p = 0; p < P; ++p) s += s_h[p * K + k];
+    sg[k] = s;
+    for (int p = 0; p < P; ++p) {
+      const double v = s > 0 ? s_h[p * K + k] / s : s_h[p * K + k];
+      s_h[p * K + k] = v;
+      HGAMMA[p * K + k] = v;
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < F * K; idx += blockDim.x) {
+    const int f = idx / K, k = idx % K;
+    double w = 0.0;
+    for (int p = 0; p < P; ++p) w += WGAMMA[f * P + p] * s_h[p * K + k];
+    WPHI[idx] = w;
+  }
+}
+
+// HPHI *= outer(sg, ones); s = column sums; HPHI[:, s>0] /= s  (:808-811)
+__global__ void k_hphi_rescale(double *__restrict__ HPHI, const double *__restrict__ sg,
+                               double *__restrict__ s_out, int K, int N) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double h = HPHI[(size_t)k * N + n] * sg[k];
+    HPHI[(size_t)k * N + n] = h;
+    s += h;
+  }
+  if (s > 0)
+    for (int k = 0; k < K; ++k) HPHI[(size_t)k * N + n] /= s;
+  s_out[n] = s;
+}
+
+// WM update (stereo :844-853, mono :377-385) then column normalisation; one
+// block per accompaniment column r.  P_* = X_* HM^T (unscaled products).
+__global__ __launch_bounds__(256) void k_wm_update(double *__restrict__ WM,
+                                                   const double *__restrict__ PnR,
+                                                   const double *__restrict__ PdR,
+                                                   const double *__restrict__ PnL,
+                                                   const double *__restrict__ PdL,
+                                                   const double *__restrict__ bR,
+                                                   const double *__restrict__ bL,
+                                                   double *__restrict__ sw, int F, int R,
+                                                   double omega, int stereo) {
+  __shared__ double s_red[256];
+  const int r = blockIdx.x;
+  double part = 0.0;
+  const double br = stereo ? bR[r] * bR[r] : 1.0, bl = stereo ? bL[r] * bL[r] : 0.0;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    const size_t i = (size_t)f * R + r;
+    double ratio;
+    if (stereo)
+      ratio = (PnR[i] * br + PnL[i] * bl) / (PdR[i] * br + PdL[i] * bl);   // no eps floor (:844)
+    else
+      ratio = PnR[i] / fmax(PdR[i], kSimmEps);
+    const double w = WM[i] * powo(ratio, omega);
+    WM[i] = w;
+    part += w;
+  }
+  s_red[threadIdx.x] = part;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double s = s_red[0];
+  if (s > 0)
+    for (int f = threadIdx.x; f < F; f += 256) WM[(size_t)f * R + r] /= s;
+  if (threadIdx.x == 0) sw[r] = s;
+}
+
+// HM *= vstack(sumWM) (stereo, :855) ; mono N7 quirk handled on the host
+__global__ void k_rowscale(double *__restrict__ X, const double *__restrict__ s, int R, int N) {
+  GRID_STRIDE(i, (size_t)R * N) X[i] *= s[i / N];
+}
+
+// WMb = WM * beta^2 (column scale), F x R
+__global__ void k_wm_beta(const double *__restrict__ WM, const double *__restrict__ b,
+                          double *__restrict__ WMb, int F, int R) {
+  GRID_STRIDE(i, (size_t)F * R) {
+    const double bb = b[i % R];
+    WMb[i] = WM[i] * (bb * bb);
+  }
+}
+
+// alpha sums (:875-885): [sum numR, sum denR, sum numL, sum denL] partials
+__global__ __launch_bounds__(256) void k_alpha_partial(
+    const double *__restrict__ SF0, const double *__restrict__ SPHI, const double *__restrict__ hR,
+    const double *__restrict__ hL, const double *__restrict__ SXR, const double *__restrict__ SXL,
+    double *__restrict__ part, size_t n) {
+  __shared__ double s_red[4][256];
+  double a[4] = {0, 0, 0, 0};
+  GRID_STRIDE(i, n) {
+    const double l = SF0[i] * SPHI[i];
+    const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
+    const double dR = l / mr, dL = l / ml;
+    a[0] += dR * SXR[i] / mr;
+    a[1] += dR;
+    a[2] += dL * SXL[i] / ml;
+    a[3] += dL;
+  }
+  for (int q = 0; q < 4; ++q) s_red[q][threadIdx.x] = a[q];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int q = 0; q < 4; ++q) s_red[q][threadIdx.x] += s_red[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) part[(size_t)blockIdx.x * 4 + threadIdx.x] = s_red[threadIdx.x][0];
+}
+
+__global__ void k_alpha_update(const double *__restrict__ part, int nb, double *__restrict__ alpha,
+                               double omega) {
+  if (threadIdx.x != 0) return;
+  double s[4] = {0, 0, 0, 0};
+  for (int b = 0; b < nb; ++b)
+    for (int q = 0; q < 4; ++q) s[q] += part[(size_t)b * 4 + q];
+  double aR = fmax(alpha[0] * pow(s[0] / s[1], omega * .1), kSimmEps);
+  double aL = fmax(alpha[1] * pow(s[2] / s[3], omega * .1), kSimmEps);
+  aR = aR / fmax(aR + aL, .001);
+  alpha[0] = aR;
+  alpha[1] = 1 - aR;
+}
+
+// out[r] = sum_n T[r][n] HM[r][n] (diag of (WM^T X) HM^T, :910-918); block per r
+__global__ __launch_bounds__(256) void k_rowdot(const double *__restrict__ T,
+                                                const double *__restrict__ HM,
+                                                double *__restrict__ out, int N) {
+  __shared__ double s_red[256];
+  const int r = blockIdx.x;
+  double a = 0.0;
+  for (int n = threadIdx.x; n < N; n += 256) a += T[(size_t)r * N + n] * HM[(size_t)r * N + n];
+  s_red[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[r] = s_red[0];
+}
+
+// beta update (:909-921): d[0..R) numR, [R..2R) denR, [2R..3R) numL, [3R..4R) denL
+__global__ void k_beta_update(const double *__restrict__ d, double *__restrict__ bR,
+                              double *__restrict__ bL, int R, double omega) {
+  const int r = threadIdx.x;
+  if (r >= R) return;
+  double br = bR[r] * pow(d[r] / d[R + r], omega * .1);
+  double bl = bL[r] * pow(d[2 * R + r] / d[3 * R + r], omega * .1);
+  br = br / fmax(br + bl, kSimmEps);
+  bR[r] = br;
+  bL[r] = 1 - br;
+}
+
+// Itakura-Saito divergence partials (ISDistortion, SIMM.py:34-44) of
+// SXR vs hR (+ SXL vs hL): sum(-log(r) + r - 1), r = SX/hat
+__global__ __launch_bounds__(256) void k_is_partial(const double *__restrict__ SXR,
+                                                    const double *__restrict__ hR,
+                                                    const double *__restrict__ SXL,
+                                                    const double *__restrict__ hL,
+                                                    double *__restrict__ part, size_t n,
+                                                    int stereo) {
+  __shared__ double s_red[256];
+  double a = 0.0;
+  GRID_STRIDE(i, n) {
+    double r = SXR[i] / hR[i];
+    a += (-log(r) + r) - 1;
+    if (stereo) {
+      r = SXL[i] / hL[i];
+      a += (-log(r) + r) - 1;
+    }
+  }
+  s_red[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = s_red[0];
+}
+
+__global__ void k_is_final(const double *__restrict__ part, int nb, double *__restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += part[b];
+  *out = s;
+}
+
+}  // namespace fasst
+
+using namespace fasst;
+
+// ============================================================================ context
+struct simm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
+  int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
+  DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
+  DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, NP0, NP1, WMb, s_col, sg, sw;
+  DBuf<double> hpart, hrows, apart, bd, gwork, P0, P1, P2, P3, RN0, RN1, reco;
+};
+
+namespace {
+
+int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, double *C, int ldc,
+            int M, int N, int K) {
+  const double *Bs[1] = {B};
+  double *Cs[1] = {C};
+  return gemm<false, false, 1>(c->stream, A, lda, Bs, ldb, Cs, ldc, M, N, K, c->gwork.p);
+}
+
+// SMR = (WM bR^2) HM, SML = (WM bL^2) HM  (stereo); SM = WM HM (mono)
+int refresh_sm(simm_ctx *c) {
+  if (c->stereo) {
+    k_wm_beta<<<egrid((size_t)c->F * c->R), 256, 0, c->stream>>>(c->WM.p, c->bR.p, c->WMb.p, c->F, c->R);
+    int st = gemm_nn(c, c->WMb.p, c->R, c->HM.p, c->N, c->SMR.p, c->N, c->F, c->N, c->R);
+    if (st) return st;
+    k_wm_beta<<<egrid((size_t)c->F * c->R), 256, 0, c->stream>>>(c->WM.p, c->bL.p, c->WMb.p, c->F, c->R);
+    return gemm_nn(c, c->WMb.p, c->R, c->HM.p, c->N, c->SML.p, c->N, c->F, c->N, c->R);
+  }
+  return gemm_nn(c, c->WM.p, c->R, c->HM.p, c->N, c->SMR.p, c->N, c->F, c->N, c->R);
+}
+
+int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi) {
+  k_simm_refresh<<<egrid((size_t)c->F * c->N), 256, 0, c->stream>>>(
+      c->SF0.p, c->SPHI.p, c->WPHI.p, c->HPHI.p, colscale, c->SMR.p, c->SML.p, c->alpha.p,
+      c->hR.p, c->hL.p, c->F, c->N, c->K, c->stereo, recompute_sphi);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+void reco_error(simm_ctx *c, double *slot) {
+  const size_t FN = (size_t)c->F * c->N;
+  k_is_partial<<<c->nb_alpha, 256, 0, c->stream>>>(c->SXR.p, c->hR.p, c->SXL.p, c->hL.p,
+                                                    c->apart.p, FN, c->stereo);
+  k_is_final<<<1, 64, 0, c->stream>>>(c->apart.p, c->nb_alpha, slot);
+}
+
+// one loop body; reco (device, may be null) receives the IS divergence
+// after the HF0 and after the HPHI updates (SIMM.py:676-683, :721-728)
+int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
+  const size_t FN = (size_t)c->F * c->N;
+  const int F = c->F, N = c->N, NF0 = c->NF0, K = c->K, R = c->R;
+  int st;
+  // ---- HF0 (:623-674 / :281-291)
+  k_simm_numden<<<egrid(FN), 256, 0, c->stream>>>(c->SPHI.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p,
+                                                   c->alpha.p, c->T0.p, c->T1.p, FN, c->stereo);
+  {
+    const double *Bs[2] = {c->T0.p, c->T1.p};
+    double *Cs[2] = {c->NP0.p, c->NP1.p};
+    if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, N, Cs, N, NF0, N, F, c->gwork.p)))
+      return st;
+  }
+  k_mu_apply<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->NP0.p, c->NP1.p,
+                                                             (size_t)NF0 * N, omega, 0);
+  if ((st = gemm_nn(c, c->WF0.p, NF0, c->HF0.p, N, c->SF0.p, N, F, N, NF0))) return st;
+  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  if (reco) reco_error(c, reco);
+  // ---- HPHI (:686-729 / :296-313)
+  k_hphi_partial<<<dim3((N + 255) / 256, c->nchunk_h), 256, 0, c->stream>>>(
+      c->SF0.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p, c->alpha.p, c->WPHI.p, c->hpart.p, F, N, K,
+      c->fchunk_h, c->stereo);
+  k_hphi_update<<<(N + 255) / 256, 256, 0, c->stream>>>(c->HPHI.p, c->hpart.p, c->nchunk_h,
+                                                         c->s_col.p, K, N, omega);
+  k_colscale<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->s_col.p, NF0, N);
+  if ((st = refresh_hat(c, c->s_col.p, 1))) return st;
+  if (reco) reco_error(c, reco + 1);
+  // ---- HM (:740-773 / :318-331)
+  if (c->stereo) {
+    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
+    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p, FN, c->stereo);
+    const double *Bs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
+    double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
+    if ((st = gemm<true, false, 4>(c->stream, c->WM.p, R, Bs, N, Cs, N, R, N, F, c->gwork.p)))
+      return st;
+    k_hm_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
+                                                             c->RN0.p + (size_t)R * N,
+                                                             c->RN1.p + (size_t)R * N, c->bR.p,
+                                                             c->bL.p, R, N, omega);
+  } else {
+    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
+    const double *Bs[2] = {c->T0.p, c->T1.p};
+    double *Cs[2] = {c->RN0.p, c->RN1.p};
+    if ((st = gemm<true, false, 2>(c->stream, c->WM.p, R, Bs, N, Cs, N, R, N, F, c->gwork.p)))
+      return st;
+    k_mu_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
+                                                            (size_t)R * N, omega, 1);
+  }
+  if ((st = refresh_sm(c))) return st;
+  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  // ---- HGAMMA (:776-823 / :335-350)
+  if (update_hgamma) {
+    k_hgamma_rows<<<F, 256, 0, c->stream>>>(c->SF0.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p,
+                                             c->alpha.p, c->HPHI.p, c->hrows.p, N, K, c->stereo);
+    k_hgamma_update<<<1, 256, 0, c->stream>>>(c->HGAMMA.p, c->WGAMMA.p, c->hrows.p, c->WPHI.p,
+                                              c->sg.p, F, c->P, K, omega);
+    k_hphi_rescale<<<(N + 255) / 256, 256, 0, c->stream>>>(c->HPHI.p, c->sg.p, c->s_col.p, K, N);
+    k_colscale<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->s_col.p, NF0, N);
+    if ((st = refresh_hat(c, c->s_col.p, 1))) return st;
+  }
+  // ---- WM (:826-869 / :355-387)
+  if (c->stereo) {
+    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
+    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p, FN, c->stereo);
+    const double *srcs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
+    double *dsts[4] = {c->P0.p, c->P1.p, c->P2.p, c->P3.p};
+    for (int q = 0; q < 4; ++q) {  // X HM^T : (F x N)(N x R)
+      const double *Bs[1] = {c->HM.p};
+      double *Cs[1] = {dsts[q]};
+      if ((st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p)))
+        return st;
+    }
+    k_wm_update<<<R, 256, 0, c->stream>>>(c->WM.p, c->P0.p, c->P1.p, c->P2.p, c->P3.p, c->bR.p,
+                                          c->bL.p, c->sw.p, F, R, omega, 1);
+    k_rowscale<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->sw.p, R, N);
+  } else {
+    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
+    const double *srcs[2] = {c->T0.p, c->T1.p};
+    double *dsts[2] = {c->P0.p, c->P1.p};
+    for (int q = 0; q < 2; ++q) {
+      const double *Bs[1] = {c->HM.p};
+      double *Cs[1] = {dsts[q]};
+      if ((st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p)))
+        return st;
+    }
+    k_wm_update<<<R, 256, 0, c->stream>>>(c->WM.p, c->P0.p, c->P1.p, nullptr, nullptr, nullptr,
+                                          nullptr, c->sw.p, F, R, omega, 0);
+    // N7 (SIMM.py:388): HM *= sumWM broadcasts over the frame axis
+    if (R == 1)
+      k_rowscale<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->sw.p, R, N);
+    else
+      k_colscale<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->sw.p, R, N);  // R == N
+  }
+  if ((st = refresh_sm(c))) return st;
+  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  if (!c->stereo) return FASST_OK;
+  // ---- alpha (:872-906)
+  k_alpha_partial<<<c->nb_alpha, 256, 0, c->stream>>>(c->SF0.p, c->SPHI.p, c->hR.p, c->hL.p,
+                                                       c->SXR.p, c->SXL.p, c->apart.p, FN);
+  k_alpha_update<<<1, 64, 0, c->stream>>>(c->apart.p, c->nb_alpha, c->alpha.p, omega);
+  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  // ---- beta (:909-941)
+  k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
+  k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p, FN, c->stereo);
+  {
+    const double *Bs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
+    double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
+    if ((st = gemm<true, false, 4>(c->stream, c->WM.p, R, Bs, N, Cs, N, R, N, F, c->gwork.p)))
+      return st;
+  }
+  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p, c->HM.p, c->bd.p, N);
+  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p, c->HM.p, c->bd.p + R, N);
+  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p + (size_t)R * N, c->HM.p, c->bd.p + 2 * R, N);
+  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p + (size_t)R * N, c->HM.p, c->bd.p + 3 * R, N);
+  k_beta_update<<<1, 64, 0, c->stream>>>(c->bd.p, c->bR.p, c->bL.p, R, omega);
+  if ((st = refresh_sm(c))) return st;
+  return refresh_hat(c, nullptr, 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int stereo, simm_ctx **out) {
+  if (!out || F < 1 || N < 1 || NF0 < 1 || P < 1 || K < 1 || K > 8 || R < 1 || P * K > 512) {
+    set_error("simm_create: unsupported sizes F=%d N=%d NF0=%d P=%d K=%d R=%d", F, N, NF0, P, K, R);
+    return FASST_ERR_SHAPE;
+  }
+  if (!stereo && R != 1 && R != N) {
+    set_error("operands could not be broadcast together (SIMM.py:388 needs R == 1 or R == N)");
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(device);
+  simm_ctx *c = new simm_ctx();
+  c->device = device;
+  c->F = F;
+  c->N = N;
+  c->NF0 = NF0;
+  c->P = P;
+  c->K = K;
+  c->R = R;
+  c->stereo = stereo ? 1 : 0;
+  c->fchunk_h = std::max(1, (F + 15) / 16);
+  c->nchunk_h = (F + c->fchunk_h - 1) / c->fchunk_h;
+  c->nb_alpha = 1024;
+  const size_t FN = (size_t)F * N;
+  int st = FASST_OK;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
+  size_t gw = 0;
+  gw = std::max(gw, gemm_workspace(NF0, N, F, 2));
+  gw = std::max(gw, gemm_workspace(F, N, NF0, 1));
+  gw = std::max(gw, gemm_workspace(F, N, R, 1));
+  gw = std::max(gw, gemm_workspace(R, N, F, stereo ? 4 : 2));
+  gw = std::max(gw, gemm_workspace(F, R, N, 1));
+#define SA(buf, n) \
+  if (!st) st = c->buf.alloc(n)
+  SA(SXR, FN);
+  SA(SXL, stereo ? FN : 1);
+  SA(WF0, (size_t)F * NF0);
+  SA(WGAMMA, (size_t)F * P);
+  SA(HGAMMA, (size_t)P * K);
+  SA(HPHI, (size_t)K * N);
+  SA(HF0, (size_t)NF0 * N);
+  SA(HM, (size_t)R * N);
+  SA(WM, (size_t)F * R);
+  SA(bR, R);
+  SA(bL, R);
+  SA(alpha, 2);
+  SA(WPHI, (size_t)F * K);
+  SA(SF0, FN);
+  SA(SPHI, FN);
+  SA(hR, FN);
+  SA(hL, stereo ? FN : 1);
+  SA(SMR, FN);
+  SA(SML, stereo ? FN : 1);
+  SA(T0, FN);
+  SA(T1, FN);
+  SA(T2, stereo ? FN : 1);
+  SA(T3, stereo ? FN : 1);
+  SA(NP0, (size_t)NF0 * N);
+  SA(NP1, (size_t)NF0 * N);
+  SA(WMb, (size_t)F * R);
+  SA(s_col, N);
+  SA(sg, K);
+  SA(sw, R);
+  SA(hpart, (size_t)c->nchunk_h * 2 * K * N);
+  SA(hrows, (size_t)F * 2 * K);
+  SA(apart, (size_t)c->nb_alpha * 4);
+  SA(bd, 4 * (size_t)R);
+  SA(gwork, std::max<size_t>(gw, 1));
+  SA(P0, (size_t)F * R);
+  SA(P1, (size_t)F * R);
+  SA(P2, (size_t)F * R);
+  SA(P3, (size_t)F * R);
+  SA(RN0, 2 * (size_t)R * N);
+  SA(RN1, 2 * (size_t)R * N);
+#undef SA
+  if (st) {
+    simm_destroy(c);
+    return st;
+  }
+  *out = c;
+  return FASST_OK;
+}
+
+int simm_destroy(simm_ctx *c) {
+  if (!c) return FASST_OK;
+  {
+    DeviceGuard g(c->device);
+    if (c->stream) {
+      (void)hipStreamSynchronize(c->stream);
+      (void)hipStreamDestroy(c->stream);
+    }
+  }
+  delete c;  // DBuf destructors free device memory
+  return FASST_OK;
+}
+
+int simm_set_data(simm_ctx *c, const double *SXR, const double *SXL, const double *WF0,
+                  const double *WGAMMA) {
+  if (!c || !SXR || !WF0 || !WGAMMA || (c->stereo && !SXL)) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  const size_t FN = (size_t)c->F * c->N;
+  FASST_HIP(hipMemcpyAsync(c->SXR.p, SXR, FN * 8, hipMemcpyHostToDevice, c->stream));
+  if (c->stereo) FASST_HIP(hipMemcpyAsync(c->SXL.p, SXL, FN * 8, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(c->WF0.p, WF0, (size_t)c->F * c->NF0 * 8, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(c->WGAMMA.p, WGAMMA, (size_t)c->F * c->P * 8, hipMemcpyHostToDevice,
+                           c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int simm_set_params(simm_ctx *c, const double *HGAMMA, const double *HPHI, const double *HF0,
+                    const double *HM, const double *WM, const double *alpha, const double *betaR) {
+  if (!c || !HGAMMA || !HPHI || !HF0 || !HM || !WM) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  const int F = c->F, N = c->N, K = c->K, R = c->R;
+  FASST_HIP(hipMemcpyAsync(c->HGAMMA.p, HGAMMA, (size_t)c->P * K * 8, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(c->HPHI.p, HPHI, (size_t)K * N * 8, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(c->HF0.p, HF0, (size_t)c->NF0 * N * 8, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(c->HM.p, HM, (size_t)R * N * 8, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(c->WM.p, WM, (size_t)F * R * 8, hipMemcpyHostToDevice, c->stream));
+  if (c->stereo) {
+    std::vector<double> bl(R);
+    for (int r = 0; r < R; ++r) bl[r] = 1 - betaR[r];  // betaL = 1 - betaR (:576)
+    FASST_HIP(hipMemcpyAsync(c->alpha.p, alpha, 2 * 8, hipMemcpyHostToDevice, c->stream));
+    FASST_HIP(hipMemcpyAsync(c->bR.p, betaR, R * 8, hipMemcpyHostToDevice, c->stream));
+    FASST_HIP(hipMemcpyAsync(c->bL.p, bl.data(), R * 8, hipMemcpyHostToDevice, c->stream));
+    FASST_HIP(hipStreamSynchronize(c->stream));
+  }
+  // model from the initial parameters (:578-585 / :229-233): WPHI, SF0, SPHI, SM, hat
+  int st;
+  if ((st = gemm_nn(c, c->WGAMMA.p, c->P, c->HGAMMA.p, K, c->WPHI.p, K, F, K, c->P))) return st;
+  if ((st = gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, N, c->SF0.p, N, F, N, c->NF0))) return st;
+  if ((st = refresh_sm(c))) return st;
+  // the reference's initial hat is not floored by eps (:579-585); every use
+  // floors it again with max(., eps), so the floored copy is equivalent
+  if ((st = refresh_hat(c, nullptr, 1))) return st;
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int simm_run(simm_ctx *c, int n_iter, double omega, int update_hgamma, double *reco_err) {
+  if (!c || n_iter < 0) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  if (reco_err && c->reco.n < (size_t)2 * n_iter) {
+    int st = c->reco.alloc(std::max(2 * n_iter, 1));
+    if (st) return st;
+  }
+  for (int it = 0; it < n_iter; ++it) {
+    int st = simm_iteration(c, omega, c->stereo ? update_hgamma : 1,
+                            reco_err ? c->reco.p + 2 * it : nullptr);
+    if (st) return st;
+  }
+  if (reco_err && n_iter > 0)
+    FASST_HIP(hipMemcpyAsync(reco_err, c->reco.p, (size_t)2 * n_iter * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int simm_reco_error(simm_ctx *c, double *out) {
+  if (!c || !out) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  if (c->reco.n < 1) {
+    int st = c->reco.alloc(2);
+    if (st) return st;
+  }
+  reco_error(c, c->reco.p);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipMemcpyAsync(out, c->reco.p, 8, hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int simm_get_params(simm_ctx *c, double *HGAMMA, double *HPHI, double *HF0, double *HM, double *WM,
+                    double *alpha, double *betaR, double *betaL) {
+  if (!c) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  const int N = c->N, K = c->K, R = c->R;
+  if (HGAMMA) FASST_HIP(hipMemcpyAsync(HGAMMA, c->HGAMMA.p, (size_t)c->P * K * 8, hipMemcpyDeviceToHost, c->stream));
+  if (HPHI) FASST_HIP(hipMemcpyAsync(HPHI, c->HPHI.p, (size_t)K * N * 8, hipMemcpyDeviceToHost, c->stream));
+  if (HF0) FASST_HIP(hipMemcpyAsync(HF0, c->HF0.p, (size_t)c->NF0 * N * 8, hipMemcpyDeviceToHost, c->stream));
+  if (HM) FASST_HIP(hipMemcpyAsync(HM, c->HM.p, (size_t)R * N * 8, hipMemcpyDeviceToHost, c->stream));
+  if (WM) FASST_HIP(hipMemcpyAsync(WM, c->WM.p, (size_t)c->F * R * 8, hipMemcpyDeviceToHost, c->stream));
+  if (c->stereo) {
+    if (alpha) FASST_HIP(hipMemcpyAsync(alpha, c->alpha.p, 2 * 8, hipMemcpyDeviceToHost, c->stream));
+    if (betaR) FASST_HIP(hipMemcpyAsync(betaR, c->bR.p, R * 8, hipMemcpyDeviceToHost, c->stream));
+    if (betaL) FASST_HIP(hipMemcpyAsync(betaL, c->bL.p, R * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+}  // extern "C"

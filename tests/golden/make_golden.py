@@ -144,6 +144,50 @@ def run_nmf():
     print("nmf")
 
 
+def run_simm():
+    """Stereo_SIMM (SIMM.py:397-943) and SIMM (SIMM.py:46-395) on seeded
+    synthetic inputs (random positive bases stand in for the KLGLOTT88 WF0)."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    from pyfasst.SeparateLeadStereo.SIMM import SIMM as S
+    rs = np.random.RandomState(11)
+    F, N, NF0, P, K, R = 65, 40, 24, 6, 3, 5
+    SXR = rs.gamma(0.8, 1.0, size=(F, N))
+    SXL = rs.gamma(0.8, 1.0, size=(F, N))
+    WF0 = rs.gamma(1.0, 1.0, size=(F, NF0))
+    WGAMMA = rs.gamma(1.0, 1.0, size=(F, P))
+    np.random.seed(1)
+    out = S.Stereo_SIMM(SXR, SXL, WF0, WGAMMA, numberOfFilters=K,
+                        numberOfAccompanimentSpectralShapes=R, numberOfIterations=4,
+                        verbose=False)
+    names = ['alphaR', 'alphaL', 'HGAMMA', 'HPHI', 'HF0', 'betaR', 'betaL', 'HM', 'WM', 'recoError']
+    res = {'st_' + n: np.asarray(v) for n, v in zip(names, out)}
+    # mono SIMM with R = 1 (the estimHF0 call, SeparateLeadStereoTF.py:996)
+    np.random.seed(2)
+    mout = S.SIMM(SXR, WF0, WGAMMA, numberOfFilters=K, numberOfAccompanimentSpectralShapes=1,
+                  numberOfIterations=4, verbose=False)
+    res.update({'mono_' + n: np.asarray(v) for n, v in
+                zip(['HGAMMA', 'HPHI', 'HF0', 'HM', 'WM', 'recoError'], mout)})
+    # stereo with computeError, frozen HGAMMA and omega != 1
+    np.random.seed(3)
+    out = S.Stereo_SIMM(SXR, SXL, WF0, WGAMMA, numberOfFilters=K,
+                        numberOfAccompanimentSpectralShapes=R, numberOfIterations=3,
+                        updateRulePower=0.7, updateHGAMMA=False, computeError=True,
+                        verbose=False)
+    res.update({'st2_' + n: np.asarray(v) for n, v in zip(names, out)})
+    # mono with R == N (the other shape quirk N7 admits, SIMM.py:388)
+    np.random.seed(4)
+    mout = S.SIMM(SXR, WF0, WGAMMA, numberOfFilters=K, numberOfAccompanimentSpectralShapes=N,
+                  numberOfIterations=3, verbose=False)
+    res.update({'monoN_' + n: np.asarray(v) for n, v in
+                zip(['HGAMMA', 'HPHI', 'HF0', 'HM', 'WM', 'recoError'], mout)})
+    np.savez_compressed(os.path.join(HERE, "simm.npz"), SXR=SXR, SXL=SXL, WF0=WF0,
+                        WGAMMA=WGAMMA, **res)
+    print("simm")
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -166,12 +210,12 @@ if __name__ == "__main__":
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     if len(sys.argv) > 2 and sys.argv[1] == "--case":
         name = sys.argv[2]
-        {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm}.get(
+        {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
-    names = sys.argv[1:] or (["inv_herm", "stft", "nmf"] + list(CASES))
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

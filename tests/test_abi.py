@@ -1,8 +1,9 @@
-"""The C-ABI library loads and exports every symbol of include/fasst_hip.h.
+"""The C-ABI library loads and exports every symbol declared in include/*.h.
 
 CPU-only: no compute call is made (there is no GPU in the build container).
 """
 import ctypes
+import glob
 import os
 import re
 
@@ -10,15 +11,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "fasst_hip.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(fasst_\w+)\s*\(", src)))
+    syms = set()
+    for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))):
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        syms |= set(re.findall(r"\b((?:fasst|simm|nmf)_\w+)\s*\(", src))
+    return sorted(syms)
 
 
 def test_header_declares_the_boundary():
     syms = declared_symbols()
     for s in ("fasst_create", "fasst_configure", "fasst_run", "fasst_wiener_images",
-              "fasst_stft", "fasst_istft", "fasst_inv_herm_mat_2d", "fasst_destroy"):
+              "fasst_stft", "fasst_istft", "fasst_inv_herm_mat_2d", "fasst_destroy",
+              "simm_create", "simm_run", "simm_set_params", "simm_get_params"):
         assert s in syms
 
 

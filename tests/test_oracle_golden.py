@@ -60,3 +60,33 @@ def test_em_golden(case):
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['final_TW_%d' % j])
     S = m.separated_images(X)
     assert rel(np.abs(S), np.abs(g['images'])) == 0.0
+
+
+def _simm_check(g, prefix, out, names):
+    for n, v in zip(names, out):
+        np.testing.assert_array_equal(np.asarray(v), g[prefix + n], err_msg=prefix + n)
+
+
+def test_simm_golden():
+    import simm_ref
+    g = load("simm")
+    st_names = ['alphaR', 'alphaL', 'HGAMMA', 'HPHI', 'HF0', 'betaR', 'betaL', 'HM', 'WM',
+                'recoError']
+    mono_names = ['HGAMMA', 'HPHI', 'HF0', 'HM', 'WM', 'recoError']
+    K, R = g['st_HGAMMA'].shape[1], g['st_HM'].shape[0]
+    np.random.seed(1)
+    out = simm_ref.stereo_simm(g['SXR'], g['SXL'], g['WF0'], g['WGAMMA'], K, R,
+                               numberOfIterations=4)
+    _simm_check(g, 'st_', out, st_names)
+    np.random.seed(2)
+    _simm_check(g, 'mono_', simm_ref.simm(g['SXR'], g['WF0'], g['WGAMMA'], K, 1,
+                                          numberOfIterations=4), mono_names)
+    np.random.seed(3)
+    out = simm_ref.stereo_simm(g['SXR'], g['SXL'], g['WF0'], g['WGAMMA'], K, R,
+                               numberOfIterations=3, updateRulePower=0.7, updateHGAMMA=False,
+                               computeError=True)
+    _simm_check(g, 'st2_', out, st_names)
+    np.random.seed(4)
+    N = g['SXR'].shape[1]
+    _simm_check(g, 'monoN_', simm_ref.simm(g['SXR'], g['WF0'], g['WGAMMA'], K, N,
+                                           numberOfIterations=3), mono_names)
