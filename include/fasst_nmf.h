@@ -1,0 +1,40 @@
+/*
+ * fasst_nmf.h -- C ABI of the IS-NMF engine (libfasst_hip.so).
+ *
+ * Replaces the multiplicative-update loops of the reference's tools/nmf.py:
+ *   NMF_decomposition (nmf.py:24-61)  -> nmf_run(update_w=1, update_h=1)
+ *   NMF_decomp_init   (nmf.py:63-159) -> nmf_run(update_w, update_h)
+ * Random initialisation stays on the host (NumPy's global stream, nmf.py:30-32,
+ * :119-140) and is handed over with nmf_set_params; the Python host side is
+ * pyfasst_amd/tools/nmf.py.
+ *
+ * Conventions are those of fasst_hip.h.  SX [F][N], W [F][K], H [K][N]
+ * (NMF_decomp_init's frame-major H is transposed by the host).
+ */
+#ifndef FASST_NMF_H
+#define FASST_NMF_H
+
+#include "fasst_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nmf_ctx nmf_ctx;
+
+int nmf_create(int device, int F, int N, int K, nmf_ctx **out);
+int nmf_destroy(nmf_ctx *ctx);
+int nmf_set_data(nmf_ctx *ctx, const double *SX);
+int nmf_set_params(nmf_ctx *ctx, const double *W, const double *H);
+
+/* n_iter iterations of nmf.py:34-59 (W update, column renormalisation of W
+ * with the scale moved into H, then H update); either update may be
+ * switched off (NMF_decomp_init's updateW / updateH, nmf.py:142-157).      */
+int nmf_run(nmf_ctx *ctx, int n_iter, int update_w, int update_h);
+int nmf_get_params(nmf_ctx *ctx, double *W, double *H);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FASST_NMF_H */

@@ -530,3 +530,40 @@ def nmf_decomposition(SX, nbComps=10, niter=10, rng=np.random):
         den = np.dot(W.T, 1 / np.maximum(hat, EPS))
         H *= num / np.maximum(den, EPS)
     return W, H
+
+
+def nmf_decomp_init(SX, nbComps=10, niter=10, Winit=None, Hinit=None, updateW=True,
+                    updateH=True, rng=np.random):
+    """tools/nmf.py:63-159: frame-major H internally, returned transposed."""
+    nf, nt = SX.shape
+    if Winit is None or Winit.shape != (nf, nbComps):
+        W = rng.randn(nf, nbComps) ** 2
+    else:
+        W = np.copy(Winit)
+    if Hinit is not None:
+        if Hinit.shape == (nbComps, nt):
+            H = np.copy(Hinit.T)
+        elif Hinit.shape == (nt, nbComps):
+            H = np.copy(Hinit)
+        else:
+            raise AttributeError('Hinit not in the right shape.')
+    else:
+        H = rng.randn(nt, nbComps) ** 2
+    if updateW:
+        W /= W.sum(axis=0)
+    for _ in range(niter):
+        if updateW:
+            hat = np.dot(W, H.T)
+            num = np.dot(SX / np.maximum(hat ** 2, EPS), H)
+            den = np.dot(1 / np.maximum(hat, EPS), H)
+            W *= num / np.maximum(den, EPS)
+            s = W.sum(axis=0)
+            s[s == 0] = 1.
+            W /= s
+            H *= s
+        if updateH:
+            hat = np.dot(H, W.T)
+            num = np.dot(SX.T / np.maximum(hat ** 2, EPS), W)
+            den = np.dot(1 / np.maximum(hat, EPS), W)
+            H *= num / np.maximum(den, EPS)
+    return W, H.T

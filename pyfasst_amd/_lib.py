@@ -1,5 +1,5 @@
-"""ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h and
-include/fasst_simm.h).
+"""ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h,
+include/fasst_simm.h and include/fasst_nmf.h).
 
 The product path has no CPU fallback: if the HIP library is missing this
 module raises at import time, and every compute call raises if the device
@@ -71,6 +71,13 @@ SIGNATURES = {
     "simm_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_int, _dp]),
     "simm_reco_error": (ctypes.c_int, [_vp, _dp]),
     "simm_get_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    # include/fasst_nmf.h
+    "nmf_create": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(_vp)]),
+    "nmf_destroy": (ctypes.c_int, [_vp]),
+    "nmf_set_data": (ctypes.c_int, [_vp, _dp]),
+    "nmf_set_params": (ctypes.c_int, [_vp, _dp, _dp]),
+    "nmf_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "nmf_get_params": (ctypes.c_int, [_vp, _dp, _dp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -132,5 +132,7 @@ GemmPlan gemm_plan(int M, int N, int K);
 template <bool TA, bool TB, int NB>
 int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ldb, double *const *C,
          int ldc, int M, int N, int K, double *work);
+// doubles of `work` gemm() needs for these sizes (0: no split)
+size_t gemm_workspace(int M, int N, int K, int NB);
 
 }  // namespace fasst

@@ -140,7 +140,19 @@ def run_nmf():
     SX = rs.gamma(0.7, 1.0, size=(97, 150)) * np.outer(rs.gamma(2, 1, 97), np.ones(150))
     np.random.seed(1)
     W, H = nmf.NMF_decomposition(SX, nbComps=6, niter=7)
-    np.savez_compressed(os.path.join(HERE, "nmf.npz"), SX=SX, W=W, H=H)
+    res = dict(SX=SX, W=W, H=H)
+    # NMF_decomp_init: random start; given W frozen; given frame-major H
+    np.random.seed(2)
+    res['di_W'], res['di_H'] = nmf.NMF_decomp_init(SX, nbComps=5, niter=6)
+    Winit = rs.gamma(1.0, 1.0, size=(97, 4))
+    Hinit = rs.gamma(1.0, 1.0, size=(150, 4))
+    np.random.seed(3)
+    res['Winit'], res['Hinit'] = Winit, Hinit
+    res['dw_W'], res['dw_H'] = nmf.NMF_decomp_init(SX, nbComps=4, niter=5, Winit=Winit,
+                                                   updateW=False)
+    np.random.seed(4)
+    res['dh_W'], res['dh_H'] = nmf.NMF_decomp_init(SX, nbComps=4, niter=5, Hinit=Hinit)
+    np.savez_compressed(os.path.join(HERE, "nmf.npz"), **res)
     print("nmf")
 
 

@@ -40,6 +40,18 @@ def test_nmf_golden():
     W, H = R.nmf_decomposition(g['SX'], nbComps=6, niter=7, rng=rng)
     np.testing.assert_array_equal(W, g['W'])
     np.testing.assert_array_equal(H, g['H'])
+    np.random.seed(2)
+    W, H = R.nmf_decomp_init(g['SX'], nbComps=5, niter=6)
+    np.testing.assert_array_equal(W, g['di_W'])
+    np.testing.assert_array_equal(H, g['di_H'])
+    np.random.seed(3)
+    W, H = R.nmf_decomp_init(g['SX'], nbComps=4, niter=5, Winit=g['Winit'], updateW=False)
+    np.testing.assert_array_equal(W, g['dw_W'])
+    np.testing.assert_array_equal(H, g['dw_H'])
+    np.random.seed(4)
+    W, H = R.nmf_decomp_init(g['SX'], nbComps=4, niter=5, Hinit=g['Hinit'])
+    np.testing.assert_array_equal(W, g['dh_W'])
+    np.testing.assert_array_equal(H, g['dh_H'])
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
