@@ -116,6 +116,11 @@ int fasst_stft(int device, const double *x, int L, const double *window, int wle
  * y out float64 [hop*(n_frames-1)+wlen - wlen/2].                           */
 int fasst_istft(int device, const double *X, int n_frames, const double *window,
                 const double *analysis_window, int wlen, int nfft, int hop, double *y);
+/* istft of the SIMM pipeline (SeparateLeadStereo/separateLeadFunctions.py:
+ * 163-233): no half-window trim, edge normalisation copied from the
+ * neighbouring window; y out float64 [hop*(n_frames-1)+wlen] (>= 2 wlen). */
+int fasst_istft_simm(int device, const double *X, int n_frames, const double *window,
+                     const double *analysis_window, int wlen, int nfft, int hop, double *y);
 /* inv_herm_mat_2d (tools/signalTools.py:132-196) on n matrices:
  * diag[2][n], off complex128[n] -> inv_diag[2][n], inv_off complex128[n], det[n]. */
 int fasst_inv_herm_mat_2d(int device, int n, const double *diag, const double *off,

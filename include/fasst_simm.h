@@ -36,16 +36,18 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
                 simm_ctx **out);
 int simm_destroy(simm_ctx *ctx);
 
-/* the data to be fitted and the fixed dictionaries (SIMM.py:397-403) */
+/* the data to be fitted and the fixed dictionaries (SIMM.py:397-403);
+ * SXR / SXL may be NULL when only simm_separate is wanted                  */
 int simm_set_data(simm_ctx *ctx, const double *SXR, const double *SXL, const double *WF0,
                   const double *WGAMMA);
 
-/* initial parameters (SIMM.py:525-576); alpha and betaR are read for stereo
- * only (alpha = (0.5, 0.5) in the reference, betaL = 1 - betaR, :575-576).
+/* initial parameters (SIMM.py:525-576); alpha and betaR / betaL are read for
+ * stereo only (alpha = (0.5, 0.5) in the reference; betaL NULL means
+ * 1 - betaR, :575-576).
  * Builds WPHI, SF0, SPHI and the model spectrograms (:578-585).           */
 int simm_set_params(simm_ctx *ctx, const double *HGAMMA, const double *HPHI, const double *HF0,
                     const double *HM, const double *WM, const double *alpha,
-                    const double *betaR);
+                    const double *betaR, const double *betaL);
 
 /* n_iter iterations of the reference loop body (:613-941 / :278-393);
  * omega = updateRulePower; update_hgamma = updateHGAMMA (stereo only).
@@ -56,6 +58,12 @@ int simm_run(simm_ctx *ctx, int n_iter, double omega, int update_hgamma, double 
 /* ISDistortion(SXR, hatSXR) [+ ISDistortion(SXL, hatSXL)] of the current
  * model (SIMM.py:34-44, :602-603)                                          */
 int simm_reco_error(simm_ctx *ctx, double *out);
+
+/* writeSeparatedSignals masks (SeparateLeadStereo/SeparateLeadStereoTF.py:
+ * 1762-1846) from the current parameters: XR, XL complex128 [F][N] mixture
+ * STFTs -> lead VR, VL and accompaniment MR, ML complex128 [F][N] (stereo). */
+int simm_separate(simm_ctx *ctx, const double *XR, const double *XL, double *VR, double *VL,
+                  double *MR, double *ML);
 
 /* current parameters; any pointer may be NULL (alpha/beta: stereo only) */
 int simm_get_params(simm_ctx *ctx, double *HGAMMA, double *HPHI, double *HF0, double *HM,

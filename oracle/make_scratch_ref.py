@@ -60,6 +60,24 @@ PATCHES = [
      "lengthData = int(hopsize*(numberFrames-1) + lengthWindow)"),
     ("tftransforms/stft.py", r"\[\(lengthWindow/2\.0\):\]", "[int(lengthWindow//2):]"),
     ("tftransforms/stft.py", r"self\.freqbins = self\.ftlen / 2 \+ 1", "self.freqbins = self.ftlen // 2 + 1"),
+    # SIMM-pipeline stft / istft (separateLeadFunctions.py:90-233) float sizes/indices
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"np\.zeros\(lengthWindow / 2\.0\)",
+     "np.zeros(int(lengthWindow / 2.0))"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"np\.zeros\(\[newLengthData - lengthData\]\)",
+     "np.zeros([int(newLengthData - lengthData)])"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"numberFrequencies = nfft / 2\.0 \+ 1",
+     "numberFrequencies = int(nfft / 2.0 + 1)"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"        stop = numberFrames\n",
+     "        stop = int(numberFrames)\n"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"beginFrame = n \* hopsize",
+     "beginFrame = int(n * hopsize)"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"np\.fft\.rfft\(frameToProcess, nfft\)",
+     "np.fft.rfft(frameToProcess, int(nfft))"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"np\.fft\.irfft\(X\[:,n\], nfft\)",
+     "np.fft.irfft(X[:,n], int(nfft))"),
+    ("SeparateLeadStereo/separateLeadFunctions.py",
+     r"lengthData = hopsize \* \(numberFrames - 1\) \+ lengthWindow",
+     "lengthData = int(hopsize * (numberFrames - 1) + lengthWindow)"),
     # the Cython tracker is not built: use the reference's own pure-Python
     # fallback (tracking/tracking.py), only needed at import time here
     ("SeparateLeadStereo/SeparateLeadStereoTF.py",

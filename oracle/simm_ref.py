@@ -228,3 +228,70 @@ def stereo_simm(SXR, SXL, WF0, WGAMMA, numberOfFilters=4, numberOfAccompanimentS
         bL = 1 - bR
         hR, hL = _hat(SF0, SPHI, WM, HM, aR, aL, bR, bL)
     return aR, aL, HGAMMA, HPHI, HF0, np.diag(bR), np.diag(bL), HM, WM, recoError
+
+
+# ---------------------------------------------------------------- lead / accompaniment
+SEP_EPS = 10 ** -9   # SeparateLeadStereoTF.py:31
+
+
+def sinebell(L):
+    """tools/utils.py:43-57"""
+    return np.sin((np.pi * (np.arange(L))) / (1.0 * L))
+
+
+def slf_stft(data, window, hopsize, nfft, fs=44100.0, start=0, stop=None):
+    """SIMM-pipeline stft (separateLeadFunctions.py:90-161)."""
+    L = window.size
+    data = np.concatenate((np.zeros(int(L / 2.0)), data, np.zeros(int(L / 2.0))))
+    n_data = data.size
+    n_frames = np.ceil((n_data - L) / hopsize + 1) + 1
+    new_len = (n_frames - 1) * hopsize + L
+    data = np.concatenate((data, np.zeros([int(new_len - n_data)])))
+    n_freqs = int(nfft / 2.0 + 1)
+    if stop is None:
+        stop = int(n_frames)
+    X = np.zeros([n_freqs, stop - start], dtype=complex)
+    for n in np.arange(start, stop):
+        b = int(n * hopsize)
+        X[:, n - start] = np.fft.rfft(window * data[b:b + L], int(nfft))
+    return X, np.arange(n_freqs) / nfft * fs, np.arange(n_frames) * hopsize / fs
+
+
+def slf_istft(X, analysisWindow=None, window=None, hopsize=256.0, nfft=2048.0,
+              originalDataLen=None):
+    """SIMM-pipeline istft (separateLeadFunctions.py:163-233)."""
+    if analysisWindow is None:
+        analysisWindow = window
+    L = window.size
+    n_freqs, n_frames = X.shape
+    n_data = int(hopsize * (n_frames - 1) + L)
+    norm = np.zeros(n_data)
+    data = np.zeros(n_data)
+    for n in np.arange(n_frames):
+        b = int(n * hopsize)
+        frame = np.fft.irfft(X[:, n], int(nfft))[:L]
+        norm[b:b + L] = norm[b:b + L] + window * analysisWindow
+        data[b:b + L] = data[b:b + L] + window * frame
+    norm[:L] = norm[L:2 * L]
+    norm[-L:] = norm[(-2 * L):(-L)]
+    norm[norm == 0] = 1.
+    data /= norm
+    if originalDataLen is not None:
+        data = data[:originalDataLen]
+    return data
+
+
+def lead_masks(P, XR, XL):
+    """The four masked STFTs of writeSeparatedSignals
+    (SeparateLeadStereoTF.py:1785-1846): lead R/L, accompaniment R/L."""
+    SPHI = np.dot(np.dot(P['WGAMMA'], P['HGAMMA']), P['HPHI'])
+    SF0 = np.dot(P['WF0'], P['HF0'])
+    aR, aL, bR, bL, WM, HM = (P['alphaR'], P['alphaL'], P['betaR'], P['betaL'], P['WM'],
+                              P['HM'])
+    hR = np.maximum((aR ** 2) * SF0 * SPHI + np.dot(np.dot(WM, bR ** 2), HM), SEP_EPS)
+    hL = np.maximum((aL ** 2) * SF0 * SPHI + np.dot(np.dot(WM, bL ** 2), HM), SEP_EPS)
+    vR = (aR ** 2) * SPHI * SF0 / hR * XR
+    vL = (aL ** 2) * SPHI * SF0 / hL * XL
+    mR = (np.dot(np.dot(WM, bR ** 2), HM)) / hR * XR
+    mL = (np.dot(np.dot(WM, bL ** 2), HM)) / hL * XL
+    return vR, vL, mR, mL

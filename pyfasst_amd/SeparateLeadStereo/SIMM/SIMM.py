@@ -78,7 +78,7 @@ def _run(SXs, WF0, WGAMMA, K, R, params, alpha, betaR, n_iter, omega, update_hga
     bR = _c(betaR if stereo else np.zeros(R))
     _lib.check(_lib.lib.simm_set_params(ctx.ptr, _lib.dptr(HGAMMA), _lib.dptr(HPHI),
                                         _lib.dptr(HF0), _lib.dptr(HM), _lib.dptr(WM),
-                                        _lib.dptr(a), _lib.dptr(bR)), "simm_set_params")
+                                        _lib.dptr(a), _lib.dptr(bR), None), "simm_set_params")
     recoError = np.zeros([n_iter * 5 * 2 + NF0 * 2 + 1])
     if compute_error:
         out = np.zeros(1)

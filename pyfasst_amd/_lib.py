@@ -58,6 +58,8 @@ SIGNATURES = {
                                   ctypes.c_int, ctypes.c_int, _dp, _ip]),
     "fasst_istft": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, _dp]),
+    "fasst_istft_simm": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, _dp]),
     "fasst_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "fasst_kernel_times": (ctypes.c_int, [_vp, _dp, ctypes.POINTER(ctypes.c_long), ctypes.c_int]),
     "fasst_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
@@ -67,9 +69,10 @@ SIGNATURES = {
     "simm_create": (ctypes.c_int, [ctypes.c_int] * 8 + [ctypes.POINTER(_vp)]),
     "simm_destroy": (ctypes.c_int, [_vp]),
     "simm_set_data": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp]),
-    "simm_set_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    "simm_set_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
     "simm_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_int, _dp]),
     "simm_reco_error": (ctypes.c_int, [_vp, _dp]),
+    "simm_separate": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp]),
     "simm_get_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
     # include/fasst_nmf.h
     "nmf_create": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(_vp)]),

@@ -458,6 +458,30 @@ __global__ void k_is_final(const double *__restrict__ part, int nb, double *__re
   *out = s;
 }
 
+// writeSeparatedSignals masks (SeparateLeadStereoTF.py:1785-1846), eps 1e-9:
+//   hat = max(a^2 SF0 SPHI + WM b^2 HM, eps); lead = a^2 SPHI SF0 / hat X;
+//   accompaniment = (WM b^2 HM) / hat X      (per channel)
+__global__ void k_lead_masks(const double *__restrict__ SF0, const double *__restrict__ SPHI,
+                             const double *__restrict__ SMR, const double *__restrict__ SML,
+                             const double *__restrict__ alpha, const double2 *__restrict__ XR,
+                             const double2 *__restrict__ XL, double2 *__restrict__ VR,
+                             double2 *__restrict__ VL, double2 *__restrict__ MR,
+                             double2 *__restrict__ ML, size_t n) {
+  const double aR2 = alpha[0] * alpha[0], aL2 = alpha[1] * alpha[1];
+  GRID_STRIDE(i, n) {
+    const double sf = SF0[i], sp = SPHI[i];
+    const double hr = fmax(aR2 * sf * sp + SMR[i], 1e-9);
+    const double hl = fmax(aL2 * sf * sp + SML[i], 1e-9);
+    const double vr = aR2 * sp * sf / hr, vl = aL2 * sp * sf / hl;
+    const double mr = SMR[i] / hr, ml = SML[i] / hl;
+    const double2 xr = XR[i], xl = XL[i];
+    VR[i] = make_double2(vr * xr.x, vr * xr.y);
+    VL[i] = make_double2(vl * xl.x, vl * xl.y);
+    MR[i] = make_double2(mr * xr.x, mr * xr.y);
+    ML[i] = make_double2(ml * xl.x, ml * xl.y);
+  }
+}
+
 }  // namespace fasst
 
 using namespace fasst;
@@ -499,6 +523,21 @@ int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi) {
       c->SF0.p, c->SPHI.p, c->WPHI.p, c->HPHI.p, colscale, c->SMR.p, c->SML.p, c->alpha.p,
       c->hR.p, c->hL.p, c->F, c->N, c->K, c->stereo, recompute_sphi);
   FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+// WPHI, SF0, SPHI, SM and the model spectrograms from the parameters
+// (:578-585 / :229-233)
+int rebuild_model(simm_ctx *c) {
+  int st;
+  const int F = c->F, N = c->N, K = c->K;
+  if ((st = gemm_nn(c, c->WGAMMA.p, c->P, c->HGAMMA.p, K, c->WPHI.p, K, F, K, c->P))) return st;
+  if ((st = gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, N, c->SF0.p, N, F, N, c->NF0))) return st;
+  if ((st = refresh_sm(c))) return st;
+  // the reference's initial hat is not floored by eps (:579-585); every use
+  // floors it again with max(., eps), so the floored copy is equivalent
+  if ((st = refresh_hat(c, nullptr, 1))) return st;
+  FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
 }
 
@@ -731,11 +770,12 @@ int simm_destroy(simm_ctx *c) {
 
 int simm_set_data(simm_ctx *c, const double *SXR, const double *SXL, const double *WF0,
                   const double *WGAMMA) {
-  if (!c || !SXR || !WF0 || !WGAMMA || (c->stereo && !SXL)) return FASST_ERR_SHAPE;
+  if (!c || !WF0 || !WGAMMA) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   const size_t FN = (size_t)c->F * c->N;
-  FASST_HIP(hipMemcpyAsync(c->SXR.p, SXR, FN * 8, hipMemcpyHostToDevice, c->stream));
-  if (c->stereo) FASST_HIP(hipMemcpyAsync(c->SXL.p, SXL, FN * 8, hipMemcpyHostToDevice, c->stream));
+  if (SXR) FASST_HIP(hipMemcpyAsync(c->SXR.p, SXR, FN * 8, hipMemcpyHostToDevice, c->stream));
+  if (c->stereo && SXL)
+    FASST_HIP(hipMemcpyAsync(c->SXL.p, SXL, FN * 8, hipMemcpyHostToDevice, c->stream));
   FASST_HIP(hipMemcpyAsync(c->WF0.p, WF0, (size_t)c->F * c->NF0 * 8, hipMemcpyHostToDevice, c->stream));
   FASST_HIP(hipMemcpyAsync(c->WGAMMA.p, WGAMMA, (size_t)c->F * c->P * 8, hipMemcpyHostToDevice,
                            c->stream));
@@ -744,7 +784,8 @@ int simm_set_data(simm_ctx *c, const double *SXR, const double *SXL, const doubl
 }
 
 int simm_set_params(simm_ctx *c, const double *HGAMMA, const double *HPHI, const double *HF0,
-                    const double *HM, const double *WM, const double *alpha, const double *betaR) {
+                    const double *HM, const double *WM, const double *alpha, const double *betaR,
+                    const double *betaL) {
   if (!c || !HGAMMA || !HPHI || !HF0 || !HM || !WM) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   const int F = c->F, N = c->N, K = c->K, R = c->R;
@@ -755,22 +796,13 @@ int simm_set_params(simm_ctx *c, const double *HGAMMA, const double *HPHI, const
   FASST_HIP(hipMemcpyAsync(c->WM.p, WM, (size_t)F * R * 8, hipMemcpyHostToDevice, c->stream));
   if (c->stereo) {
     std::vector<double> bl(R);
-    for (int r = 0; r < R; ++r) bl[r] = 1 - betaR[r];  // betaL = 1 - betaR (:576)
+    for (int r = 0; r < R; ++r) bl[r] = betaL ? betaL[r] : 1 - betaR[r];  // (:576)
     FASST_HIP(hipMemcpyAsync(c->alpha.p, alpha, 2 * 8, hipMemcpyHostToDevice, c->stream));
     FASST_HIP(hipMemcpyAsync(c->bR.p, betaR, R * 8, hipMemcpyHostToDevice, c->stream));
     FASST_HIP(hipMemcpyAsync(c->bL.p, bl.data(), R * 8, hipMemcpyHostToDevice, c->stream));
     FASST_HIP(hipStreamSynchronize(c->stream));
   }
-  // model from the initial parameters (:578-585 / :229-233): WPHI, SF0, SPHI, SM, hat
-  int st;
-  if ((st = gemm_nn(c, c->WGAMMA.p, c->P, c->HGAMMA.p, K, c->WPHI.p, K, F, K, c->P))) return st;
-  if ((st = gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, N, c->SF0.p, N, F, N, c->NF0))) return st;
-  if ((st = refresh_sm(c))) return st;
-  // the reference's initial hat is not floored by eps (:579-585); every use
-  // floors it again with max(., eps), so the floored copy is equivalent
-  if ((st = refresh_hat(c, nullptr, 1))) return st;
-  FASST_HIP(hipStreamSynchronize(c->stream));
-  return FASST_OK;
+  return rebuild_model(c);
 }
 
 int simm_run(simm_ctx *c, int n_iter, double omega, int update_hgamma, double *reco_err) {
@@ -802,6 +834,31 @@ int simm_reco_error(simm_ctx *c, double *out) {
   reco_error(c, c->reco.p);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipMemcpyAsync(out, c->reco.p, 8, hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int simm_separate(simm_ctx *c, const double *XR, const double *XL, double *VR, double *VL,
+                  double *MR, double *ML) {
+  if (!c || !c->stereo || !XR || !XL || !VR || !VL || !MR || !ML) return FASST_ERR_SHAPE;
+  DeviceGuard g(c->device);
+  int st = rebuild_model(c);
+  if (st) return st;
+  const size_t FN = (size_t)c->F * c->N;
+  DBuf<double2> dx[2], dout[4];
+  for (auto &b : dx)
+    if ((st = b.alloc(FN))) return st;
+  for (auto &b : dout)
+    if ((st = b.alloc(FN))) return st;
+  FASST_HIP(hipMemcpyAsync(dx[0].p, XR, FN * 16, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(dx[1].p, XL, FN * 16, hipMemcpyHostToDevice, c->stream));
+  k_lead_masks<<<egrid(FN), 256, 0, c->stream>>>(c->SF0.p, c->SPHI.p, c->SMR.p, c->SML.p,
+                                                  c->alpha.p, dx[0].p, dx[1].p, dout[0].p,
+                                                  dout[1].p, dout[2].p, dout[3].p, FN);
+  FASST_LAUNCH_CHECK();
+  double *outs[4] = {VR, VL, MR, ML};
+  for (int q = 0; q < 4; ++q)
+    FASST_HIP(hipMemcpyAsync(outs[q], dout[q].p, FN * 16, hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
 }

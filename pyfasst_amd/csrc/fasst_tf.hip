@@ -117,6 +117,46 @@ __global__ void k_ola(const double *__restrict__ frames, int nframes, int wlen, 
   }
 }
 
+// SIMM-pipeline overlap-add (separateLeadFunctions.py:163-233): no half-window
+// trim; the normalisation's first / last window are copied from the
+// neighbouring window (:214-217), zeros become 1.  Needs len_out >= 2 wlen.
+__device__ __forceinline__ double ola_norm(int s, int nframes, int wlen, int hop,
+                                           const double *__restrict__ win,
+                                           const double *__restrict__ awin) {
+  long nlo = (s - wlen) / hop + 1;
+  if (s - wlen < 0) nlo = 0;
+  long nhi = s / hop;
+  if (nhi > nframes - 1) nhi = nframes - 1;
+  double nrm = 0.0;
+  for (long n = nlo; n <= nhi; ++n) {
+    const int p = (int)(s - n * hop);
+    if (p < 0 || p >= wlen) continue;
+    nrm = nrm + win[p] * awin[p];
+  }
+  return nrm;
+}
+
+__global__ void k_ola_simm(const double *__restrict__ frames, int nframes, int wlen, int hop,
+                           const double *__restrict__ win, const double *__restrict__ awin,
+                           double *__restrict__ y, int len_out) {
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < len_out; o += gridDim.x * blockDim.x) {
+    long nlo = (o - wlen) / hop + 1;
+    if (o - wlen < 0) nlo = 0;
+    long nhi = o / hop;
+    if (nhi > nframes - 1) nhi = nframes - 1;
+    double acc = 0.0;
+    for (long n = nlo; n <= nhi; ++n) {
+      const int p = (int)(o - n * hop);
+      if (p < 0 || p >= wlen) continue;
+      acc = acc + frames[(size_t)n * wlen + p];
+    }
+    int u = o >= len_out - wlen ? o - wlen : o;  // norm[-L:] = norm[-2L:-L]
+    if (u < wlen) u += wlen;                     // norm[:L] = norm[L:2L]
+    double nrm = ola_norm(u, nframes, wlen, hop, win, awin);
+    y[o] = acc / (nrm == 0.0 ? 1.0 : nrm);
+  }
+}
+
 // Cx planes from the resident STFT images X[c][t][f].
 __global__ void k_cx_from_X(const double2 *__restrict__ X, double *__restrict__ cx, size_t plane) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < plane;
@@ -419,6 +459,44 @@ int fasst_istft(int device, const double *X, int n_frames, const double *window,
                                                      ilog2(nfft), dframes.p);
   FASST_LAUNCH_CHECK();
   k_ola<<<(len_out + 255) / 256, 256>>>(dframes.p, T, wlen, hop, dw.p, daw.p, dy.p, len_out);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipDeviceSynchronize());
+  FASST_HIP(hipMemcpy(y, dy.p, (size_t)len_out * sizeof(double), hipMemcpyDeviceToHost));
+  return FASST_OK;
+}
+
+int fasst_istft_simm(int device, const double *X, int n_frames, const double *window,
+                     const double *analysis_window, int wlen, int nfft, int hop, double *y) {
+  int st = check_fft(nfft, wlen, hop);
+  if (st) return st;
+  if (n_frames < 1 || !X || !y) return FASST_ERR_SHAPE;
+  const int F = nfft / 2 + 1, T = n_frames;
+  const int len_out = hop * (T - 1) + wlen;
+  if (len_out < 2 * wlen) {
+    set_error("istft: %d samples < two windows (%d); the reference's edge copy fails", len_out,
+              wlen);
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(device);
+  if ((st = fft_smem(nfft))) return st;
+  DBuf<double> dw, daw, dframes, dy;
+  DBuf<double2> dtw, dX, dXt;
+  if ((st = dw.alloc(wlen)) || (st = daw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)) ||
+      (st = dX.alloc((size_t)T * F)) || (st = dXt.alloc((size_t)T * F)) ||
+      (st = dframes.alloc((size_t)T * wlen)) || (st = dy.alloc(len_out)))
+    return st;
+  auto tw = twiddles(nfft, +1);
+  FASST_HIP(hipMemcpy(dw.p, window, (size_t)wlen * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(daw.p, analysis_window ? analysis_window : window,
+                      (size_t)wlen * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dtw.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dX.p, X, (size_t)T * F * sizeof(double2), hipMemcpyHostToDevice));
+  k_ft_to_tf<<<dim3((T + 15) / 16, (F + 15) / 16, 1), 256>>>(dX.p, dXt.p, F, T, F, T);
+  FASST_LAUNCH_CHECK();
+  k_istft_frames<<<T, 256, nfft * sizeof(double2)>>>(dXt.p, F, dw.p, wlen, dtw.p, nfft,
+                                                     ilog2(nfft), dframes.p);
+  FASST_LAUNCH_CHECK();
+  k_ola_simm<<<(len_out + 255) / 256, 256>>>(dframes.p, T, wlen, hop, dw.p, daw.p, dy.p, len_out);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipDeviceSynchronize());
   FASST_HIP(hipMemcpy(y, dy.p, (size_t)len_out * sizeof(double), hipMemcpyDeviceToHost));

@@ -200,6 +200,68 @@ def run_simm():
     print("simm")
 
 
+def run_lead():
+    """SIMM-pipeline stft/istft (separateLeadFunctions.py:90-233) and the
+    writeSeparatedSignals masks (SeparateLeadStereoTF.py:1762-1871) applied
+    with the stereo SIMM golden parameters to a seeded stereo signal."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    import scipy.io.wavfile as wf
+    from pyfasst.SeparateLeadStereo import separateLeadFunctions as slf
+    from pyfasst.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    rs = np.random.RandomState(21)
+    out = {}
+    x = rs.randn(1216)
+    out['x'] = x
+    for (wlen, hop, nfft, start, stop) in ((128, 32, 128, 0, None), (256, 64, 512, 3, 17),
+                                           (100, 25, 128, 0, None)):
+        tag = '%d_%d_%d' % (wlen, hop, nfft)
+        X, F, N = slf.stft(x, window=slf.sinebell(wlen), hopsize=float(hop), nfft=float(nfft),
+                           fs=8000., start=start, stop=stop)
+        out['X_' + tag], out['F_' + tag], out['N_' + tag] = X, F, N
+        out['y_' + tag] = slf.istft(X, window=slf.sinebell(wlen), hopsize=float(hop),
+                                    nfft=float(nfft))
+        out['yh_' + tag] = slf.istft(X, analysisWindow=np.hanning(wlen),
+                                     window=slf.sinebell(wlen), hopsize=float(hop),
+                                     nfft=float(nfft), originalDataLen=1000)
+    g = np.load(os.path.join(HERE, "simm.npz"))
+    xs = (rs.randn(1216, 2) * 3000)
+    XR = slf.stft(xs[:, 0], window=slf.sinebell(128), hopsize=32., nfft=128.)[0]
+    XL = slf.stft(xs[:, 1], window=slf.sinebell(128), hopsize=32., nfft=128.)[0]
+    proc = object.__new__(SL.SeparateLeadProcess)
+    proc.SIMMParams = {'WF0': g['WF0'], 'HF0': g['st_HF0'], 'WGAMMA': g['WGAMMA'],
+                       'HGAMMA': g['st_HGAMMA'], 'HPHI': g['st_HPHI'], 'HM': g['st_HM'],
+                       'WM': g['st_WM'], 'alphaR': g['st_alphaR'], 'alphaL': g['st_alphaL'],
+                       'betaR': g['st_betaR'], 'betaL': g['st_betaL']}
+    proc.stftParams = {'windowSizeInSamples': 128, 'hopsize': 32., 'NFT': 128}
+    proc.tfrepresentation = 'stft'
+    proc.XR, proc.XL = XR, XL
+    proc.scaleData = 1.0
+    proc.dataType = np.int16
+    proc.fs = 8000
+    proc.files = {'voc_output_file': '/tmp/golden_lead_voc.wav',
+                  'mus_output_file': '/tmp/golden_lead_mus.wav'}
+    seen = []
+    orig = SL.slf.istft
+
+    def capture(X, *a, **kw):
+        y = orig(X, *a, **kw)
+        seen.append((np.array(X), np.array(y)))
+        return y
+    SL.slf.istft = capture
+    proc.writeSeparatedSignals()
+    SL.slf.istft = orig
+    out['XR'], out['XL'] = XR, XL
+    for i, name in enumerate(('vR', 'vL', 'mR', 'mL')):
+        out['mask_' + name], out['est_' + name] = seen[i]
+    out['voc_wav'] = wf.read('/tmp/golden_lead_voc.wav')[1]
+    out['mus_wav'] = wf.read('/tmp/golden_lead_mus.wav')[1]
+    np.savez_compressed(os.path.join(HERE, "lead.npz"), **out)
+    print("lead", {k: np.shape(v) for k, v in out.items() if k.startswith(('mask', 'voc'))})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -222,12 +284,13 @@ if __name__ == "__main__":
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     if len(sys.argv) > 2 and sys.argv[1] == "--case":
         name = sys.argv[2]
-        {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm}.get(
+        {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
+         "lead": run_lead}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
-    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm"] + list(CASES))
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

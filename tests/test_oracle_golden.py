@@ -102,3 +102,35 @@ def test_simm_golden():
     N = g['SXR'].shape[1]
     _simm_check(g, 'monoN_', simm_ref.simm(g['SXR'], g['WF0'], g['WGAMMA'], K, N,
                                            numberOfIterations=3), mono_names)
+
+
+def test_lead_golden():
+    """SIMM-pipeline stft/istft and the writeSeparatedSignals masks."""
+    import simm_ref as S
+    g = load("lead")
+    for (wlen, hop, nfft, start, stop) in ((128, 32, 128, 0, None), (256, 64, 512, 3, 17),
+                                           (100, 25, 128, 0, None)):
+        tag = '%d_%d_%d' % (wlen, hop, nfft)
+        X, F, N = S.slf_stft(g['x'], S.sinebell(wlen), float(hop), float(nfft), fs=8000.,
+                             start=start, stop=stop)
+        np.testing.assert_array_equal(X, g['X_' + tag])
+        np.testing.assert_array_equal(F, g['F_' + tag])
+        np.testing.assert_array_equal(N, g['N_' + tag])
+        np.testing.assert_array_equal(
+            S.slf_istft(X, window=S.sinebell(wlen), hopsize=float(hop), nfft=float(nfft)),
+            g['y_' + tag])
+        np.testing.assert_array_equal(
+            S.slf_istft(X, analysisWindow=np.hanning(wlen), window=S.sinebell(wlen),
+                        hopsize=float(hop), nfft=float(nfft), originalDataLen=1000),
+            g['yh_' + tag])
+    s = load("simm")
+    P = {'WF0': s['WF0'], 'HF0': s['st_HF0'], 'WGAMMA': s['WGAMMA'], 'HGAMMA': s['st_HGAMMA'],
+         'HPHI': s['st_HPHI'], 'HM': s['st_HM'], 'WM': s['st_WM'], 'alphaR': s['st_alphaR'],
+         'alphaL': s['st_alphaL'], 'betaR': s['st_betaR'], 'betaL': s['st_betaL']}
+    masks = S.lead_masks(P, g['XR'], g['XL'])
+    for name, m in zip(('vR', 'vL', 'mR', 'mL'), masks):
+        np.testing.assert_array_equal(m, g['mask_' + name])
+        y = S.slf_istft(m, window=S.sinebell(128), hopsize=32., nfft=128)
+        np.testing.assert_array_equal(y, g['est_' + name])
+    voc = np.array(np.round(np.array([g['est_vR'], g['est_vL']]).T), dtype=np.int16)
+    np.testing.assert_array_equal(voc, g['voc_wav'])
