@@ -1,0 +1,97 @@
+"""Secondary benchmarks of the §8 rows next to the headline (bench.py):
+
+  --workload simm   Stereo_SIMM iterations/s at config 5 (F=2049, T=20000,
+                    NF0=1092, P=30, K=4, R=40), SIMM.py:613-941
+  --workload nmf    NMF_decomposition iterations/s at config 2 (F=1025,
+                    T=2000, K=64), tools/nmf.py:34-59
+
+Inputs are synthetic and resident in HBM before the timed region; the timed
+region is `steps` iterations of the update loop (simm_run / nmf_run, which
+synchronise at the end).  Prints one JSON line.  Not part of the driver
+contract; the headline metric is bench.py's.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK = 78.6e12
+
+
+def bench_simm(steps, warmup, F=2049, N=20000, NF0=1092, P=30, K=4, R=40, seed=0):
+    from pyfasst_amd import _lib
+    from pyfasst_amd.SeparateLeadStereo.SIMM.SIMM import _SimmContext, _c
+    rs = np.random.RandomState(seed)
+    SXR = rs.gamma(0.8, 1.0, size=(F, N))
+    SXL = rs.gamma(0.8, 1.0, size=(F, N))
+    WF0 = rs.gamma(1.0, 1.0, size=(F, NF0))
+    WG = rs.gamma(1.0, 1.0, size=(F, P))
+    HG, HPHI, HF0 = np.abs(rs.randn(P, K)), np.abs(rs.randn(K, N)), np.abs(rs.randn(NF0, N))
+    HM, WM = np.abs(rs.randn(R, N)), np.abs(rs.randn(F, R))
+    ctx = _SimmContext(F, N, NF0, P, K, R, True, _lib.default_device())
+    _lib.check(_lib.lib.simm_set_data(ctx.ptr, _lib.dptr(SXR), _lib.dptr(SXL), _lib.dptr(WF0),
+                                      _lib.dptr(WG)), "set_data")
+    alpha, bR = np.array([.5, .5]), rs.rand(R)
+    _lib.check(_lib.lib.simm_set_params(ctx.ptr, *[_lib.dptr(_c(a)) for a in
+                                                   (HG, HPHI, HF0, HM, WM, alpha, bR)], None),
+               "set_params")
+    if warmup:
+        _lib.check(_lib.lib.simm_run(ctx.ptr, warmup, 1.0, 1, None), "run")
+    t0 = time.perf_counter()
+    _lib.check(_lib.lib.simm_run(ctx.ptr, steps, 1.0, 1, None), "run")
+    dt = time.perf_counter() - t0
+    # GEMM flops per iteration: WF0^T{num,den} (2), SF0 recompute (1) on F x NF0 x N;
+    # the R-sized products (HM: 4, WM: 4, beta: 4, SM refreshes: 2 x 3) on F x R x N
+    flops = 2.0 * F * N * (3 * NF0 + 18 * R)
+    return {"metric": "Stereo_SIMM iterations/sec (config 5)", "value": round(steps / dt, 4),
+            "unit": "SIMM it/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+            "warmup": warmup, "dtype": "f64", "data": "synthetic gamma spectrograms, RandomState(0)",
+            "config": {"workload": "Stereo_SIMM F=%d N=%d NF0=%d P=%d K=%d R=%d" % (F, N, NF0, P, K, R)},
+            "gemm_tflops_per_s": round(flops / (dt / steps) / 1e12, 2),
+            "reference_cpu": "14.27 s/iter = 0.070 it/s (BASELINE/SURVEY §6, measured on CPU)"}
+
+
+def bench_nmf(steps, warmup, F=1025, N=2000, K=64, seed=0):
+    from pyfasst_amd import _lib
+    from pyfasst_amd.tools.nmf import _NmfContext
+    rs = np.random.RandomState(seed)
+    SX = rs.gamma(0.7, 1.0, size=(F, N))
+    W = rs.randn(F, K) ** 2
+    H = rs.randn(K, N) ** 2
+    W /= W.sum(axis=0)
+    ctx = _NmfContext(F, N, K, _lib.default_device())
+    _lib.check(_lib.lib.nmf_set_data(ctx.ptr, _lib.dptr(SX)), "set_data")
+    _lib.check(_lib.lib.nmf_set_params(ctx.ptr, _lib.dptr(W), _lib.dptr(H)), "set_params")
+    if warmup:
+        _lib.check(_lib.lib.nmf_run(ctx.ptr, warmup, 1, 1), "run")
+    t0 = time.perf_counter()
+    _lib.check(_lib.lib.nmf_run(ctx.ptr, steps, 1, 1), "run")
+    dt = time.perf_counter() - t0
+    flops = 2.0 * F * N * K * 6
+    return {"metric": "NMF_decomposition iterations/sec (config 2)", "value": round(steps / dt, 3),
+            "unit": "NMF it/s", "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
+            "warmup": warmup, "dtype": "f64", "data": "synthetic gamma spectrogram, RandomState(0)",
+            "config": {"workload": "IS-NMF F=%d T=%d K=%d" % (F, N, K)},
+            "gemm_tflops_per_s": round(flops / (dt / steps) / 1e12, 2),
+            "reference_cpu": "0.0318 s/iter = 31.4 it/s (SURVEY §6, measured on CPU)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=("simm", "nmf"), required=True)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    fn = bench_simm if a.workload == "simm" else bench_nmf
+    print(json.dumps(fn(a.steps, a.warmup)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
