@@ -34,7 +34,8 @@ struct fasst_ctx {
   fasst::DBuf<double2> A, Pinst;
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
-  fasst::DBuf<double> epart, llpart, bnum, bden, psd, ll, hsum, rscal, rtpart;
+  int nsplit_t = 1, fpc_t = 1;  // TW contraction bin chunks
+  fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rtpart;
   int nchunk_r = 1;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart
@@ -42,7 +43,7 @@ struct fasst_ctx {
   double *h_ll = nullptr;        // pinned host mirror (one value)
   int psd_cap = 0, ll_cap = 0;
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
-  static constexpr int kNK = 11;
+  static constexpr int kNK = 12;
   int prof = 0;
   int ablate = 0;  // FASST_ABLATE (profiling builds of the E-step; never in the product)
   hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};

@@ -627,88 +627,118 @@ __global__ void k_mix_inst(const IArgs a) {
 // ---------------------------------------------------------------- FB update
 struct BArgs {
   const double *TW, *Wkf, *FWHt, *hatW;
-  double *bnum, *bden;  // [nchunk][J][Fp][KP]
-  int F, T, Fp, Tp, KP, J, ntt, tpc;
+  double *bnum;  // [nchunk][J][Fp][KP]
+  int F, T, Fp, Tp, KP, J, ntt, nft, tpc;
+  int fb_free[kMaxJ];
 };
 
-// One wave per (bin tile, source, frame chunk):
-//   num[f][k] = sum_t hat_W/V^2 * V * (FW.H)^T[t][k],  den = sum_t V/V * (FW.H)^T
-// (single-factor N1 quirk: other_fact_power == V, audioModel.py:1511-1520).
-template <int NKC>
+// FB numerator over t (:1521-1575), one wave per (FPW bin tiles, source,
+// frame chunk):  num[f][k] = sum_t (hat_W / V^2 * V) (FW.H)^T[t][k].
+// The single-factor quirk N1 makes other_fact_power == spat_comp_power == V,
+// so the denominator sum_t (V * (1/V)) (FW.H)^T[t][k] is the f-independent
+// sum_t (FW.H)^T[t][k] = (FW . rowsum(TW))[k] (to one rounding of V*(1/V));
+// k_fb_update forms it from hsum, and only the numerator is contracted here.
+// The V tiles reuse the A operand (TW) across the FPW bin tiles and the
+// (FW.H)^T B operand across them as well.
+template <int NKC, int FPW>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
+  constexpr int NKS = 4 * NKC;  // KP / 4
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
-  const int f0 = blockIdx.x * 16, j = blockIdx.y;
-  const int f = f0 + fl;
-  d4 num[NKC], den[NKC];
+  const int ft0 = blockIdx.x * FPW, j = blockIdx.y;
+  if (!a.fb_free[j]) return;
+  double wk[FPW][NKS];
 #pragma unroll
-  for (int kc = 0; kc < NKC; ++kc) num[kc] = den[kc] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int p = 0; p < FPW; ++p) {
+    const int f = (ft0 + p) * 16 + fl;
+    const bool fin = ft0 + p < a.nft;
+    const double *w = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) wk[p][s] = fin ? w[(size_t)(4 * s) * a.Fp] : 0.0;
+  }
+  d4 num[FPW][NKC];
+#pragma unroll
+  for (int p = 0; p < FPW; ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
-  const int nks = a.KP >> 2;
-  const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
-  const double *hw = a.hatW + (size_t)j * a.Tp * a.Fp + f;
-  const double *fwh = a.FWHt + (size_t)j * a.Tp * a.KP + fl;
+  const double *hwj = a.hatW + (size_t)j * a.Tp * a.Fp;
   for (int tt = tb; tt < te; ++tt) {
     const int t0 = tt * 16;
-    d4 v = d4{0.0, 0.0, 0.0, 0.0};
-    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
-    for (int s = 0; s < nks; ++s) v = mfma4(tw[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v);
-    double r1[4], r2[4];
+    double tw[NKS], fb[4][NKC];
+    const double *twp = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = t0 + tq + 4 * i;
-      const double h = hw[(size_t)t * a.Fp];
-      const double vm = fmax(v[i], kEps);
-      const double rv = 1.0 / vm;
-      const bool ok = t < a.T;
-      r1[i] = ok ? (h * (rv * rv)) * vm : 0.0;
-      r2[i] = ok ? vm * rv : 0.0;
-    }
+    for (int s = 0; s < NKS; ++s) tw[s] = twp[(size_t)(4 * s) * a.Tp];
+    const double *fwh = a.FWHt + ((size_t)j * a.Tp + t0 + tq) * a.KP + fl;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double *b = fwh + (size_t)(t0 + 4 * i + tq) * a.KP;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) {
-        const double bb = b[kc * 16];
-        num[kc] = mfma4(r1[i], bb, num[kc]);
-        den[kc] = mfma4(r2[i], bb, den[kc]);
+      for (int kc = 0; kc < NKC; ++kc) fb[i][kc] = fwh[(size_t)(4 * i) * a.KP + kc * 16];
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      if (ft0 + p >= a.nft) break;  // wave-uniform: no bin tile left
+      const int f = (ft0 + p) * 16 + fl;
+      double h[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h[i] = hwj[(size_t)(t0 + tq + 4 * i) * a.Fp + f];
+      d4 v = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) v = mfma4(tw[s], wk[p][s], v);
+      double r1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double vm = fmax(v[i], kEps);
+        const double rv = 1.0 / vm;
+        r1[i] = t0 + tq + 4 * i < a.T ? (h[i] * (rv * rv)) * vm : 0.0;
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) num[p][kc] = mfma4(r1[i], fb[i][kc], num[p][kc]);
     }
   }
   const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Fp;
 #pragma unroll
-  for (int kc = 0; kc < NKC; ++kc)
+  for (int p = 0; p < FPW; ++p) {
+    if (ft0 + p >= a.nft) break;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const size_t o = (base + f0 + tq + 4 * m) * a.KP + kc * 16 + fl;
-      a.bnum[o] = num[kc][m];
-      a.bden[o] = den[kc][m];
-    }
+    for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        a.bnum[(base + (ft0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl] = num[p][kc][m];
+  }
 }
 
 struct UArgs {
   double *FB;
-  const double *FW, *bnum, *bden;
+  const double *FW, *bnum, *hsum;
   double *Wkf_new, *Wfk_new;
   int F, Fp, KP, J, nchunk;
   double omega;
   int K[kMaxJ], fb_free[kMaxJ];
 };
+// FB *= (num / max(den, eps))^omega with den = FW . rowsum(TW) (see
+// k_fb_contract), then W_new = FB . FW in both layouts.
 __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double s_fb[];  // [16][KP]
+  extern __shared__ __attribute__((aligned(16))) double s_fb[];  // [16][KP] + [KP]
   const int f0 = blockIdx.x * 16, j = blockIdx.y;
   const int KP = a.KP;
+  double *s_den = s_fb + 16 * KP;
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
+    const double *fw = a.FW + ((size_t)j * KP + k) * KP;
+    const double *hs = a.hsum + (size_t)j * KP;
+    double d = 0.0;
+    for (int q = 0; q < KP; ++q) d += fw[q] * hs[q];
+    s_den[k] = d;
+  }
+  __syncthreads();
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int fl = idx / KP, k = idx % KP, f = f0 + fl;
     const size_t o = ((size_t)j * a.Fp + f) * KP + k;
     double fb = a.FB[o];
     if (a.fb_free[j] && f < a.F && k < a.K[j]) {
-      double num = 0.0, den = 0.0;
-      for (int c = 0; c < a.nchunk; ++c) {
-        const size_t po = (((size_t)c * a.J + j) * a.Fp + f) * KP + k;
-        num += a.bnum[po];
-        den += a.bden[po];
-      }
-      const double ratio = num / fmax(den, kEps);
+      double num = 0.0;
+      for (int c = 0; c < a.nchunk; ++c) num += a.bnum[(((size_t)c * a.J + j) * a.Fp + f) * KP + k];
+      const double ratio = num / fmax(s_den[k], kEps);
       fb *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
       a.FB[o] = fb;
     }
@@ -727,81 +757,141 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
 
 // ---------------------------------------------------------------- TW update
 struct TArgs {
+  const double *TW, *Wkf_old, *Wkf_new, *Wfk_new, *hatW;
+  double *tnum, *tden;  // [nsplit][J][Tp][KP]
+  int F, T, Fp, Tp, KP, J, nft, ntt, fpc;
+  int tw_free[kMaxJ];
+};
+
+// TW numerator / denominator over f (:1694-1726), one wave per (TPW frame
+// tiles, source, bin chunk):
+//   num[k][t] = sum_f W_new[f][k] * V_old * hat_W / V_new^2,
+//   den[k][t] = sum_f W_new[f][k] * V_old / V_new
+// V_old = W_old . TW, V_new = W_new . TW recomputed in registers; the W
+// operands (A of the V tiles, B of the contraction) are shared by the TPW
+// frame tiles.  Partial sums per bin chunk go to tnum / tden.
+template <int NKC, int TPW>
+__global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
+  constexpr int NKS = 4 * NKC;
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int tt0 = blockIdx.x * TPW, j = blockIdx.y;
+  if (!a.tw_free[j]) return;
+  double bt[TPW][NKS];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    const bool tin = tt0 + p < a.ntt;
+    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + (tt0 + p) * 16 + fl;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) bt[p][s] = tin ? tw[(size_t)(4 * s) * a.Tp] : 0.0;
+  }
+  d4 num[TPW][NKC], den[TPW][NKC];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+  const int fb = blockIdx.z * a.fpc, fe = min(fb + a.fpc, a.nft);
+  const double *wo = a.Wkf_old + ((size_t)j * a.KP + tq) * a.Fp + fl;
+  const double *wn = a.Wkf_new + ((size_t)j * a.KP + tq) * a.Fp + fl;
+  const double *wfk = a.Wfk_new + ((size_t)j * a.Fp + tq) * a.KP + fl;
+  const double *hwj = a.hatW + (size_t)j * a.Tp * a.Fp;
+  for (int ft = fb; ft < fe; ++ft) {
+    const int f0 = ft * 16;
+    double ao[NKS], an[NKS], bw[4][NKC];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      ao[s] = wo[(size_t)(4 * s) * a.Fp + f0];
+      an[s] = wn[(size_t)(4 * s) * a.Fp + f0];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) bw[i][kc] = wfk[(size_t)(f0 + 4 * i) * a.KP + kc * 16];
+#pragma unroll
+    for (int p = 0; p < TPW; ++p) {
+      if (tt0 + p >= a.ntt) break;  // wave-uniform: no frame tile left
+      const int t = (tt0 + p) * 16 + fl;
+      double h[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h[i] = hwj[(size_t)t * a.Fp + f0 + tq + 4 * i];
+      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        vo = mfma4(ao[s], bt[p][s], vo);
+        vn = mfma4(an[s], bt[p][s], vn);
+      }
+      const bool tok = t < a.T;
+      double r3[4], r4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double other = fmax(vo[i], kEps);
+        const double vm = fmax(vn[i], kEps);
+        const double rv = 1.0 / vm;
+        const bool ok = tok && f0 + tq + 4 * i < a.F;
+        r3[i] = ok ? other * (h[i] * (rv * rv)) : 0.0;
+        r4[i] = ok ? other * rv : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+          num[p][kc] = mfma4(r3[i], bw[i][kc], num[p][kc]);
+          den[p][kc] = mfma4(r4[i], bw[i][kc], den[p][kc]);
+        }
+    }
+  }
+  const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Tp;
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    if (tt0 + p >= a.ntt) break;
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const size_t o = (base + (tt0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl;
+        a.tnum[o] = num[p][kc][m];
+        a.tden[o] = den[p][kc][m];
+      }
+  }
+}
+
+struct TUArgs {
   double *TW;
-  const double *Wkf_old, *Wkf_new, *Wfk_new, *hatW;
-  int F, T, Fp, Tp, KP, nft;
+  const double *tnum, *tden;
+  int T, Tp, KP, J, nsplit;
   double omega;
   int K[kMaxJ], tw_free[kMaxJ];
 };
-
-// One wave per (frame tile, source), looping over all bins:
-//   num[k][t] = sum_f W_new[f][k] * V_old * hat_W / V_new^2,
-//   den[k][t] = sum_f W_new[f][k] * V_old / V_new            (:1694-1726)
-template <int NKC>
-__global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
-  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
-  const int t0 = blockIdx.x * 16, j = blockIdx.y;
-  const int t = t0 + fl;
-  const int nks = a.KP >> 2;
-  double bt[kMaxKP / 4];
-  {
-    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
-#pragma unroll
-    for (int s = 0; s < kMaxKP / 4; ++s) bt[s] = s < nks ? tw[(size_t)(4 * s) * a.Tp] : 0.0;
-  }
-  d4 num[NKC], den[NKC];
-#pragma unroll
-  for (int kc = 0; kc < NKC; ++kc) num[kc] = den[kc] = d4{0.0, 0.0, 0.0, 0.0};
-  const double *wo = a.Wkf_old + ((size_t)j * a.KP + tq) * a.Fp + fl;
-  const double *wn = a.Wkf_new + ((size_t)j * a.KP + tq) * a.Fp + fl;
-  const double *hw = a.hatW + ((size_t)j * a.Tp + t) * a.Fp;
-  const double *wfk = a.Wfk_new + (size_t)j * a.Fp * a.KP + fl;
-  const bool tok = t < a.T;
-  for (int ft = 0; ft < a.nft; ++ft) {
-    const int f0 = ft * 16;
-    d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
-#pragma unroll
-    for (int s = 0; s < kMaxKP / 4; ++s) {
-      if (s < nks) {
-        vo = mfma4(wo[(size_t)(4 * s) * a.Fp + f0], bt[s], vo);
-        vn = mfma4(wn[(size_t)(4 * s) * a.Fp + f0], bt[s], vn);
-      }
-    }
-    double r3[4], r4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = f0 + tq + 4 * i;
-      const double h = hw[f];
-      const double other = fmax(vo[i], kEps);
-      const double vm = fmax(vn[i], kEps);
-      const double rv = 1.0 / vm;
-      const bool ok = tok && f < a.F;
-      r3[i] = ok ? other * (h * (rv * rv)) : 0.0;
-      r4[i] = ok ? other * rv : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double *b = wfk + (size_t)(f0 + 4 * i + tq) * a.KP;
-#pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) {
-        const double bb = b[kc * 16];
-        num[kc] = mfma4(r3[i], bb, num[kc]);
-        den[kc] = mfma4(r4[i], bb, den[kc]);
-      }
-    }
-  }
+// TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
+__global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
+  __shared__ double s_r[64][65];
+  const int j = blockIdx.y, t0 = blockIdx.x * 64;
   if (!a.tw_free[j]) return;
-#pragma unroll
-  for (int kc = 0; kc < NKC; ++kc)
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int tt = t0 + tq + 4 * m, k = kc * 16 + fl;
-      if (tt < a.T && k < a.K[j]) {
-        const double ratio = num[kc][m] / fmax(den[kc][m], kEps);
-        double *p = a.TW + ((size_t)j * a.KP + k) * a.Tp + tt;
-        *p *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
+  // ratios for 64 frames x KP components (coalesced over k), then a
+  // transposed, coalesced-over-t read-modify-write of TW
+  for (int kb = 0; kb < a.KP; kb += 64) {
+    const int kn = min(64, a.KP - kb);
+    for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
+      const int tl = idx / kn, kl = idx % kn, t = t0 + tl;
+      double r = 1.0;
+      if (t < a.T) {
+        double num = 0.0, den = 0.0;
+        for (int c = 0; c < a.nsplit; ++c) {
+          const size_t o = (((size_t)c * a.J + j) * a.Tp + t) * a.KP + kb + kl;
+          num += a.tnum[o];
+          den += a.tden[o];
+        }
+        const double ratio = num / fmax(den, kEps);
+        r = a.omega == 1.0 ? ratio : pow(ratio, a.omega);
       }
+      s_r[kl][tl] = r;
     }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
+      const int kl = idx / 64, tl = idx % 64, t = t0 + tl, k = kb + kl;
+      if (t < a.T && k < a.K[j]) a.TW[((size_t)j * a.KP + k) * a.Tp + t] *= s_r[kl][tl];
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- renormalize
@@ -939,11 +1029,11 @@ __global__ void k_renorm_flags(const RArgs a, int J) {
 
 // ---------------------------------------------------------------- host side
 enum KernelId {
-  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN
+  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU
 };
 static const char *kKernelNames[fasst_ctx::kNK] = {
     "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep", "k_loglik", "k_mix",
-    "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm"};
+    "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm", "k_tw_update"};
 
 static inline void prof_begin(fasst_ctx *c, int id) {
   if (c->prof) {
@@ -1009,10 +1099,17 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   c->tpc_e = std::max(4, (c->ntt + 7) / 8);
   while (c->tpc_e > 4 && (size_t)c->nft * ((c->ntt + c->tpc_e - 1) / c->tpc_e) < 1024) c->tpc_e /= 2;
   c->nchunk_e = (c->ntt + c->tpc_e - 1) / c->tpc_e;
-  c->tpc_b = std::max(1, (c->ntt + 3) / 4);
-  while (c->tpc_b > 8 && (size_t)c->nft * J * ((c->ntt + c->tpc_b - 1) / c->tpc_b) < 2048)
-    c->tpc_b /= 2;
+  // contractions: ~4096+ waves (4 per SIMD) so each SIMD holds several
+  const long fb_waves = (long)((c->nft + kFPW - 1) / kFPW) * J;
+  c->nchunk_b = 1;
+  while (fb_waves * c->nchunk_b < 4096 && c->ntt / (2 * c->nchunk_b) >= 8) c->nchunk_b *= 2;
+  c->tpc_b = (c->ntt + c->nchunk_b - 1) / c->nchunk_b;
   c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
+  const long tw_waves = (long)((c->ntt + kTPW - 1) / kTPW) * J;
+  c->nsplit_t = 1;
+  while (tw_waves * c->nsplit_t < 4096 && c->nft / (2 * c->nsplit_t) >= 8) c->nsplit_t *= 2;
+  c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
+  c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
   const int NP = J * (J + 1) / 2;
   c->nacc = 4 * NP + 8 * J;
   int st;
@@ -1031,7 +1128,8 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(epart, (size_t)c->nchunk_e * Fp * c->nacc);
   ALLOC(llpart, (size_t)c->nchunk_e * c->nft);
   ALLOC(bnum, (size_t)c->nchunk_b * J * Fp * KP);
-  ALLOC(bden, (size_t)c->nchunk_b * J * Fp * KP);
+  ALLOC(tnum, (size_t)c->nsplit_t * J * Tp * KP);
+  ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
   ALLOC(flags, 1 + kMaxJ);
@@ -1144,11 +1242,13 @@ template <int NKC>
 static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb) {
   if (fb) {
     prof_begin(c, KFBC);
-    k_fb_contract<NKC><<<dim3(c->nft, c->J, c->nchunk_b), 64, 0, c->stream>>>(b);
+    k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, c->nchunk_b), 64, 0,
+                               c->stream>>>(b);
     prof_end(c, KFBC);
   } else {
     prof_begin(c, KTWC);
-    k_tw_contract<NKC><<<dim3(c->ntt, c->J), 64, 0, c->stream>>>(t);
+    k_tw_contract<NKC, kTPW><<<dim3((c->ntt + kTPW - 1) / kTPW, c->J, c->nsplit_t), 64, 0,
+                               c->stream>>>(t);
     prof_end(c, KTWC);
   }
 }
@@ -1262,7 +1362,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   b.FWHt = c->FWHt.p;
   b.hatW = c->hatW.p;
   b.bnum = c->bnum.p;
-  b.bden = c->bden.p;
   b.F = c->F;
   b.T = c->T;
   b.Fp = c->Fp;
@@ -1270,6 +1369,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   b.KP = c->KP;
   b.J = J;
   b.ntt = c->ntt;
+  b.nft = c->nft;
   b.tpc = c->tpc_b;
   TArgs t;
   t.TW = c->TW.p;
@@ -1277,18 +1377,32 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   t.Wkf_new = c->Wkf_new.p;
   t.Wfk_new = c->Wfk_new.p;
   t.hatW = c->hatW.p;
+  t.tnum = c->tnum.p;
+  t.tden = c->tden.p;
   t.F = c->F;
   t.T = c->T;
   t.Fp = c->Fp;
   t.Tp = c->Tp;
   t.KP = c->KP;
+  t.J = J;
   t.nft = c->nft;
-  t.omega = omega;
+  t.ntt = c->ntt;
+  t.fpc = c->fpc_t;
+  TUArgs tu;
+  tu.TW = c->TW.p;
+  tu.tnum = c->tnum.p;
+  tu.tden = c->tden.p;
+  tu.T = c->T;
+  tu.Tp = c->Tp;
+  tu.KP = c->KP;
+  tu.J = J;
+  tu.nsplit = c->nsplit_t;
+  tu.omega = omega;
   UArgs u;
   u.FB = c->FB.p;
   u.FW = c->FW.p;
   u.bnum = c->bnum.p;
-  u.bden = c->bden.p;
+  u.hsum = c->hsum.p;
   u.Wkf_new = c->Wkf_new.p;
   u.Wfk_new = c->Wfk_new.p;
   u.F = c->F;
@@ -1299,28 +1413,30 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   u.omega = omega;
   for (int j = 0; j < kMaxJ; ++j) {
     const bool in = j < J;
-    t.K[j] = u.K[j] = in ? c->K[j] : 0;
-    t.tw_free[j] = in ? c->tw_free[j] : 0;
-    u.fb_free[j] = in ? c->fb_free[j] : 0;
+    tu.K[j] = u.K[j] = in ? c->K[j] : 0;
+    t.tw_free[j] = tu.tw_free[j] = in ? c->tw_free[j] : 0;
+    b.fb_free[j] = u.fb_free[j] = in ? c->fb_free[j] : 0;
   }
   const int nkc = c->KP / 16;
   switch (nkc) {
     case 1: launch_contract<1>(c, b, t, true); break;
     case 2: launch_contract<2>(c, b, t, true); break;
-    case 3: launch_contract<3>(c, b, t, true); break;
     default: launch_contract<4>(c, b, t, true); break;
   }
   FASST_LAUNCH_CHECK();
   prof_begin(c, KFBU);
-  k_fb_update<<<dim3(c->nft, J), 256, 16 * c->KP * sizeof(double), c->stream>>>(u);
+  k_fb_update<<<dim3(c->nft, J), 256, 17 * c->KP * sizeof(double), c->stream>>>(u);
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
   switch (nkc) {
     case 1: launch_contract<1>(c, b, t, false); break;
     case 2: launch_contract<2>(c, b, t, false); break;
-    case 3: launch_contract<3>(c, b, t, false); break;
     default: launch_contract<4>(c, b, t, false); break;
   }
+  FASST_LAUNCH_CHECK();
+  prof_begin(c, KTWU);
+  k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
+  prof_end(c, KTWU);
   FASST_LAUNCH_CHECK();
   return launch_renorm(c);
 }
@@ -1405,7 +1521,8 @@ int fasst_destroy(fasst_ctx *c) {
     c->epart.release();
     c->llpart.release();
     c->bnum.release();
-    c->bden.release();
+    c->tnum.release();
+    c->tden.release();
     c->psd.release();
     c->ll.release();
     c->rss.release();
