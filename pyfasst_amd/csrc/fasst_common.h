@@ -15,6 +15,7 @@ constexpr int kMaxJ = 4;        // sources handled by the fused E-step
 constexpr int kMaxR = 8;        // total spatial rank
 constexpr int kMaxKP = 64;      // padded NMF components
 constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge
+constexpr int kFlagHalt = 1 + kMaxJ, kFlagIter = 2 + kMaxJ, kNFlags = 3 + kMaxJ;
 constexpr int kFPW = 2;         // bin tiles per wave, FB contraction
 constexpr int kTPW = 2;         // frame tiles per wave, TW contraction
 

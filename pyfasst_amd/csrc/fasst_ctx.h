@@ -35,11 +35,13 @@ struct fasst_ctx {
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
   int nsplit_t = 1, fpc_t = 1;  // TW contraction bin chunks
-  fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rtpart;
+  fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rpmax, rpe, rtpart;
   int nchunk_r = 1;
   fasst::DBuf<double2> rss, rxs;
-  fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart
+  fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart, [kFlagHalt] halt,
+                                 // [kFlagIter] iteration that raised a restart
   int *h_flags = nullptr;        // pinned host mirror
+  const int *halt = nullptr;     // flags + kFlagHalt while fasst_run enqueues a batch
   double *h_ll = nullptr;        // pinned host mirror (one value)
   int psd_cap = 0, ll_cap = 0;
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)

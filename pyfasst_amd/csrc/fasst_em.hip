@@ -41,27 +41,46 @@ void set_error(const char *fmt, ...) {
   g_err = buf;
 }
 
+// Device-side halt: once an iteration raises a flag (singular mixing solve,
+// dead TW) every later kernel of the batch returns at entry, so a batch of
+// iterations is enqueued without host round trips and the state stays the
+// one the flagged iteration left (flags layout in fasst_ctx.h).
+#define HALT_GUARD(h)                                   \
+  do {                                                  \
+    if ((h) && *(volatile const int *)(h)) return;      \
+  } while (0)
+
 __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------- prep
 // W[j] = FB[j] . FW[j], written [KP][Fp] (f contiguous).
-__global__ void k_w_from_fb(const double *__restrict__ FB, const double *__restrict__ FW,
-                            double *__restrict__ Wkf, double *__restrict__ Wfk, int J, int Fp,
-                            int KP) {
-  const size_t n = (size_t)J * Fp * KP;
-  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    const int f = idx % Fp;
-    const int k = (idx / Fp) % KP;
-    const int j = idx / ((size_t)Fp * KP);
-    const double *fb = FB + ((size_t)j * Fp + f) * KP;
-    const double *fw = FW + (size_t)j * KP * KP + k;
+// one block per (16-bin tile, source): FB tile and FW staged in LDS; the
+// outputs are written bin-fastest (coalesced Wkf rows)
+__global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB,
+                                                   const double *__restrict__ FW,
+                                                   double *__restrict__ Wkf,
+                                                   double *__restrict__ Wfk, int J, int Fp,
+                                                   int KP, const int *halt) {
+  HALT_GUARD(halt);
+  extern __shared__ __attribute__((aligned(16))) double s_m[];
+  double *s_fb = s_m;             // [16][KP + 1]
+  double *s_fw = s_m + 16 * (KP + 1);  // [KP][KP]
+  const int j = blockIdx.y, f0 = blockIdx.x * 16;
+  for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+    const int fl = idx / KP, q = idx % KP;
+    s_fb[fl * (KP + 1) + q] = FB[((size_t)j * Fp + f0 + fl) * KP + q];
+  }
+  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
+    s_fw[idx] = FW[(size_t)j * KP * KP + idx];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+    const int k = idx / 16, fl = idx % 16;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += fb[q] * fw[(size_t)q * KP];
-    Wkf[((size_t)j * KP + k) * Fp + f] = s;
-    if (Wfk) Wfk[((size_t)j * Fp + f) * KP + k] = s;
+    for (int q = 0; q < KP; ++q) s += s_fb[fl * (KP + 1) + q] * s_fw[q * KP + k];
+    Wkf[((size_t)j * KP + k) * Fp + f0 + fl] = s;
+    if (Wfk) Wfk[((size_t)j * Fp + f0 + fl) * KP + k] = s;
   }
 }
 
@@ -69,14 +88,17 @@ __global__ void k_w_from_fb(const double *__restrict__ FB, const double *__restr
 // tile, source): FW and the TW tile staged in LDS, coalesced [t][k] writes.
 __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
                                                const double *__restrict__ TW,
-                                               double *__restrict__ FWHt, int J, int Tp, int KP) {
+                                               double *__restrict__ FWHt, int J, int Tp, int KP, const int *halt) {
+  HALT_GUARD(halt);
   extern __shared__ __attribute__((aligned(16))) double s_f[];
   double *s_fw = s_f;             // [KP][KP]
   double *s_tw = s_f + KP * KP;   // [KP][64]
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
   const int tn = min(64, Tp - t0);
-  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
-    s_fw[idx] = FW[(size_t)j * KP * KP + idx];
+  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
+    const int k = idx / KP, q = idx % KP;  // stored transposed: s_fw[q][k]
+    s_fw[q * KP + k] = FW[(size_t)j * KP * KP + idx];
+  }
   for (int idx = threadIdx.x; idx < KP * 64; idx += blockDim.x) {
     const int q = idx >> 6, tl = idx & 63;
     s_tw[idx] = tl < tn ? TW[((size_t)j * KP + q) * Tp + t0 + tl] : 0.0;
@@ -85,14 +107,15 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
   for (int idx = threadIdx.x; idx < tn * KP; idx += blockDim.x) {
     const int tl = idx / KP, k = idx % KP;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += s_fw[k * KP + q] * s_tw[q * 64 + tl];
+    for (int q = 0; q < KP; ++q) s += s_fw[q * KP + k] * s_tw[q * 64 + tl];
     FWHt[((size_t)j * Tp + t0 + tl) * KP + k] = s;
   }
 }
 
 // 'inst' mixing replicated over bins: A[r][c][f] = params[c][r]
 __global__ void k_inst_A(const double2 *__restrict__ Pinst, double2 *__restrict__ A, int R,
-                         int F, int Fp) {
+                         int F, int Fp, const int *halt) {
+  HALT_GUARD(halt);
   const int n = R * 2 * Fp;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
     const int f = idx % Fp;
@@ -113,6 +136,7 @@ struct EArgs {
   double *llpart;                         // [nchunk][nft]
   int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
   int roff[kMaxJ + 1];
+  const int *halt;
 };
 
 // Block: 4 waves on one 16-bin tile; wave w walks frame tiles w, w+4, ... of
@@ -125,8 +149,15 @@ struct EArgs {
 // NKS = KP/4 MFMA k-steps; RKU = 1 or 2: every source has that rank (no
 // predication), 0: general ranks <= kMaxR.  AB = ablation bits (profiling
 // builds only, 0 in the product).
+#ifndef ESTEP_MINB1
+#define ESTEP_MINB1 2
+#endif
+#ifndef ESTEP_MINB2
+#define ESTEP_MINB2 2
+#endif
 template <int J, int NKS, int RKU, int PART, int AB>
-__global__ __launch_bounds__(256, 2) void k_estep(const EArgs a) {
+__global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_estep(const EArgs a) {
+  HALT_GUARD(a.halt);
   constexpr int NP = J * (J + 1) / 2;
   constexpr int NACC = PART == 1 ? 4 * NP : 8 * J;
   constexpr int UOFF = PART == 1 ? 0 : 4 * NP;   // column offset in the partial rows
@@ -359,7 +390,8 @@ __global__ __launch_bounds__(256, 2) void k_estep(const EArgs a) {
 
 // sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
 __global__ void k_tw_rowsum(const double *__restrict__ TW, double *__restrict__ hsum, int T,
-                            int Tp) {
+                            int Tp, const int *halt) {
+  HALT_GUARD(halt);
   __shared__ double s[256];
   const double *row = TW + (size_t)blockIdx.x * Tp;
   double x = 0.0;
@@ -374,7 +406,8 @@ __global__ void k_tw_rowsum(const double *__restrict__ TW, double *__restrict__ 
 }
 
 __global__ void k_loglik(const double *__restrict__ llpart, int n, double *__restrict__ out,
-                         double inv_FT) {
+                         double inv_FT, const int *halt) {
+  HALT_GUARD(halt);
   __shared__ double s[256];
   double x = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) x += llpart[i];
@@ -398,6 +431,7 @@ struct MArgs {
   int F, Fp, J, R, nchunk, nacc, conv_update, KP;
   double invT;
   int jr[kMaxR];
+  const int *halt;
 };
 
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
@@ -429,6 +463,7 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 // matrix entries spread over the lanes; for 'inst' the per-bin statistics are
 // stored for k_mix_inst.
 __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
+  HALT_GUARD(a.halt);
   __shared__ double s_acc[4 * 10 + 8 * kMaxJ];
   __shared__ double2 s_A[kMaxR][2];
   __shared__ double2 s_L[kMaxR][kMaxR + 2];   // [M^T | hat_Rxs^T]
@@ -513,7 +548,10 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
       }
     }
     if (m == 0.0) {
-      if (lane == 0) atomicOr(a.flags, 1);
+      if (lane == 0) {
+        atomicOr(a.flags, 1);
+        atomicOr(a.flags + kFlagHalt, 1);
+      }
       return;
     }
     if (mi != k && lane < W) {
@@ -549,8 +587,10 @@ struct IArgs {
   int *flags;
   int F, Fp, R, nu, no;
   int upd[kMaxR], oth[kMaxR];
+  const int *halt;
 };
 __global__ void k_mix_inst(const IArgs a) {
+  HALT_GUARD(a.halt);
   __shared__ double s_b[kMaxR][2];
   __shared__ double s_m[kMaxR][kMaxR];
   const int nu = a.nu, R = a.R;
@@ -593,6 +633,7 @@ __global__ void k_mix_inst(const IArgs a) {
       }
     if (best == 0.0) {
       atomicOr(a.flags, 1);
+      atomicOr(a.flags + kFlagHalt, 1);
       return;
     }
     if (piv != k) {
@@ -630,6 +671,7 @@ struct BArgs {
   double *bnum;  // [nchunk][J][Fp][KP]
   int F, T, Fp, Tp, KP, J, ntt, nft, tpc;
   int fb_free[kMaxJ];
+  const int *halt;
 };
 
 // FB numerator over t (:1521-1575), one wave per (FPW bin tiles, source,
@@ -642,6 +684,7 @@ struct BArgs {
 // (FW.H)^T B operand across them as well.
 template <int NKC, int FPW>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
+  HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;  // KP / 4
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
   const int ft0 = blockIdx.x * FPW, j = blockIdx.y;
@@ -715,10 +758,12 @@ struct UArgs {
   int F, Fp, KP, J, nchunk;
   double omega;
   int K[kMaxJ], fb_free[kMaxJ];
+  const int *halt;
 };
 // FB *= (num / max(den, eps))^omega with den = FW . rowsum(TW) (see
 // k_fb_contract), then W_new = FB . FW in both layouts.
 __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
+  HALT_GUARD(a.halt);
   extern __shared__ __attribute__((aligned(16))) double s_fb[];  // [16][KP] + [KP]
   const int f0 = blockIdx.x * 16, j = blockIdx.y;
   const int KP = a.KP;
@@ -761,6 +806,7 @@ struct TArgs {
   double *tnum, *tden;  // [nsplit][J][Tp][KP]
   int F, T, Fp, Tp, KP, J, nft, ntt, fpc;
   int tw_free[kMaxJ];
+  const int *halt;
 };
 
 // TW numerator / denominator over f (:1694-1726), one wave per (TPW frame
@@ -772,6 +818,7 @@ struct TArgs {
 // frame tiles.  Partial sums per bin chunk go to tnum / tden.
 template <int NKC, int TPW>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
+  HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
   const int tt0 = blockIdx.x * TPW, j = blockIdx.y;
@@ -860,9 +907,11 @@ struct TUArgs {
   int T, Tp, KP, J, nsplit;
   double omega;
   int K[kMaxJ], tw_free[kMaxJ];
+  const int *halt;
 };
 // TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
 __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
+  HALT_GUARD(a.halt);
   __shared__ double s_r[64][65];
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
   if (!a.tw_free[j]) return;
@@ -898,11 +947,14 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
 struct RArgs {
   double2 *A, *Pinst;
   double *FB, *FW, *TW;
-  double *scal;   // [J][2 + 2*KP]: e_j, -, w_j[KP], w2_j[KP]
+  double *scal;   // [J][2 + 2*KP]: e_j, -, w_j[KP], w2_j[KP] (stage 2 -> 3)
+  double *pmax;   // [J][nchunk][KP] column maxima of FB per bin chunk
+  double *pe;     // [J][nchunk] partial mixing-filter energy (conv)
   double *tpart;  // [J][nchunk] partial sums of the rescaled TW
   int *flags;
-  int F, T, Fp, Tp, KP, conv, nchunk, tpc;
+  int F, T, Fp, Tp, KP, conv, nchunk, tpc, fpc;
   int K[kMaxJ], roff[kMaxJ + 1];
+  const int *halt;
 };
 
 __device__ double block_sum(double x, double *s) {
@@ -917,93 +969,115 @@ __device__ double block_sum(double x, double *s) {
   return r;
 }
 
-__device__ double spatial_energy(const RArgs &a, int j, double *s_red) {
-  const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
-  double e = 0.0;
+// renormalize_parameters (audioModel.py:1991-2037) in two passes over
+// (source, chunk) blocks.  Stage 1: per bin chunk, the column maxima of FB
+// and (conv) the partial energy of the mixing filters.  Since x -> fl(x e) is
+// monotone for e >= 0, max_f fl(FB e) = fl(e max_f FB): the maxima are taken
+// on the raw FB and scaled in stage 2.
+__global__ __launch_bounds__(256) void k_renorm_stats(const RArgs a) {
+  HALT_GUARD(a.halt);
+  __shared__ double s_red[256];
+  const int j = blockIdx.y, c = blockIdx.x, KP = a.KP;
+  const int fb = c * a.fpc, fe = min(fb + a.fpc, a.F);
+  const int groups = blockDim.x / KP, k = threadIdx.x % KP, g = threadIdx.x / KP;
+  double m = -INFINITY;
+  if (g < groups)
+    for (int f = fb + g; f < fe; f += groups) m = fmax(m, a.FB[((size_t)j * a.Fp + f) * KP + k]);
+  s_red[threadIdx.x] = m;
+  __syncthreads();
+  if (threadIdx.x < KP) {
+    double x = s_red[threadIdx.x];
+    for (int q = 1; q < groups; ++q) x = fmax(x, s_red[q * KP + threadIdx.x]);
+    a.pmax[((size_t)j * a.nchunk + c) * KP + threadIdx.x] = x;
+  }
+  __syncthreads();
   if (a.conv) {
-    const int n = nr * 2 * a.F;
-    for (int idx = threadIdx.x; idx < n; idx += blockDim.x) {
-      const int f = idx % a.F, rc = idx / a.F;
+    const int r0 = a.roff[j], nr = a.roff[j + 1] - r0, w = fe - fb;
+    double e = 0.0;
+    for (int idx = threadIdx.x; idx < nr * 2 * w; idx += blockDim.x) {
+      const int f = fb + idx % w, rc = idx / w;
       const double2 x = a.A[(size_t)(2 * r0 + rc) * a.Fp + f];
       e += x.x * x.x + x.y * x.y;
     }
-    return block_sum(e, s_red) / (double)n;
-  }
-  for (int idx = threadIdx.x; idx < nr * 2; idx += blockDim.x) {
-    const double2 x = a.Pinst[2 * r0 + idx];
-    e += x.x * x.x + x.y * x.y;
-  }
-  return block_sum(e, s_red) / (double)(nr * 2);
-}
-
-// renormalize_parameters (audioModel.py:1991-2037), stage 1: one 256-thread
-// block per (source j, NMF column k): e_j = mean|params_j|^2 (recomputed per
-// block, it is tiny), FB[:,k] *= e_j, w = max_f FB[:,k] (0 -> 1), FB[:,k] /= w.
-__global__ __launch_bounds__(256) void k_renorm_fb(const RArgs a) {
-  __shared__ double s_red[256];
-  const int j = blockIdx.y, k = blockIdx.x;
-  const double e = spatial_energy(a, j, s_red);
-  if (k >= a.K[j]) return;
-  double *col = a.FB + (size_t)j * a.Fp * a.KP + k;
-  double m = -INFINITY;
-  for (int f = threadIdx.x; f < a.F; f += blockDim.x) {
-    const double x = col[(size_t)f * a.KP] * e;
-    col[(size_t)f * a.KP] = x;
-    m = fmax(m, x);
-  }
-  s_red[threadIdx.x] = m;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) s_red[threadIdx.x] = fmax(s_red[threadIdx.x], s_red[threadIdx.x + w]);
-    __syncthreads();
-  }
-  const double wk = s_red[0] == 0.0 ? 1.0 : s_red[0];
-  for (int f = threadIdx.x; f < a.F; f += blockDim.x) col[(size_t)f * a.KP] /= wk;
-  if (threadIdx.x == 0) {
-    double *sc = a.scal + (size_t)j * (2 + 2 * a.KP);
-    sc[2 + k] = wk;
-    if (k == 0) sc[0] = e;
+    e = block_sum(e, s_red);
+    if (threadIdx.x == 0) a.pe[(size_t)j * a.nchunk + c] = e;
   }
 }
 
-// stage 2: one block per (source, frame chunk): FW *= w (rows), w2 = mean
-// over rows, FW /= w2 (chunk 0 writes FW, the others recompute w2), TW[:,
-// chunk] *= w2, params /= sqrt(e) (chunk 0), partial sum of TW.
-__global__ __launch_bounds__(256) void k_renorm_tw(const RArgs a) {
+// Stage 2: every block recombines the (tiny) stage-1 partials into e_j,
+// w_j[k] = max_f FB[:,k] e_j (0 -> 1) and w2_j[c] = mean_r FW[r,c] w_j[r]
+// (0 -> 1), then scales its chunk: FB rows (FB e / w), TW columns (TW w2,
+// with partial sums for the restart test), the mixing filters / sqrt(e).
+// FW and the 'inst' parameters are read by every block here, so they are
+// rewritten in stage 3 from the scales chunk 0 records.
+__global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
+  HALT_GUARD(a.halt);
   __shared__ double s_red[256];
-  __shared__ double s_w2[kMaxKP];
-  const int j = blockIdx.y, chunk = blockIdx.x;
+  __shared__ double s_w[kMaxKP], s_w2[kMaxKP];
+  __shared__ double s_e;
+  const int j = blockIdx.y, c = blockIdx.x;
   const int K = a.K[j], KP = a.KP;
-  const double *sc = a.scal + (size_t)j * (2 + 2 * KP);
-  double *FW = a.FW + (size_t)j * KP * KP;
-  if (threadIdx.x < K) {
-    const int c = threadIdx.x;
-    double s = 0.0;
-    for (int r = 0; r < K; ++r) s += FW[r * KP + c] * sc[2 + r];
-    s /= (double)K;
-    s_w2[c] = s == 0.0 ? 1.0 : s;
+  const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+  if (threadIdx.x == 0) {
+    double e = 0.0;
+    if (a.conv) {
+      for (int q = 0; q < a.nchunk; ++q) e += a.pe[(size_t)j * a.nchunk + q];
+      e /= (double)(nr * 2 * a.F);
+    } else {
+      for (int q = 0; q < nr * 2; ++q) {
+        const double2 x = a.Pinst[2 * r0 + q];
+        e += x.x * x.x + x.y * x.y;
+      }
+      e /= (double)(nr * 2);
+    }
+    s_e = e;
   }
   __syncthreads();
-  if (chunk == 0) {
-    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
-      const int r = idx / K, c = idx % K;
-      FW[r * KP + c] = (FW[r * KP + c] * sc[2 + r]) / s_w2[c];
+  const double e = s_e;
+  if (threadIdx.x < KP) {
+    double m = -INFINITY;
+    for (int q = 0; q < a.nchunk; ++q) m = fmax(m, a.pmax[((size_t)j * a.nchunk + q) * KP + threadIdx.x]);
+    const double w = m * e;
+    s_w[threadIdx.x] = w == 0.0 ? 1.0 : w;
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int cc = threadIdx.x;
+    const double *FW = a.FW + (size_t)j * KP * KP;
+    double s = 0.0;
+    for (int r = 0; r < K; ++r) s += FW[r * KP + cc] * s_w[r];
+    s /= (double)K;
+    s_w2[cc] = s == 0.0 ? 1.0 : s;
+  }
+  __syncthreads();
+  // FB rows of this chunk (only the K live columns carry data)
+  const int fb = c * a.fpc, fe = min(fb + a.fpc, a.F);
+  for (int idx = threadIdx.x; idx < (fe - fb) * KP; idx += blockDim.x) {
+    const int f = fb + idx / KP, k = idx % KP;
+    if (k < K) {
+      double *p = a.FB + ((size_t)j * a.Fp + f) * KP + k;
+      *p = (*p * e) / s_w[k];
     }
-    const double se = sqrt(sc[0]);
-    const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
-    if (a.conv) {
-      for (int idx = threadIdx.x; idx < nr * 2 * a.F; idx += blockDim.x) {
-        const int f = idx % a.F, rc = idx / a.F;
-        double2 *p = a.A + (size_t)(2 * r0 + rc) * a.Fp + f;
-        *p = make_double2(p->x / se, p->y / se);
-      }
-    } else if (threadIdx.x < nr * 2) {
-      double2 *p = a.Pinst + 2 * r0 + threadIdx.x;
+  }
+  const double se = sqrt(e);
+  if (a.conv) {
+    const int w = fe - fb;
+    for (int idx = threadIdx.x; idx < nr * 2 * w; idx += blockDim.x) {
+      const int f = fb + idx % w, rc = idx / w;
+      double2 *p = a.A + (size_t)(2 * r0 + rc) * a.Fp + f;
       *p = make_double2(p->x / se, p->y / se);
     }
   }
+  if (c == 0) {  // FW and 'inst' parameters are rewritten in stage 3 (read above)
+    double *sc = a.scal + (size_t)j * (2 + 2 * KP);
+    if (threadIdx.x == 0) sc[0] = e;
+    if (threadIdx.x < KP) {
+      sc[2 + threadIdx.x] = s_w[threadIdx.x];
+      sc[2 + KP + threadIdx.x] = s_w2[threadIdx.x];
+    }
+  }
   double *TW = a.TW + (size_t)j * KP * a.Tp;
-  const int t0 = chunk * a.tpc, t1 = min(t0 + a.tpc, a.T);
+  const int t0 = c * a.tpc, t1 = min(t0 + a.tpc, a.T);
   const int w = t1 - t0;
   double tsum = 0.0;
   if (w > 0)
@@ -1015,16 +1089,39 @@ __global__ __launch_bounds__(256) void k_renorm_tw(const RArgs a) {
       tsum += x;
     }
   tsum = block_sum(tsum, s_red);
-  if (threadIdx.x == 0) a.tpart[(size_t)j * a.nchunk + chunk] = tsum;
+  if (threadIdx.x == 0) a.tpart[(size_t)j * a.nchunk + c] = tsum;
 }
 
-// stage 3: sum(TW_j) < eps -> host-side random restart (audioModel.py:2023)
-__global__ void k_renorm_flags(const RArgs a, int J) {
+// Stage 3 (one block): FW = FW w / w2, 'inst' parameters / sqrt(e), and the
+// restart test sum(TW_j) < eps -> host-side random restart (audioModel.py:2023)
+__global__ void k_renorm_final(const RArgs a, int J, int iter) {
+  HALT_GUARD(a.halt);
+  for (int j = 0; j < J; ++j) {
+    const int K = a.K[j], KP = a.KP;
+    const double *sc = a.scal + (size_t)j * (2 + 2 * KP);
+    double *FW = a.FW + (size_t)j * KP * KP;
+    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+      const int r = idx / K, cc = idx % K;
+      FW[r * KP + cc] = (FW[r * KP + cc] * sc[2 + r]) / sc[2 + KP + cc];
+    }
+    const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+    if (!a.conv && threadIdx.x < nr * 2) {
+      const double se = sqrt(sc[0]);
+      double2 *p = a.Pinst + 2 * r0 + threadIdx.x;
+      *p = make_double2(p->x / se, p->y / se);
+    }
+  }
+  __syncthreads();
   const int j = threadIdx.x;
   if (j >= J) return;
   double s = 0.0;
   for (int c = 0; c < a.nchunk; ++c) s += a.tpart[(size_t)j * a.nchunk + c];
-  a.flags[1 + j] = s < kEps ? 1 : 0;
+  const int dead = s < kEps ? 1 : 0;
+  a.flags[1 + j] = dead;
+  if (dead) {
+    a.flags[kFlagHalt] = 1;
+    a.flags[kFlagIter] = iter;
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -1132,10 +1229,12 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
-  ALLOC(flags, 1 + kMaxJ);
+  ALLOC(flags, kNFlags);
   ALLOC(hsum, (size_t)J * KP);
-  c->nchunk_r = std::max(1, std::min(64, (c->T + 255) / 256));
+  c->nchunk_r = std::max(1, std::min(64, std::min((c->T + 255) / 256, (c->F + 15) / 16)));
   ALLOC(rscal, (size_t)J * (2 + 2 * KP));
+  ALLOC(rpmax, (size_t)J * c->nchunk_r * KP);
+  ALLOC(rpe, (size_t)J * c->nchunk_r);
   ALLOC(rtpart, (size_t)J * c->nchunk_r);
 #undef ALLOC
   c->configured = 1;
@@ -1146,7 +1245,7 @@ int build_inst_A(fasst_ctx *c) {
   if (c->conv) return FASST_OK;
   prof_begin(c, KINSTA);
   k_inst_A<<<launch_grid((size_t)c->R * 2 * c->Fp), 256, 0, c->stream>>>(c->Pinst.p, c->A.p, c->R,
-                                                                        c->F, c->Fp);
+                                                                        c->F, c->Fp, c->halt);
   prof_end(c, KINSTA);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
@@ -1154,14 +1253,14 @@ int build_inst_A(fasst_ctx *c) {
 
 int launch_w_old(fasst_ctx *c) {
   prof_begin(c, KW);
-  k_w_from_fb<<<launch_grid((size_t)c->J * c->Fp * c->KP), 256, 0, c->stream>>>(
-      c->FB.p, c->FW.p, c->Wkf.p, nullptr, c->J, c->Fp, c->KP);
+  k_w_from_fb<<<dim3(c->nft, c->J), 256, (size_t)(16 * (c->KP + 1) + c->KP * c->KP) * sizeof(double),
+                c->stream>>>(c->FB.p, c->FW.p, c->Wkf.p, nullptr, c->J, c->Fp, c->KP, c->halt);
   prof_end(c, KW);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
 }
 
-static int launch_renorm(fasst_ctx *c) {
+static int launch_renorm(fasst_ctx *c, int iter) {
   RArgs r;
   r.A = c->A.p;
   r.Pinst = c->Pinst.p;
@@ -1169,8 +1268,11 @@ static int launch_renorm(fasst_ctx *c) {
   r.FW = c->FW.p;
   r.TW = c->TW.p;
   r.scal = c->rscal.p;
+  r.pmax = c->rpmax.p;
+  r.pe = c->rpe.p;
   r.tpart = c->rtpart.p;
   r.flags = c->flags.p;
+  r.halt = c->halt;
   r.F = c->F;
   r.T = c->T;
   r.Fp = c->Fp;
@@ -1179,12 +1281,13 @@ static int launch_renorm(fasst_ctx *c) {
   r.conv = c->conv;
   r.nchunk = c->nchunk_r;
   r.tpc = (c->T + c->nchunk_r - 1) / c->nchunk_r;
+  r.fpc = (c->F + c->nchunk_r - 1) / c->nchunk_r;
   for (int j = 0; j < kMaxJ; ++j) r.K[j] = j < c->J ? c->K[j] : 0;
   for (int j = 0; j <= kMaxJ; ++j) r.roff[j] = j <= c->J ? c->roff[j] : c->R;
   prof_begin(c, KREN);
-  k_renorm_fb<<<dim3(c->KP, c->J), 256, 0, c->stream>>>(r);
-  k_renorm_tw<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
-  k_renorm_flags<<<1, 64, 0, c->stream>>>(r, c->J);
+  k_renorm_stats<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
+  k_renorm_apply<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
+  k_renorm_final<<<1, 256, 0, c->stream>>>(r, c->J, iter);
   prof_end(c, KREN);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
@@ -1254,13 +1357,14 @@ static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool f
 }
 
 // One GEM iteration, all launches asynchronous on c->stream.
-static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega) {
+static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
+                         int iter) {
   const int J = c->J;
   int st = launch_w_old(c);
   if (st) return st;
   prof_begin(c, KFWH);
   k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, (size_t)(c->KP * c->KP + c->KP * 64) * sizeof(double),
-            c->stream>>>(c->FW.p, c->TW.p, c->FWHt.p, J, c->Tp, c->KP);
+            c->stream>>>(c->FW.p, c->TW.p, c->FWHt.p, J, c->Tp, c->KP, c->halt);
   prof_end(c, KFWH);
   st = build_inst_A(c);
   if (st) return st;
@@ -1274,6 +1378,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.A = c->A.p;
   e.psd = psd_dev;
   e.hatW = c->hatW.p;
+  e.halt = c->halt;
   e.part = c->epart.p;
   e.llpart = c->llpart.p;
   e.F = c->F;
@@ -1293,11 +1398,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     default: launch_estep<4>(c, e); break;
   }
   FASST_LAUNCH_CHECK();
-  k_tw_rowsum<<<J * c->KP, 256, 0, c->stream>>>(c->TW.p, c->hsum.p, c->T, c->Tp);
+  k_tw_rowsum<<<J * c->KP, 256, 0, c->stream>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
   FASST_LAUNCH_CHECK();
   prof_begin(c, KLL);
   k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
-                                     1.0 / ((double)c->F * (double)c->T));
+                                     1.0 / ((double)c->F * (double)c->T), c->halt);
   prof_end(c, KLL);
   FASST_LAUNCH_CHECK();
   // mixing update
@@ -1316,6 +1421,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     m.rss = c->rss.p;
     m.rxs = c->rxs.p;
     m.flags = c->flags.p;
+    m.halt = c->halt;
     m.F = c->F;
     m.Fp = c->Fp;
     m.J = J;
@@ -1337,6 +1443,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
       ia.A = c->A.p;
       ia.Pinst = c->Pinst.p;
       ia.flags = c->flags.p;
+      ia.halt = c->halt;
       ia.F = c->F;
       ia.Fp = c->Fp;
       ia.R = c->R;
@@ -1362,6 +1469,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   b.FWHt = c->FWHt.p;
   b.hatW = c->hatW.p;
   b.bnum = c->bnum.p;
+  b.halt = c->halt;
   b.F = c->F;
   b.T = c->T;
   b.Fp = c->Fp;
@@ -1378,6 +1486,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   t.Wfk_new = c->Wfk_new.p;
   t.hatW = c->hatW.p;
   t.tnum = c->tnum.p;
+  t.halt = c->halt;
   t.tden = c->tden.p;
   t.F = c->F;
   t.T = c->T;
@@ -1391,6 +1500,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   TUArgs tu;
   tu.TW = c->TW.p;
   tu.tnum = c->tnum.p;
+  tu.halt = c->halt;
   tu.tden = c->tden.p;
   tu.T = c->T;
   tu.Tp = c->Tp;
@@ -1402,6 +1512,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   u.FB = c->FB.p;
   u.FW = c->FW.p;
   u.bnum = c->bnum.p;
+  u.halt = c->halt;
   u.hsum = c->hsum.p;
   u.Wkf_new = c->Wkf_new.p;
   u.Wfk_new = c->Wfk_new.p;
@@ -1438,7 +1549,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
   prof_end(c, KTWU);
   FASST_LAUNCH_CHECK();
-  return launch_renorm(c);
+  return launch_renorm(c, iter);
 }
 
 }  // namespace fasst
@@ -1482,7 +1593,7 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
     st = FASST_ERR_DEVICE;
   }
   if (!st) st = c->cx.alloc((size_t)4 * c->Tp * c->Fp);
-  if (!st && hipHostMalloc((void **)&c->h_flags, (1 + kMaxJ) * sizeof(int)) != hipSuccess)
+  if (!st && hipHostMalloc((void **)&c->h_flags, kNFlags * sizeof(int)) != hipSuccess)
     st = FASST_ERR_OOM;
   if (!st && hipHostMalloc((void **)&c->h_ll, 64 * sizeof(double)) != hipSuccess) st = FASST_ERR_OOM;
   if (st) {
@@ -1530,6 +1641,8 @@ int fasst_destroy(fasst_ctx *c) {
     c->flags.release();
     c->hsum.release();
     c->rscal.release();
+    c->rpmax.release();
+    c->rpe.release();
     c->rtpart.release();
     for (int i = 0; i < fasst_ctx::kNK; ++i) {
       if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
@@ -1648,10 +1761,11 @@ int fasst_renormalize(fasst_ctx *c, int *restart_mask) {
   int st = need_model(c, 0);
   if (st) return st;
   DeviceGuard g(c->device);
-  FASST_HIP(hipMemsetAsync(c->flags.p, 0, (1 + kMaxJ) * sizeof(int), c->stream));
-  st = launch_renorm(c);
+  FASST_HIP(hipMemsetAsync(c->flags.p, 0, kNFlags * sizeof(int), c->stream));
+  c->halt = nullptr;
+  st = launch_renorm(c, 0);
   if (st) return st;
-  FASST_HIP(hipMemcpyAsync(c->h_flags, c->flags.p, (1 + kMaxJ) * sizeof(int),
+  FASST_HIP(hipMemcpyAsync(c->h_flags, c->flags.p, kNFlags * sizeof(int),
                            hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));
   int mask = 0;
@@ -1681,32 +1795,43 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   FASST_HIP(hipMemsetAsync(c->psd.p, 0, (size_t)n_iter * c->Fp * sizeof(double), c->stream));
   FASST_HIP(hipMemcpy2DAsync(c->psd.p, c->Fp * sizeof(double), psd, c->F * sizeof(double),
                              c->F * sizeof(double), n_iter, hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemsetAsync(c->flags.p, 0, kNFlags * sizeof(int), c->stream));
+  // Without profiling the whole batch is enqueued at once: a flag raised in
+  // iteration i halts every later kernel on the device (HALT_GUARD), and the
+  // host reads the flags once at the end.  Profiling keeps one sync per
+  // iteration so the per-kernel events can be folded.
+  c->halt = c->ablate ? nullptr : c->flags.p + kFlagHalt;
+  const int sync_every = c->prof ? 1 : n_iter;
+  int done = 0;
   for (int it = 0; it < n_iter; ++it) {
-    FASST_HIP(hipMemsetAsync(c->flags.p, 0, (1 + kMaxJ) * sizeof(int), c->stream));
-    st = gem_iteration(c, c->psd.p + (size_t)it * c->Fp, c->ll.p + it, omega);
-    if (st) return st;
-    FASST_HIP(hipMemcpyAsync(c->h_flags, c->flags.p, (1 + kMaxJ) * sizeof(int),
+    st = gem_iteration(c, c->psd.p + (size_t)it * c->Fp, c->ll.p + it, omega, it);
+    if (st) {
+      c->halt = nullptr;
+      return st;
+    }
+    if ((it + 1) % sync_every && it + 1 < n_iter) continue;
+    FASST_HIP(hipMemcpyAsync(c->h_flags, c->flags.p, kNFlags * sizeof(int),
                              hipMemcpyDeviceToHost, c->stream));
     FASST_HIP(hipStreamSynchronize(c->stream));
     prof_collect(c);
-    if (c->h_flags[0] && !c->ablate) {
-      set_error("Singular Matrix");
-      return FASST_ERR_SINGULAR;
-    }
-    int mask = 0;
-    for (int j = 0; j < c->J; ++j)
-      if (c->h_flags[1 + j]) mask |= 1 << j;
-    if (iters_done) *iters_done = it + 1;
-    if (mask) {
-      if (restart_mask) *restart_mask = mask;
-      FASST_HIP(hipMemcpy(logliks, c->ll.p, (size_t)(it + 1) * sizeof(double),
-                          hipMemcpyDeviceToHost));
-      return FASST_TW_RESTART;
-    }
+    done = it + 1;
+    if (c->h_flags[kFlagHalt] || c->h_flags[0]) break;
   }
-  FASST_HIP(hipMemcpyAsync(logliks, c->ll.p, (size_t)n_iter * sizeof(double),
-                           hipMemcpyDeviceToHost, c->stream));
-  FASST_HIP(hipStreamSynchronize(c->stream));
+  c->halt = nullptr;
+  if (c->h_flags[0] && !c->ablate) {
+    set_error("Singular Matrix");
+    return FASST_ERR_SINGULAR;
+  }
+  int mask = 0;
+  for (int j = 0; j < c->J; ++j)
+    if (c->h_flags[1 + j]) mask |= 1 << j;
+  if (mask) done = c->h_flags[kFlagIter] + 1;
+  if (iters_done) *iters_done = done;
+  FASST_HIP(hipMemcpy(logliks, c->ll.p, (size_t)done * sizeof(double), hipMemcpyDeviceToHost));
+  if (mask) {
+    if (restart_mask) *restart_mask = mask;
+    return FASST_TW_RESTART;
+  }
   return FASST_OK;
 }
 
