@@ -230,6 +230,19 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
 
   const int tb = blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
+  // V^T tile of frame tile tt (all sources) on the MFMA pipe
+  auto tile_v = [&](int tt, d4 *v, int lofs) {
+    const int t0 = tt * 16;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      v[j] = d4{0.0, 0.0, 0.0, 0.0};
+      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
+      const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s)
+        v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], sw[4 * s * 16], v[j]);
+    }
+  };
   for (int tt = tb + wv; tt < te; tt += 4) {
     const int t0 = tt * 16;
     // the W tile and mixing coefficients are loop-invariant LDS data: launder
@@ -246,15 +259,7 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
       cim[i] = a.cxi[off];
     }
     d4 v[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      v[j] = d4{0.0, 0.0, 0.0, 0.0};
-      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
-      const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
-#pragma unroll
-      for (int s = 0; s < NKS; ++s)
-        v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], sw[4 * s * 16], v[j]);
-    }
+    tile_v(tt, v, lofs);
     const double *cj = s_cj + lofs + fl;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1161,6 +1166,26 @@ static int launch_grid(size_t n, int block = 256) {
   return (int)(g ? g : 1);
 }
 
+static int estep_occupancy(const fasst_ctx *c);
+static int contract_occupancy(const fasst_ctx *c, bool fb);
+
+// Split count c in [1, max_split] for a launch of unit * c equal blocks on
+// `cap` resident slots: maximises the filled fraction of the last round
+// (unit c / (cap ceil(unit c / cap))), preferring fewer splits within 1.5%.
+static int best_split(long unit, long cap, int max_split) {
+  max_split = std::max(1, max_split);
+  auto eff = [&](int k) {
+    const long blocks = unit * k;
+    const long rounds = (blocks + cap - 1) / cap;
+    return (double)blocks / (double)(rounds * cap);
+  };
+  double best = 0.0;
+  for (int k = 1; k <= max_split; ++k) best = std::max(best, eff(k));
+  for (int k = 1; k <= max_split; ++k)
+    if (eff(k) >= best - 0.015) return k;
+  return 1;
+}
+
 int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv) {
   if (J < 1 || J > kMaxJ) {
     set_error("J=%d outside the HIP path (1..%d sources)", J, kMaxJ);
@@ -1192,21 +1217,36 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
     c->spat_free[j] = c->fb_free[j] = c->tw_free[j] = 1;
   }
   const int Fp = c->Fp, Tp = c->Tp, KP = c->KP;
-  // E-step chunks: enough blocks to cover the chip (>= ~4 blocks per CU)
-  c->tpc_e = std::max(4, (c->ntt + 7) / 8);
-  while (c->tpc_e > 4 && (size_t)c->nft * ((c->ntt + c->tpc_e - 1) / c->tpc_e) < 1024) c->tpc_e /= 2;
+  // Launch shapes sized to whole rounds of resident blocks (a partial last
+  // round idles most of the chip): E-step blocks = f tiles x frame chunks,
+  // FB waves = bin-tile pairs x sources x frame chunks, TW waves = frame-tile
+  // pairs x sources x bin chunks.
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const long cap_e = (long)estep_occupancy(c) * ncu;
+  // (measured at C3: chunks of >= ~40 frame tiles keep the E-step's per-block
+  // prologue/epilogue small; the contractions tolerate finer splits)
+  c->nchunk_e = best_split(c->nft, cap_e, c->ntt / 40);
+  if (const char *v = getenv("FASST_NCHUNK_E")) c->nchunk_e = std::max(1, std::min(atoi(v), c->ntt));
+  c->tpc_e = (c->ntt + c->nchunk_e - 1) / c->nchunk_e;
   c->nchunk_e = (c->ntt + c->tpc_e - 1) / c->tpc_e;
-  // contractions: ~4096+ waves (4 per SIMD) so each SIMD holds several
-  const long fb_waves = (long)((c->nft + kFPW - 1) / kFPW) * J;
-  c->nchunk_b = 1;
-  while (fb_waves * c->nchunk_b < 4096 && c->ntt / (2 * c->nchunk_b) >= 8) c->nchunk_b *= 2;
+  const long cap_b = (long)contract_occupancy(c, true) * ncu;
+  c->nchunk_b = best_split((long)((c->nft + kFPW - 1) / kFPW) * J, cap_b, c->ntt / 16);
+  if (const char *v = getenv("FASST_NCHUNK_B")) c->nchunk_b = std::max(1, std::min(atoi(v), c->ntt));
   c->tpc_b = (c->ntt + c->nchunk_b - 1) / c->nchunk_b;
   c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
-  const long tw_waves = (long)((c->ntt + kTPW - 1) / kTPW) * J;
-  c->nsplit_t = 1;
-  while (tw_waves * c->nsplit_t < 4096 && c->nft / (2 * c->nsplit_t) >= 8) c->nsplit_t *= 2;
+  const long cap_t = (long)contract_occupancy(c, false) * ncu;
+  c->nsplit_t = best_split((long)((c->ntt + kTPW - 1) / kTPW) * J, cap_t, c->nft / 16);
+  if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
   c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
+  if (getenv("FASST_VERBOSE"))
+    fprintf(stderr,
+            "fasst: %d CUs; estep %d chunks (cap %ld blocks); fb %d chunks (cap %ld); tw %d "
+            "splits (cap %ld)\n",
+            ncu, c->nchunk_e, cap_e, c->nchunk_b, cap_b, c->nsplit_t, cap_t);
   const int NP = J * (J + 1) / 2;
   c->nacc = 4 * NP + 8 * J;
   int st;
@@ -1293,52 +1333,91 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   return FASST_OK;
 }
 
-template <int J, int NKS, int RKU, int AB>
-static void launch_estep_t(fasst_ctx *c, const EArgs &e) {
-  constexpr int NP = J * (J + 1) / 2;
-  const size_t base = (size_t)(kMaxR * 4 * 16 + J * 4 * 16 + 4);
-  const size_t sm1 = (base + std::max(J * 4 * NKS * 16, 4 * (4 * NP) * 16)) * sizeof(double);
-  const size_t sm2 = (base + std::max(J * 4 * NKS * 16, 4 * (8 * J) * 16)) * sizeof(double);
-  dim3 grid(c->nft, c->nchunk_e);
-  prof_begin(c, KESTEP);
-  k_estep<J, NKS, RKU, 1, AB><<<grid, 256, sm1, c->stream>>>(e);
-  k_estep<J, NKS, RKU, 2, AB><<<grid, 256, sm2, c->stream>>>(e);
-  prof_end(c, KESTEP);
+// E-step instantiation chosen from the model structure; `f` receives an
+// ETag carrying the template parameters (used for launches and occupancy).
+template <int J_, int NKS_, int RKU_, int AB_>
+struct ETag {
+  static constexpr int J = J_, NKS = NKS_, RKU = RKU_, AB = AB_;
+};
+
+template <class T>
+static size_t estep_smem(int part) {
+  constexpr int NP = T::J * (T::J + 1) / 2;
+  const size_t base = (size_t)(kMaxR * 4 * 16 + T::J * 4 * 16 + 4);
+  const size_t red = part == 1 ? 4 * (4 * NP) * 16 : 4 * (8 * T::J) * 16;
+  return (base + std::max((size_t)(T::J * 4 * T::NKS * 16), red)) * sizeof(double);
 }
 
-template <int J, int NKS>
-static void launch_estep_r(fasst_ctx *c, const EArgs &e) {
+template <int J, int NKS, class F>
+static void estep_dispatch_r(const fasst_ctx *c, F &&f) {
   bool all1 = true, all2 = true;
   for (int j = 0; j < J; ++j) {
     all1 &= c->rank[j] == 1;
     all2 &= c->rank[j] == 2;
   }
   if (all1)
-    launch_estep_t<J, NKS, 1, 0>(c, e);
+    f(ETag<J, NKS, 1, 0>{});
   else if (all2)
-    launch_estep_t<J, NKS, 2, 0>(c, e);
+    f(ETag<J, NKS, 2, 0>{});
   else
-    launch_estep_t<J, NKS, 0, 0>(c, e);
+    f(ETag<J, NKS, 0, 0>{});
 }
 
-template <int J>
-static void launch_estep(fasst_ctx *c, const EArgs &e) {
+template <int J, class F>
+static void estep_dispatch_j(const fasst_ctx *c, F &&f) {
   bool all2 = true;
   for (int j = 0; j < J; ++j) all2 &= c->rank[j] == 2;
   if (J == 4 && c->KP == 32 && all2 && c->ablate) {  // profiling builds only
     switch (c->ablate) {
-      case 1: launch_estep_t<4, 8, 2, 1>(c, e); return;
-      case 2: launch_estep_t<4, 8, 2, 2>(c, e); return;
-      case 4: launch_estep_t<4, 8, 2, 4>(c, e); return;
-      case 7: launch_estep_t<4, 8, 2, 7>(c, e); return;
+      case 1: f(ETag<4, 8, 2, 1>{}); return;
+      case 2: f(ETag<4, 8, 2, 2>{}); return;
+      case 4: f(ETag<4, 8, 2, 4>{}); return;
+      case 7: f(ETag<4, 8, 2, 7>{}); return;
       default: break;
     }
   }
   switch (c->KP) {
-    case 16: launch_estep_r<J, 4>(c, e); break;
-    case 32: launch_estep_r<J, 8>(c, e); break;
-    default: launch_estep_r<J, 16>(c, e); break;
+    case 16: estep_dispatch_r<J, 4>(c, f); break;
+    case 32: estep_dispatch_r<J, 8>(c, f); break;
+    default: estep_dispatch_r<J, 16>(c, f); break;
   }
+}
+
+template <class F>
+static void estep_dispatch(const fasst_ctx *c, F &&f) {
+  switch (c->J) {
+    case 1: estep_dispatch_j<1>(c, f); break;
+    case 2: estep_dispatch_j<2>(c, f); break;
+    case 3: estep_dispatch_j<3>(c, f); break;
+    default: estep_dispatch_j<4>(c, f); break;
+  }
+}
+
+static void launch_estep(fasst_ctx *c, const EArgs &e) {
+  estep_dispatch(c, [&](auto tag) {
+    using T = decltype(tag);
+    dim3 grid(c->nft, c->nchunk_e);
+    prof_begin(c, KESTEP);
+    k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
+    k_estep<T::J, T::NKS, T::RKU, 2, T::AB><<<grid, 256, estep_smem<T>(2), c->stream>>>(e);
+    prof_end(c, KESTEP);
+  });
+}
+
+// resident blocks per CU of the E-step pair (the lower of the two parts)
+static int estep_occupancy(const fasst_ctx *c) {
+  int occ = 1;
+  estep_dispatch(c, [&](auto tag) {
+    using T = decltype(tag);
+    int n1 = 0, n2 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &n1, k_estep<T::J, T::NKS, T::RKU, 1, T::AB>, 256, estep_smem<T>(1)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &n2, k_estep<T::J, T::NKS, T::RKU, 2, T::AB>, 256, estep_smem<T>(2)) != hipSuccess)
+      n1 = n2 = 1;
+    occ = std::max(1, std::min(n1, n2));
+  });
+  return occ;
 }
 
 template <int NKC>
@@ -1354,6 +1433,26 @@ static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool f
                                c->stream>>>(t);
     prof_end(c, KTWC);
   }
+}
+
+static int contract_occupancy(const fasst_ctx *c, bool fb) {
+  int n = 1;
+  hipError_t e = hipSuccess;
+  switch (c->KP / 16) {
+    case 1:
+      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<1, kFPW>, 64, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<1, kTPW>, 64, 0);
+      break;
+    case 2:
+      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<2, kFPW>, 64, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<2, kTPW>, 64, 0);
+      break;
+    default:
+      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<4, kFPW>, 64, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<4, kTPW>, 64, 0);
+      break;
+  }
+  return e == hipSuccess ? std::max(1, n) : 1;
 }
 
 // One GEM iteration, all launches asynchronous on c->stream.
@@ -1391,12 +1490,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.tpc = c->tpc_e;
   e.nft = c->nft;
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
-  switch (J) {
-    case 1: launch_estep<1>(c, e); break;
-    case 2: launch_estep<2>(c, e); break;
-    case 3: launch_estep<3>(c, e); break;
-    default: launch_estep<4>(c, e); break;
-  }
+  launch_estep(c, e);
   FASST_LAUNCH_CHECK();
   k_tw_rowsum<<<J * c->KP, 256, 0, c->stream>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
   FASST_LAUNCH_CHECK();
