@@ -16,8 +16,14 @@ constexpr int kMaxR = 8;        // total spatial rank
 constexpr int kMaxKP = 64;      // padded NMF components
 constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge
 constexpr int kFlagHalt = 1 + kMaxJ, kFlagIter = 2 + kMaxJ, kNFlags = 3 + kMaxJ;
-constexpr int kFPW = 2;         // bin tiles per wave, FB contraction
-constexpr int kTPW = 2;         // frame tiles per wave, TW contraction
+#ifndef FASST_FPW
+#define FASST_FPW 2
+#endif
+#ifndef FASST_TPW
+#define FASST_TPW 2
+#endif
+constexpr int kFPW = FASST_FPW;  // bin tiles per wave, FB contraction
+constexpr int kTPW = FASST_TPW;  // frame tiles per wave, TW contraction
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 

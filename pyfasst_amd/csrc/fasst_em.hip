@@ -728,9 +728,14 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       double h[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) h[i] = hwj[(size_t)(t0 + tq + 4 * i) * a.Fp + f];
-      d4 v = d4{0.0, 0.0, 0.0, 0.0};
+      // two independent MFMA chains (even / odd k-steps) for latency hiding
+      d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) v = mfma4(tw[s], wk[p][s], v);
+      for (int s = 0; s < NKS; s += 2) {
+        v = mfma4(tw[s], wk[p][s], v);
+        v2 = mfma4(tw[s + 1], wk[p][s + 1], v2);
+      }
+      v += v2;
       double r1[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -865,12 +870,16 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       double h[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) h[i] = hwj[(size_t)t * a.Fp + f0 + tq + 4 * i];
-      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
+      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) {
+      for (int s = 0; s < NKS; s += 2) {
         vo = mfma4(ao[s], bt[p][s], vo);
         vn = mfma4(an[s], bt[p][s], vn);
+        vo2 = mfma4(ao[s + 1], bt[p][s + 1], vo2);
+        vn2 = mfma4(an[s + 1], bt[p][s + 1], vn2);
       }
+      vo += vo2;
+      vn += vn2;
       const bool tok = t < a.T;
       double r3[4], r4[4];
 #pragma unroll
@@ -1233,12 +1242,16 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   c->tpc_e = (c->ntt + c->nchunk_e - 1) / c->nchunk_e;
   c->nchunk_e = (c->ntt + c->tpc_e - 1) / c->tpc_e;
   const long cap_b = (long)contract_occupancy(c, true) * ncu;
-  c->nchunk_b = best_split((long)((c->nft + kFPW - 1) / kFPW) * J, cap_b, c->ntt / 16);
+  c->nchunk_b = best_split((long)((c->nft + kFPW - 1) / kFPW) * J, cap_b, c->ntt / 32);
   if (const char *v = getenv("FASST_NCHUNK_B")) c->nchunk_b = std::max(1, std::min(atoi(v), c->ntt));
   c->tpc_b = (c->ntt + c->nchunk_b - 1) / c->nchunk_b;
   c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
   const long cap_t = (long)contract_occupancy(c, false) * ncu;
-  c->nsplit_t = best_split((long)((c->ntt + kTPW - 1) / kTPW) * J, cap_t, c->nft / 16);
+  // (the bin split also multiplies k_tw_update's reduction: a fixed, small
+  // split measured best at C3)
+  c->nsplit_t = std::max(1, std::min(4, c->nft / 32));
+  if ((long)((c->ntt + kTPW - 1) / kTPW) * J * c->nsplit_t < cap_t)
+    c->nsplit_t = best_split((long)((c->ntt + kTPW - 1) / kTPW) * J, cap_t, c->nft / 16);
   if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
   c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
