@@ -83,6 +83,64 @@ PATCHES = [
     ("SeparateLeadStereo/SeparateLeadStereoTF.py",
      r"from \.tracking\._tracking import viterbiTracking as viterbiTrackingArray",
      "from .tracking.tracking import viterbiTrackingArray"),
+    # tftransforms/minqt.py (CQT / MinQT): numpy-2 aliases,
+    # float sizes / indices, scipy >= 1.13 window location
+    ("tftransforms/minqt.py", r"np\.complex\b", "complex"),
+    ("tools/utils.py", r"spsig\.blackmanharris\(M\)", "spsig.windows.blackmanharris(M)"),
+    ("tftransforms/minqt.py", r"np\.zeros\(\[bins \* winNr, FFTLen\],", "np.zeros([int(bins * winNr), int(FFTLen)],"),
+    ("tftransforms/minqt.py", r"tempKernel = np\.zeros\(FFTLen, dtype=complex\)", "tempKernel = np.zeros(int(FFTLen), dtype=complex)"),
+    ("tftransforms/minqt.py", r"winFct = winFunc\(Nk\)", "winFct = winFunc(int(Nk))"),
+    ("tftransforms/minqt.py", r"tempKernel\[shift:\(Nk\+shift\)\] = tempKernelBin", "tempKernel[int(shift):int(Nk+shift)] = tempKernelBin"),
+    ("tftransforms/minqt.py", r"self\.linBins = linFTLen/2 - Kmax \+ 1", "self.linBins = linFTLen//2 - Kmax + 1"),
+    ("tftransforms/minqt.py", r"self\.cellCQT\[i\] = np\.zeros\(\[self\.cqtkernel\.bins \*\n\s+self\.cqtkernel\.winNr,\n\s+nframes\],",
+     "self.cellCQT[i] = np.zeros([int(self.cqtkernel.bins * self.cqtkernel.winNr), int(nframes)],"),
+    ("tftransforms/minqt.py", r"self\._spCQT = np\.zeros\(\[self\.cqtkernel\.bins\n\s+\* self\.octaveNr,\n\s+nframes \* atomNr\],",
+     "self._spCQT = np.zeros([int(self.cqtkernel.bins * self.octaveNr), int(nframes * atomNr)],"),
+    ("tftransforms/minqt.py", r"CQTframe = np\.zeros\(\[self\.cqtkernel\.bins \* atomNr, nframes\],",
+     "CQTframe = np.zeros([int(self.cqtkernel.bins * atomNr), int(nframes)],"),
+    ("tftransforms/minqt.py", r"XX = np\.zeros\(\[self\.cqtkernel\.FFTLen, nframes\],", "XX = np.zeros([int(self.cqtkernel.FFTLen), int(nframes)],"),
+    ("tftransforms/minqt.py", r"for n in np\.arange\(nframes\):\n(\s+)if self\.verbose>2:", r"for n in np.arange(int(nframes)):\n\1if self.verbose>2:"),
+    ("tftransforms/minqt.py", r"framestart = n \* self\.cqtkernel\.fftHOP\n", "framestart = int(n * self.cqtkernel.fftHOP)\n"),
+    ("tftransforms/minqt.py", r"framestop = framestart \+ self\.cqtkernel\.FFTLen\n", "framestop = int(framestart + self.cqtkernel.FFTLen)\n"),
+    ("tftransforms/minqt.py", r"XX\[:,n\]= np\.fft\.fft\(x\[framestart:framestop\],\n\s+n=cqtkernel\.FFTLen\)",
+     "XX[:,n]= np.fft.fft(x[framestart:framestop], n=int(cqtkernel.FFTLen))"),
+    ("tftransforms/minqt.py", r"for nshift in np\.arange\(2\*\*i\):", "for nshift in np.arange(int(2**i)):"),
+    ("tftransforms/minqt.py", r"X,F,N = stft\(data=x\[self\.offsetSTFT:\],", "X,F,N = stft(data=x[int(self.offsetSTFT):],"),
+    ("tftransforms/minqt.py", r"self\.cellCQT\['linear'\] = X\[self\.cqtkernel\.Kmax:,\n\s+:self\.nframes\[0\] \* self\.cqtkernel\.winNr\]",
+     "self.cellCQT['linear'] = X[self.cqtkernel.Kmax:, :int(self.nframes[0] * self.cqtkernel.winNr)]"),
+    ("tftransforms/minqt.py", r"self\._spCQT = np\.vstack\(\[\n\s+self\._spCQT,\n\s+np\.zeros\(\[self\.cqtkernel\.linBins,\n\s+self\._spCQT\.shape\[1\]\],\n\s+dtype=complex\)\]\)",
+     "self._spCQT = np.vstack([self._spCQT, np.zeros([int(self.cqtkernel.linBins), self._spCQT.shape[1]], dtype=complex)])"),
+    ("tftransforms/minqt.py", r"self\._spCQT\[\(self\.cqtkernel\.bins \* self\.octaveNr\):,", "self._spCQT[int(self.cqtkernel.bins * self.octaveNr):,"),
+    ("tftransforms/minqt.py", r"self\.maxBlock = \(\n\s+cqtkernel\.FFTLen \*\n\s+\(2\*\*\(self\.octaveNr-1\)\)\)", "self.maxBlock = int(cqtkernel.FFTLen * (2**(self.octaveNr-1)))"),
+    ("tftransforms/minqt.py", r"int\(nshift\):\(nframes\*nshifts\):nshifts\] = \(", "int(nshift):int(nframes*nshifts):nshifts] = ("),
+    ("tftransforms/minqt.py", r"y = np\.zeros\(np\.ceil\(self\.datalen_init /\n\s+\(2\.\*\*\(self\.octaveNr-1\)\)\)\)",
+     "y = np.zeros(int(np.ceil(self.datalen_init / (2.**(self.octaveNr-1)))))"),
+    ("tftransforms/minqt.py", r"y = np\.concatenate\(\[y, np\.zeros\(ylen-y\.size\)\]\)", "y = np.concatenate([y, np.zeros(int(ylen-y.size))])"),
+    ("tftransforms/minqt.py", r"yoct = np\.zeros\(self\.cqtkernel\.FFTLen\)", "yoct = np.zeros(int(self.cqtkernel.FFTLen))"),
+    ("tftransforms/minqt.py", r"frastop = frastart \+ self\.cqtkernel\.FFTLen\n", "frastop = int(frastart + self.cqtkernel.FFTLen)\n"),
+    ("tftransforms/minqt.py", r"frastart = n \* self\.cqtkernel\.fftHOP\n", "frastart = int(n * self.cqtkernel.fftHOP)\n"),
+    ("tftransforms/minqt.py", r"np\.fft\.ifft\(Y\[:,n\], n=self\.cqtkernel\.FFTLen\)", "np.fft.ifft(Y[:,n], n=int(self.cqtkernel.FFTLen))"),
+    ("tftransforms/minqt.py", r"self\._spCQT\[int\(self\.cqtkernel\.bins\*\(self\.octaveNr-noct-1\)\):\n(\s+)int\(self\.cqtkernel\.bins\*\(self\.octaveNr-noct\)\),\n(\s+):-1\] = \(",
+     r"self._spCQT[int(self.cqtkernel.bins*(self.octaveNr-noct-1)):int(self.cqtkernel.bins*(self.octaveNr-noct)), :-1] = ("),
+    ("tftransforms/minqt.py", r"newy = np\.zeros\(y\.size\*2\)", "newy = np.zeros(int(y.size*2))"),
+    ("tftransforms/minqt.py", r"y = y\[self\.prefixZeros:\]", "y = y[int(self.prefixZeros):]"),
+    ("tftransforms/minqt.py", r"y = y\[:self\.datalen_init\]", "y = y[:int(self.datalen_init)]"),
+    ("tftransforms/minqt.py", r"np\.hstack\(\[np\.zeros\(\[self\.cqtkernel\.bins, dropped\]\),", "np.hstack([np.zeros([int(self.cqtkernel.bins), int(dropped)]),"),
+    ("tftransforms/minqt.py", r"np\.zeros\(\[self\.cqtkernel\.bins,\n\s+np\.ceil\(X\.shape\[1\]/\n\s+self\.cqtkernel\.winNr\)\*\n\s+self\.cqtkernel\.winNr -\n\s+X\.shape\[1\]\]\)",
+     "np.zeros([int(self.cqtkernel.bins), int(np.ceil(X.shape[1]/self.cqtkernel.winNr)*self.cqtkernel.winNr - X.shape[1])])"),
+    ("tftransforms/minqt.py", r"np\.ascontiguousarray\(self\.cellCQT\[noct\]\[:,:self\.nframes\[noct\]\]\)", "np.ascontiguousarray(self.cellCQT[noct][:,:int(self.nframes[noct])])"),
+    ("tftransforms/minqt.py", r"np\.hstack\(\[np\.zeros\(\[self\.cqtkernel\.linBins, dropped\]\),", "np.hstack([np.zeros([int(self.cqtkernel.linBins), int(dropped)]),"),
+    ("tftransforms/minqt.py", r"self\.cellCQT\['linear'\]\[:,:\(self\.nframes\[0\]\*\n\s+self\.cqtkernel\.winNr\)\]",
+     "self.cellCQT['linear'][:,:int(self.nframes[0]*self.cqtkernel.winNr)]"),
+    ("tftransforms/minqt.py", r"Y = np\.zeros\(\[self\.cqtkernel\.linFTLen / 2 \+ 1,", "Y = np.zeros([self.cqtkernel.linFTLen // 2 + 1,"),
+    ("tftransforms/minqt.py", r"y = y\[\(self\.prefixZeros-self\.offsetSTFT\):\]", "y = y[int(self.prefixZeros-self.offsetSTFT):]"),
+    ("tftransforms/minqt.py", r"X\.shape\[1\]/self\.cqtkernel\.winNr, order='F'\)", "int(X.shape[1]//self.cqtkernel.winNr), order='F')"),
+    ("tftransforms/minqt.py", r"np\.ceil\(X\.shape\[1\]/\n\s+self\.cqtkernel\.winNr\)\],", "int(np.ceil(X.shape[1]/self.cqtkernel.winNr))],"),
+    ("tftransforms/minqt.py", r"CQTframe\[nb\*atomNr\+a\]", "CQTframe[int(nb*atomNr+a)]"),
+    ("tftransforms/minqt.py", r"self\.cellCQT\[noct\]\[nb\*atomNr\+a\]", "self.cellCQT[noct][int(nb*atomNr+a)]"),
+    ("tftransforms/minqt.py", r"self\.cellCQT\[noct\] = np\.zeros\(\[self\.cqtkernel\.bins \*\n\s+self\.cqtkernel\.winNr,",
+     "self.cellCQT[noct] = np.zeros([int(self.cqtkernel.bins * self.cqtkernel.winNr),"),
+    ("tftransforms/minqt.py", r"X\[nbin\]\.reshape\(\n\s+self\.cqtkernel\.winNr,", "X[nbin].reshape(int(self.cqtkernel.winNr),"),
 ]
 
 

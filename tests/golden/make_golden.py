@@ -36,6 +36,11 @@ CASES = {
                     conv=True, n=6000, fs=8000, kw=dict(iter_num=5, wlen=256, hopsize=64)),
     "em_conv_j4": dict(cls="MultiChanNMFConv", nbComps=4, nbNMFComps=16, spatial_rank=2,
                        conv=True, n=6000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64)),
+    # FASST on the MinQT front end (transf='mqt', audioModel.py:156,206-214,1187-1203)
+    "em_mqt": dict(cls="MultiChanNMFConv", nbComps=2, nbNMFComps=6, spatial_rank=2,
+                   conv=True, n=4000, fs=8000,
+                   kw=dict(iter_num=3, wlen=256, hopsize=64, transf='mqt', tffmin=200,
+                           tfbpo=12)),
     "em_conv_j1": dict(cls="MultiChanNMFConv", nbComps=1, nbNMFComps=3, spatial_rank=[2],
                        conv=True, n=3000, fs=8000, kw=dict(iter_num=3, wlen=128, hopsize=32)),
 }
@@ -262,6 +267,44 @@ def run_lead():
     print("lead", {k: np.shape(v) for k, v in out.items() if k.startswith(('mask', 'voc'))})
 
 
+CQT_CASES = (
+    # name, class, kwargs (perfRast=1 as FASST builds them, audioModel.py:206-214)
+    ("mqt12", "MinQTransfo", dict(fmin=25, fmax=3000, bins=12, fs=8000, linFTLen=512,
+                                  atomHopFactor=0.25)),
+    ("mqt48", "MinQTransfo", dict(fmin=100, fmax=18000, bins=48, fs=8000, linFTLen=256,
+                                  atomHopFactor=0.25)),
+    ("mqt_h", "MinQTransfo", dict(fmin=300, fmax=18000, bins=24, fs=16000, linFTLen=512,
+                                  atomHopFactor=0.0625)),
+    ("cqt12", "CQTransfo", dict(fmin=100, fmax=3000, bins=12, fs=8000, atomHopFactor=0.25)),
+    ("cqt_h", "CQTransfo", dict(fmin=150, fmax=3500, bins=24, fs=8000, atomHopFactor=0.5)),
+)
+
+
+def run_cqt():
+    """CQTransfo / MinQTransfo (tftransforms/minqt.py) forward + inverse with
+    perfRast=1 on a seeded signal: spCQT (transfo), frame counts, frequency
+    stamps and invertTransform() of the same spCQT."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    from pyfasst.tftransforms import minqt
+    rs = np.random.RandomState(31)
+    x = rs.randn(3000) * (1 + np.sin(np.arange(3000) / 300.))
+    out = {'x': x}
+    for name, cls, kw in CQT_CASES:
+        t = getattr(minqt, cls)(perfRast=1, **kw)
+        t.computeTransform(x)
+        X = np.array(t.transfo)
+        out['X_' + name] = X
+        out['nframes_' + name] = np.array(t.nframes)
+        out['freqs_' + name] = np.array(t.freq_stamps)
+        t.transfo = X
+        out['y_' + name] = np.array(t.invertTransform())
+    np.savez_compressed(os.path.join(HERE, "cqt.npz"), **out)
+    print("cqt", {k: np.shape(v) for k, v in out.items() if k.startswith('X_')})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -285,12 +328,12 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--case":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
-         "lead": run_lead}.get(
+         "lead": run_lead, "cqt": run_cqt}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
-    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead"] + list(CASES))
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

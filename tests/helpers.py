@@ -14,7 +14,21 @@ CASES = {
     "em_conv": (3, 8, 2, True, dict(iter_num=5, wlen=256, hopsize=64)),
     "em_conv_j4": (4, 16, 2, True, dict(iter_num=4, wlen=256, hopsize=64)),
     "em_conv_j1": (1, 3, [2], True, dict(iter_num=3, wlen=128, hopsize=32)),
+    "em_mqt": (2, 6, 2, True, dict(iter_num=3, wlen=256, hopsize=64, transf='mqt', tffmin=200,
+                                   tfbpo=12)),
 }
+
+# tests/golden/cqt.npz cases; mirrors CQT_CASES of tests/golden/make_golden.py
+CQT_CASES = (
+    ("mqt12", "mqt", dict(fmin=25, fmax=3000, bins=12, fs=8000, linFTLen=512,
+                          atomHopFactor=0.25)),
+    ("mqt48", "mqt", dict(fmin=100, fmax=18000, bins=48, fs=8000, linFTLen=256,
+                          atomHopFactor=0.25)),
+    ("mqt_h", "mqt", dict(fmin=300, fmax=18000, bins=24, fs=16000, linFTLen=512,
+                          atomHopFactor=0.0625)),
+    ("cqt12", "cqt", dict(fmin=100, fmax=3000, bins=12, fs=8000, atomHopFactor=0.25)),
+    ("cqt_h", "cqt", dict(fmin=150, fmax=3500, bins=24, fs=8000, atomHopFactor=0.5)),
+)
 
 
 def load(name):
@@ -34,8 +48,15 @@ def oracle_model_from_golden(g, case):
     J, K, rank, conv, kw = CASES[case]
     x, _ = R.read_scaled(g['wav'])
     wlen, hop = kw['wlen'], kw['hopsize']
-    w = np.hanning(wlen)
-    X = [R.stft(x[:, c], w, hop, wlen) for c in range(2)]
+    if kw.get('transf', 'stft') == 'stft':
+        w = np.hanning(wlen)
+        X = [R.stft(x[:, c], w, hop, wlen) for c in range(2)]
+    else:   # FASST's MinQT / CQT front end (audioModel.py:206-214)
+        import cqt_ref
+        t = cqt_ref.RefCQT(kw['transf'].replace('minqt', 'mqt'), fmin=kw.get('tffmin', 25),
+                           fmax=kw.get('tffmax', 18000), bins=kw.get('tfbpo', 48),
+                           fs=int(g['fs']), linFTLen=wlen, atomHopFactor=hop / float(wlen))
+        X = [t.forward(x[:, c]) for c in range(2)]
     okw = {k: v for k, v in kw.items() if k in ('iter_num', 'sim_ann_opt', 'nmfUpdateCoeff')}
     m = R.RefFASST(**okw)
     m.set_transform(X)

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import fasst_ref as R
-from helpers import CASES, load, oracle_model_from_golden, rel
+from helpers import CASES, CQT_CASES, load, oracle_model_from_golden, rel
 
 
 def test_inv_herm_known_answer():
@@ -32,6 +32,19 @@ def test_stft_istft_golden():
         np.testing.assert_array_equal(X, g['X_%d_%d' % (nfft, hop)])
         y = R.istft(X, np.hanning(nfft), np.hanning(nfft), hop, nfft)[:g['x'].size]
         np.testing.assert_array_equal(y, g['y_%d_%d' % (nfft, hop)])
+
+
+@pytest.mark.parametrize("name,kind,kw", CQT_CASES, ids=[c[0] for c in CQT_CASES])
+def test_cqt_golden(name, kind, kw):
+    """CQTransfo / MinQTransfo forward + inverse (tftransforms/minqt.py), perfRast=1."""
+    import cqt_ref
+    g = load("cqt")
+    t = cqt_ref.RefCQT(kind, **kw)
+    X = t.forward(g['x'])
+    np.testing.assert_array_equal(X, g['X_' + name])
+    np.testing.assert_array_equal(np.array(t.nframes), g['nframes_' + name])
+    np.testing.assert_array_equal(t.freq_stamps(), g['freqs_' + name])
+    np.testing.assert_array_equal(t.inverse(X), g['y_' + name])
 
 
 def test_nmf_golden():
