@@ -1,5 +1,5 @@
 """ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h,
-include/fasst_simm.h and include/fasst_nmf.h).
+include/fasst_simm.h, include/fasst_nmf.h and include/fasst_cqt.h).
 
 The product path has no CPU fallback: if the HIP library is missing this
 module raises at import time, and every compute call raises if the device
@@ -81,6 +81,13 @@ SIGNATURES = {
     "nmf_set_params": (ctypes.c_int, [_vp, _dp, _dp]),
     "nmf_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "nmf_get_params": (ctypes.c_int, [_vp, _dp, _dp]),
+    # include/fasst_cqt.h
+    "cqt_create": (ctypes.c_int, [ctypes.c_int] * 8 + [_dp, _dp, _dp, _dp] +
+                   [ctypes.c_int] * 3 + [_dp, ctypes.POINTER(_vp)]),
+    "cqt_destroy": (ctypes.c_int, [_vp]),
+    "cqt_shape": (ctypes.c_int, [_vp, ctypes.c_long, _ip, _ip, _ip]),
+    "cqt_forward": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
+    "cqt_inverse": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -22,6 +22,7 @@ import numpy as np
 
 from . import audioObject as ao
 from .engine import Engine
+from .tftransforms import minqt as minqt_mod
 from .tftransforms import stft as stft_mod
 
 eps = 1e-10              # audioModel.py:61
@@ -31,7 +32,7 @@ soundCelerity = 340.
 
 class FASST(object):
     """FASST base class (audioModel.py:66-248)."""
-    implemented_transf = ['stft']
+    implemented_transf = ['stft', 'mqt', 'minqt', 'cqt']
     implemented_annealing = ['ann', 'no_ann']
 
     def __init__(self, audio, transf='stft', wlen=2048, hopsize=512, iter_num=50,
@@ -59,9 +60,14 @@ class FASST(object):
         self.sig_repr_params['hopfactor'] = 1. * hopsize / self.sig_repr_params['wlen']
         if self.sig_repr_params['transf'] not in self.implemented_transf:
             raise NotImplementedError(self.sig_repr_params['transf'] + " not yet implemented.")
-        self.tft = stft_mod.STFT(linFTLen=self.sig_repr_params['fsize'],
-                                 atomHopFactor=self.sig_repr_params['hopfactor'],
-                                 fs=self._samplerate_or_default(), device=device)
+        # the transform object (audioModel.py:205-214): STFT, or the rasterised
+        # MinQT / CQT (perfRast=1) on the GPU
+        tf_cls = {'stft': stft_mod.STFT, 'mqt': minqt_mod.MinQTransfo,
+                  'minqt': minqt_mod.MinQTransfo, 'cqt': minqt_mod.CQTransfo}[
+                      self.sig_repr_params['transf']]
+        self.tft = tf_cls(fmin=tffmin, fmax=tffmax, bins=tfbpo, fs=self._samplerate_or_default(),
+                          perfRast=1, linFTLen=self.sig_repr_params['fsize'],
+                          atomHopFactor=self.sig_repr_params['hopfactor'], device=device)
         self.demixParams = {
             'tffmin': tffmin, 'tffmax': tffmax, 'tfbpo': tfbpo,
             'tfrepresentation': transf.lower(), 'wlen': self.sig_repr_params['wlen'],
@@ -124,6 +130,20 @@ class FASST(object):
                 raise NotImplementedError("the HIP path handles stereo signals (got %d)" % nc)
             data = np.asarray(aud.data, dtype=np.float64)
             L = data.shape[0]
+            if self.sig_repr_params['transf'] != 'stft':
+                # MinQT / CQT of each channel on the GPU (audioModel.py:266-280), then
+                # the channel transforms become the engine's resident observation
+                X = []
+                for n in range(nc):
+                    self.tft.computeTransform(data[:, n])
+                    X.append(self.tft.transfo)
+                F, T = X[0].shape
+                self._engine = Engine(F, T, self.device)
+                self._engine.set_stft(np.array(X))
+                self.nbFreqsSigRepr, self.nbFramesSigRepr = F, T
+                self._Cx = None
+                self._finish_noise_limits()
+                return
             hop = self.tft.fthop
             T = int(np.ceil(L / np.double(hop))) + 2
             F = self.tft.freqbins
@@ -132,6 +152,10 @@ class FASST(object):
             self.tft.datalen_init = L
             self.nbFreqsSigRepr, self.nbFramesSigRepr = F, T
             self._Cx = None
+        self._finish_noise_limits()
+
+    def _finish_noise_limits(self):
+        """Annealing limits from the mean diagonal PSD (audioModel.py:304-325)."""
         lim = self.noise['ann_PSD_lim']
         if lim[0] is None or lim[1] is None:
             mix_psd = self._engine.mix_psd()

@@ -9,6 +9,7 @@
 //   k_wiener<J>     Sigma_n = R_n V_n, Sigma_x^-1, WG_n = Sigma_n Sigma_x^-1,
 //                   S_n = WG_n X  (audioModel.py:1327-1467, :1205-1214)
 #include "fasst_ctx.h"
+#include "fasst_fft.h"
 
 #include <cmath>
 
@@ -17,27 +18,6 @@ namespace fasst {
 __device__ __forceinline__ d4 mfma4b(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
-
-// In-LDS complex FFT of size N (power of two), data already in bit-reversed
-// order.  tw[k] = exp(sign * 2 pi i k / N), k < N/2.
-__device__ void lds_fft(double2 *x, const double2 *__restrict__ tw, int N, int logN) {
-  for (int s = 0; s < logN; ++s) {
-    const int m = 1 << s;
-    const int stride = N >> (s + 1);
-    for (int b = threadIdx.x; b < (N >> 1); b += blockDim.x) {
-      const int grp = b >> s, pos = b & (m - 1);
-      const int i0 = grp * 2 * m + pos, i1 = i0 + m;
-      const double2 w = tw[pos * stride];
-      const double2 u = x[i0], v = x[i1];
-      const double2 t = make_double2(w.x * v.x - w.y * v.y, w.x * v.y + w.y * v.x);
-      x[i0] = make_double2(u.x + t.x, u.y + t.y);
-      x[i1] = make_double2(u.x - t.x, u.y - t.y);
-    }
-    __syncthreads();
-  }
-}
-
-__device__ __forceinline__ int bitrev(int i, int logN) { return (int)(__brev((unsigned)i) >> (32 - logN)); }
 
 // One block per (frame, channel).  x: [nch][L] channel-major; output either
 // [frame][bin] into a pitched device image (ld = row pitch in bins) or, for
@@ -357,23 +337,6 @@ __global__ void k_inv_herm(int n, const double *__restrict__ d, const double2 *_
     id[n + i] = d0 / det;
     det_out[i] = det;
   }
-}
-
-// twiddles exp(sign 2 pi i k / N), k < N/2, computed on the host in long double
-static std::vector<double2> twiddles(int N, int sign) {
-  std::vector<double2> tw(N / 2);
-  const long double pi = 3.141592653589793238462643383279502884L;
-  for (int k = 0; k < N / 2; ++k) {
-    const long double ang = 2.0L * pi * (long double)k / (long double)N;
-    tw[k] = make_double2((double)cosl(ang), (double)(sign * sinl(ang)));
-  }
-  return tw;
-}
-
-static int ilog2(int n) {
-  int l = 0;
-  while ((1 << l) < n) ++l;
-  return (1 << l) == n ? l : -1;
 }
 
 static int check_fft(int nfft, int wlen, int hop) {
