@@ -57,6 +57,10 @@ int cqt_forward(cqt_ctx *ctx, const double *x, long L, double *sp);
  * -> y [L]                                                                */
 int cqt_inverse(cqt_ctx *ctx, const double *sp, long L, double *y);
 
+/* Device time (HIP events on the context's stream) of the last cqt_forward /
+ * cqt_inverse, excluding the host<->device copies of x, sp and y.         */
+int cqt_device_ms(cqt_ctx *ctx, double *forward_ms, double *inverse_ms);
+
 #ifdef __cplusplus
 }
 #endif

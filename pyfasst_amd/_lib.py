@@ -88,6 +88,7 @@ SIGNATURES = {
     "cqt_shape": (ctypes.c_int, [_vp, ctypes.c_long, _ip, _ip, _ip]),
     "cqt_forward": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
     "cqt_inverse": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
+    "cqt_device_ms": (ctypes.c_int, [_vp, _dp, _dp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

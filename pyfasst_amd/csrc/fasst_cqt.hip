@@ -363,6 +363,10 @@ struct cqt_ctx {
   long cap_L = -1;
   DBuf<double> xp, sa, sb, y1, frames, yb, yc;
   DBuf<double2> XX, sp, sph;
+  // device time of the last forward / inverse (HIP events on the ctx stream,
+  // after the host->device copy and before the device->host copy)
+  hipEvent_t ev[4] = {};
+  float ms_fwd = 0.f, ms_inv = 0.f;
 };
 
 namespace {
@@ -582,6 +586,8 @@ int cqt_create(int device, int bins, int octave_nr, int win_nr, int fft_len, int
     return fail(st);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(FASST_ERR_DEVICE);
+  for (auto &e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(FASST_ERR_DEVICE);
   auto twf = twiddles(fft_len, -1), twi = twiddles(fft_len, +1);
   if (hipMemcpy(c->K.p, hK.data(), hK.size() * sizeof(double2), hipMemcpyHostToDevice) ||
       hipMemcpy(c->S.p, hS.data(), hS.size() * sizeof(double2), hipMemcpyHostToDevice) ||
@@ -619,6 +625,8 @@ int cqt_destroy(cqt_ctx *c) {
       (void)hipStreamSynchronize(c->stream);
       (void)hipStreamDestroy(c->stream);
     }
+    for (auto &e : c->ev)
+      if (e) (void)hipEventDestroy(e);
     delete c;
   }
   return FASST_OK;
@@ -646,6 +654,7 @@ int cqt_forward(cqt_ctx *c, const double *x, long L, double *sp) {
   hipStream_t s = c->stream;
   FASST_HIP(hipMemsetAsync(c->xp.p, 0, g.Lp * sizeof(double), s));
   FASST_HIP(hipMemcpyAsync(c->xp.p + g.maxBlock, x, L * sizeof(double), hipMemcpyHostToDevice, s));
+  FASST_HIP(hipEventRecord(c->ev[0], s));
   FASST_HIP(hipMemsetAsync(c->sp.p, 0, (size_t)g.W * g.F * sizeof(double2), s));
   if (c->lin_N && g.W > g.drop0) {   // computeLinearPart on the padded signal
     const long off = (long)c->first_center - c->lin_N / 2;
@@ -693,9 +702,11 @@ int cqt_forward(cqt_ctx *c, const double *x, long L, double *sp) {
   k_cqt_transpose<<<dim3((g.F + 15) / 16, (g.W + 15) / 16), 256, 0, s>>>(c->sp.p, c->sph.p, g.W,
                                                                           g.F);
   FASST_LAUNCH_CHECK();
+  FASST_HIP(hipEventRecord(c->ev[1], s));
   FASST_HIP(hipMemcpyAsync(sp, c->sph.p, (size_t)g.W * g.F * sizeof(double2),
                            hipMemcpyDeviceToHost, s));
   FASST_HIP(hipStreamSynchronize(s));
+  FASST_HIP(hipEventElapsedTime(&c->ms_fwd, c->ev[0], c->ev[1]));
   return FASST_OK;
 }
 
@@ -710,6 +721,7 @@ int cqt_inverse(cqt_ctx *c, const double *sp, long L, double *y) {
   const bool rast = c->lin_N != 0;   // MinQT: invertFromSpCQTRast; CQT: invertFromCellCQT
   FASST_HIP(hipMemcpyAsync(c->sph.p, sp, (size_t)g.W * g.F * sizeof(double2),
                            hipMemcpyHostToDevice, s));
+  FASST_HIP(hipEventRecord(c->ev[2], s));
   k_cqt_transpose<<<dim3((g.W + 15) / 16, (g.F + 15) / 16), 256, 0, s>>>(c->sph.p, c->sp.p, g.F,
                                                                           g.W);
   FASST_LAUNCH_CHECK();
@@ -798,8 +810,17 @@ int cqt_inverse(cqt_ctx *c, const double *sp, long L, double *y) {
                                                           c->lwin.p, off + c->lin_N / 2, yout, L);
     FASST_LAUNCH_CHECK();
   }
+  FASST_HIP(hipEventRecord(c->ev[3], s));
   FASST_HIP(hipMemcpyAsync(y, yout, L * sizeof(double), hipMemcpyDeviceToHost, s));
   FASST_HIP(hipStreamSynchronize(s));
+  FASST_HIP(hipEventElapsedTime(&c->ms_inv, c->ev[2], c->ev[3]));
+  return FASST_OK;
+}
+
+int cqt_device_ms(cqt_ctx *c, double *forward_ms, double *inverse_ms) {
+  if (!c) return FASST_ERR_SHAPE;
+  if (forward_ms) *forward_ms = c->ms_fwd;
+  if (inverse_ms) *inverse_ms = c->ms_inv;
   return FASST_OK;
 }
 

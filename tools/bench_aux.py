@@ -4,6 +4,11 @@
                     NF0=1092, P=30, K=4, R=40), SIMM.py:613-941
   --workload nmf    NMF_decomposition iterations/s at config 2 (F=1025,
                     T=2000, K=64), tools/nmf.py:34-59
+  --workload cqt    MinQT front end (tftransforms/minqt.py:471-646, 1410-1450)
+                    as FASST builds it at 44.1 kHz (transf='mqt', wlen 4096,
+                    hop 512: FFTLen 8192, 5 octaves x 48 bins + 1980 linear
+                    bins) on a signal of T = 10000 STFT frames (the C3 clip
+                    length): forward and inverse transforms/s, device time
 
 Inputs are synthetic and resident in HBM before the timed region; the timed
 region is `steps` iterations of the update loop (simm_run / nmf_run, which
@@ -83,13 +88,45 @@ def bench_nmf(steps, warmup, F=1025, N=2000, K=64, seed=0):
             "reference_cpu": "0.0318 s/iter = 31.4 it/s (SURVEY §6, measured on CPU)"}
 
 
+def bench_cqt(steps, warmup, fs=44100, wlen=4096, hop=512, T=10000, seed=0):
+    from pyfasst_amd import _lib
+    from pyfasst_amd.tftransforms import minqt
+    L = hop * (T - 2)
+    rs = np.random.RandomState(seed)
+    x = rs.randn(L) * (1 + np.sin(np.arange(L) / 7000.0))
+    t = minqt.MinQTransfo(fmin=25, fmax=18000, bins=48, fs=fs, perfRast=1, linFTLen=wlen,
+                          atomHopFactor=hop / float(wlen))
+    fwd, inv = [], []
+    for i in range(warmup + steps):
+        t.computeTransform(x)
+        sp = t.transfo
+        y = t.invertTransform()
+        f, b = ctypes.c_double(), ctypes.c_double()
+        _lib.check(_lib.lib.cqt_device_ms(t._context(), ctypes.byref(f), ctypes.byref(b)), "ms")
+        if i >= warmup:
+            fwd.append(f.value)
+            inv.append(b.value)
+    k = t.cqtkernel
+    fm, im = float(np.median(fwd)), float(np.median(inv))
+    return {"metric": "MinQT forward transforms/sec (device time)", "value": round(1e3 / fm, 3),
+            "unit": "transforms/s", "forward_ms": round(fm, 3), "inverse_ms": round(im, 3),
+            "msamples_per_s_forward": round(L / fm / 1e3, 1), "steps": steps, "warmup": warmup,
+            "dtype": "f64", "data": "synthetic modulated noise, RandomState(0)",
+            "config": {"workload": "MinQT fs=%d linFTLen=%d hop=%d bins=48 fmin=25: %d samples "
+                                   "(T=%d frames), spCQT %dx%d, FFTLen %d, %d octaves, "
+                                   "kernel band %s" % (fs, wlen, hop, L, T, sp.shape[0],
+                                                       sp.shape[1], int(k.FFTLen),
+                                                       int(t.octaveNr), "n/a")},
+            "roundtrip_rel_err": float(np.abs(y - x).max() / np.abs(x).max())}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("simm", "nmf"), required=True)
+    ap.add_argument("--workload", choices=("simm", "nmf", "cqt"), required=True)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
-    fn = bench_simm if a.workload == "simm" else bench_nmf
+    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt}[a.workload]
     print(json.dumps(fn(a.steps, a.warmup)), flush=True)
 
 
