@@ -141,6 +141,11 @@ PATCHES = [
     ("tftransforms/minqt.py", r"self\.cellCQT\[noct\] = np\.zeros\(\[self\.cqtkernel\.bins \*\n\s+self\.cqtkernel\.winNr,",
      "self.cellCQT[noct] = np.zeros([int(self.cqtkernel.bins * self.cqtkernel.winNr),"),
     ("tftransforms/minqt.py", r"X\[nbin\]\.reshape\(\n\s+self\.cqtkernel\.winNr,", "X[nbin].reshape(int(self.cqtkernel.winNr),"),
+    # tracking.py (the reference's pure-Python Viterbi, golden source for the
+    # tracker): integer state paths
+    ("SeparateLeadStereo/tracking/tracking.py", r"bestStatePath = zeros\(numberOfFrames\)",
+     "bestStatePath = zeros(numberOfFrames, dtype=int)"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"np\.Inf\b", "np.inf"),
 ]
 
 

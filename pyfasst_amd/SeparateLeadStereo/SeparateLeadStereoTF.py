@@ -1,11 +1,14 @@
 """Lead / accompaniment separation from SIMM parameters (reference:
 SeparateLeadStereo/SeparateLeadStereoTF.py).
 
-Only the hot-path piece of `SeparateLeadProcess` is provided: the Wiener-like
-masks of `writeSeparatedSignals` (:1762-1871), computed on the GPU
-(`simm_separate`, include/fasst_simm.h) and inverted with the SIMM-pipeline
-istft.  The rest of the pipeline (file handling, F0 estimation, Viterbi
-tracking, chunking) is outside the accelerated path.
+Provided pieces of `SeparateLeadProcess`: the Wiener-like masks of
+`writeSeparatedSignals` (:1762-1871), computed on the GPU (`simm_separate`,
+include/fasst_simm.h) and inverted with the SIMM-pipeline istft; and the
+melody tracking `runViterbi` (:1150-1319), whose Viterbi recursion runs on
+the GPU (`viterbi_tracking`, include/fasst_viterbi.h) -- the transition
+matrix and log-density of the HMM are built on the host exactly as the
+reference builds them.  The rest of the pipeline (file handling, F0
+estimation driver, chunking) is outside the accelerated path.
 """
 import ctypes
 
@@ -14,6 +17,7 @@ import scipy.io.wavfile as wav
 
 from .. import _lib
 from . import separateLeadFunctions as slf
+from .tracking._tracking import viterbiTracking as viterbiTrackingArray
 
 eps = 10 ** -9      # SeparateLeadStereoTF.py:31
 
@@ -54,7 +58,7 @@ class SeparateLeadProcess(object):
 
     def __init__(self, SIMMParams=None, stftParams=None, XR=None, XL=None, files=None,
                  fs=44100, scaleData=1.0, dataType=np.int16, tfrepresentation='stft',
-                 device=None):
+                 trackingParams=None, N=None, verbose=False, device=None):
         self.SIMMParams = SIMMParams
         self.stftParams = stftParams
         self.XR, self.XL = XR, XL
@@ -63,7 +67,70 @@ class SeparateLeadProcess(object):
         self.scaleData = scaleData
         self.dataType = dataType
         self.tfrepresentation = tfrepresentation
+        self.trackingParams = trackingParams or {'minF0search': None, 'maxF0search': None}
+        if N is not None:
+            self.N = N
+        self.verbose = verbose
         self.device = device
+
+    def computeNFrames(self):
+        """Number of frames; here the caller provides N (or HF0 defines it)."""
+        if not hasattr(self, 'N'):
+            self.N = np.asarray(self.SIMMParams['HF0']).shape[1]
+
+    def runViterbi(self):
+        """Melody line by Viterbi decoding of HF0 (SeparateLeadStereoTF.py:1150-1319)."""
+        if not ('HF0' in self.SIMMParams.keys()):
+            raise AttributeError("HF0 has probably not been estimated yet.")
+        self.computeNFrames()
+        scale = 1.0
+        P = self.SIMMParams
+        NF0 = P['NF0'] * P['chirpPerF0']
+        nmaxF0, nminF0 = NF0, 0
+        minF0, maxF0 = P['minF0'], P['maxF0']
+        minF0search = self.trackingParams['minF0search']
+        maxF0search = self.trackingParams['maxF0search']
+        if minF0search is not None and minF0search > minF0 and minF0search < maxF0:
+            nminF0 = np.where(P['F0Table'] >= minF0search)[0][0] * P['chirpPerF0']
+        if (maxF0search is not None and maxF0search > minF0 and maxF0search < maxF0 and
+                maxF0search > minF0search):
+            nmaxF0 = (np.where(P['F0Table'] >= maxF0search)[0][0] + 1) * P['chirpPerF0']
+        NF0 = nmaxF0 - nminF0
+        # Toeplitz note-distance transitions + silence state, row-normalised (:1183-1208)
+        transitions = np.exp(-np.floor(np.arange(0, NF0) / P['stepNotes']) * scale)
+        cutoffnote = np.minimum(NF0, 2 * 5 * P['stepNotes'])
+        transitions[cutoffnote:] = transitions[cutoffnote - 1]
+        T = np.zeros([NF0 + 1, NF0 + 1])
+        b = np.arange(NF0)
+        T[0:NF0, 0:NF0] = transitions[np.array(np.abs(np.outer(np.ones(NF0), b) -
+                                                      np.outer(b, np.ones(NF0))), dtype=int)]
+        T[0:NF0, NF0] = transitions[cutoffnote - 1] * 10 ** (-90)
+        T[NF0, 0:NF0] = transitions[cutoffnote - 1] * 10 ** (-80)
+        T[NF0, NF0] = transitions[cutoffnote - 1] * 10 ** (-100)
+        T = T / np.outer(np.sum(T, axis=1), np.ones(NF0 + 1))
+        prior = 1 / (NF0 + 1.0) * np.ones([NF0 + 1])
+        # log-density with the reference's floor for empty frames (:1210-1216)
+        HF0 = np.asarray(P['HF0'])
+        logHF0 = np.zeros([NF0 + 1, self.N])
+        normHF0 = np.amax(HF0[nminF0:nmaxF0], axis=0)
+        with np.errstate(divide='ignore'):
+            logHF0[0:NF0, :] = np.log(HF0[nminF0:nmaxF0])
+        logHF0[0:NF0, normHF0 == 0] = np.amin(logHF0[logHF0 > -np.inf])
+        logHF0[NF0, :] = np.maximum(np.amin(logHF0[logHF0 > -np.inf]), -100)
+        with np.errstate(divide='ignore'):
+            logT, logprior = np.log(T), np.log(prior)
+        # the pipeline tracks NF0 states of the NF0 + 1 rows (:1220-1222)
+        indexBestPath = viterbiTrackingArray(NF0, self.N, logHF0, logprior, logT,
+                                             verbose=False, device=self.device)
+        indexBestPath += nminF0
+        freqMelody = P['F0Table'][np.array(indexBestPath / P['chirpPerF0'], dtype=int)]
+        freqMelody[indexBestPath == 0] = - freqMelody[indexBestPath == 0]
+        if 'pitch_output_file' in self.files:
+            np.savetxt(self.files['pitch_output_file'],
+                       np.array([np.arange(self.N) * self.stftParams['hopsize'] /
+                                 np.double(self.fs), freqMelody]).T)
+        self.indexBestPath = indexBestPath
+        self.freqMelody = freqMelody
 
     def separated_signals(self, suffix='.wav'):
         """(vest [2][L], mest [2][L]) float waveforms before int conversion."""

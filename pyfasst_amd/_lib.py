@@ -1,5 +1,6 @@
 """ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h,
-include/fasst_simm.h, include/fasst_nmf.h and include/fasst_cqt.h).
+include/fasst_simm.h, include/fasst_nmf.h, include/fasst_cqt.h and
+include/fasst_viterbi.h).
 
 The product path has no CPU fallback: if the HIP library is missing this
 module raises at import time, and every compute call raises if the device
@@ -32,6 +33,7 @@ lib = ctypes.CDLL(LIB_PATH)
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
+_llp = ctypes.POINTER(ctypes.c_longlong)
 
 # name -> (restype, argtypes); must match include/*.h exactly
 SIGNATURES = {
@@ -89,6 +91,10 @@ SIGNATURES = {
     "cqt_forward": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
     "cqt_inverse": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
     "cqt_device_ms": (ctypes.c_int, [_vp, _dp, _dp]),
+    # include/fasst_viterbi.h
+    "viterbi_tracking": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp,
+                                        ctypes.c_long, _dp, _dp, ctypes.c_long, _llp]),
+    "viterbi_last_timing": (ctypes.c_int, [_dp, _ip]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -305,6 +305,70 @@ def run_cqt():
     print("cqt", {k: np.shape(v) for k, v in out.items() if k.startswith('X_')})
 
 
+def run_viterbi():
+    """Viterbi tracker (SeparateLeadStereo/tracking/tracking.py, the reference's
+    own pure-Python tracker; same algorithm as _tracking.pyx) on seeded
+    inputs, and runViterbi's transition / log-density construction
+    (SeparateLeadStereoTF.py:1150-1319) captured at its tracker call."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    from pyfasst.SeparateLeadStereo.tracking import tracking as TR
+    from pyfasst.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    rs = np.random.RandomState(41)
+    out = {}
+    # random dense HMM
+    S, N = 37, 53
+    T = rs.gamma(0.5, 1.0, size=(S, S))
+    T /= T.sum(axis=1)[:, None]
+    out['r_logD'] = np.log(rs.gamma(1.0, 1.0, size=(S, N)))
+    out['r_logT'] = np.log(T)
+    out['r_prior'] = np.log(np.ones(S) / S)
+    out['r_path'] = TR.viterbiTrackingArray(out['r_logD'], out['r_prior'], out['r_logT'])
+    out['r_path_naive'] = TR.viterbiTracking(out['r_logD'], out['r_prior'], out['r_logT'])
+    # ties everywhere (small integers) and impossible transitions (-inf)
+    S, N = 19, 40
+    out['t_logD'] = rs.randint(-3, 1, size=(S, N)).astype(float)
+    lt = rs.randint(-2, 1, size=(S, S)).astype(float)
+    lt[rs.rand(S, S) < 0.2] = -np.inf
+    lt[np.arange(S), np.arange(S)] = 0.0
+    out['t_logT'] = lt
+    out['t_prior'] = rs.randint(-1, 1, size=S).astype(float)
+    out['t_path'] = TR.viterbiTrackingArray(out['t_logD'], out['t_prior'], out['t_logT'])
+    out['t_path_naive'] = TR.viterbiTracking(out['t_logD'], out['t_prior'], out['t_logT'])
+    # runViterbi on a stub process: NF0 = 64 states + silence, stepNotes = 4
+    NF0, N = 64, 75
+    HF0 = rs.gamma(0.3, 1.0, size=(NF0, N))
+    HF0[:, 5] = 0.0
+    HF0[rs.rand(NF0, N) < 0.05] = 0.0
+    proc = object.__new__(SL.SeparateLeadProcess)
+    proc.SIMMParams = {'HF0': HF0, 'NF0': NF0, 'chirpPerF0': 1, 'minF0': 100., 'maxF0': 800.,
+                       'F0Table': 100. * 2 ** (np.arange(NF0) / 12.), 'stepNotes': 4}
+    proc.trackingParams = {'minF0search': 100., 'maxF0search': 800.}
+    proc.N = N
+    proc.computeNFrames = lambda: None
+    proc.files = {'pitch_output_file': '/tmp/golden_pitch.txt'}
+    proc.stftParams = {'hopsize': 256.}
+    proc.fs = 8000.
+    proc.verbose = False
+    seen = {}
+
+    def tracker(S_, N_, logD, prior, logT, verbose=False):
+        seen.update(S=S_, N=N_, logD=np.array(logD), prior=np.array(prior), logT=np.array(logT))
+        # Cython semantics: the first S_ states only
+        return TR.viterbiTrackingArray(logD[:S_, :N_], prior[:S_], logT[:S_, :S_])
+    SL.viterbiTrackingArray = tracker
+    proc.runViterbi()
+    out['m_HF0'] = HF0
+    out['m_S'] = np.array(seen['S'])
+    out['m_logD'], out['m_prior'], out['m_logT'] = seen['logD'], seen['prior'], seen['logT']
+    out['m_path'] = np.array(proc.indexBestPath)
+    out['m_freq'] = np.array(proc.freqMelody)
+    np.savez_compressed(os.path.join(HERE, "viterbi.npz"), **out)
+    print("viterbi", {k: np.shape(v) for k, v in out.items() if 'path' in k})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -328,12 +392,12 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--case":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
-         "lead": run_lead, "cqt": run_cqt}.get(
+         "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
-    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt"] + list(CASES))
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

@@ -1,0 +1,107 @@
+"""Viterbi melody tracker on the GPU vs the reference and the oracle.
+
+The path is integer output built from the reference's own double additions
+and comparisons, so every check here is bit-exact (assert_array_equal).
+tests/golden/viterbi.npz holds the reference's tracking.py outputs (random
+HMM, a tie-heavy HMM with impossible transitions, and runViterbi's
+construction on a stub SeparateLeadProcess).  Larger cases (the one-launch-
+per-frame kernel path, S > 135) are checked against the oracle restatement
+of _tracking.pyx.
+"""
+import numpy as np
+import pytest
+
+import viterbi_ref as V
+from helpers import load
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu():
+    from pyfasst_amd.SeparateLeadStereo.tracking._tracking import viterbiTracking
+    return viterbiTracking
+
+
+def _kind():
+    import ctypes
+    from pyfasst_amd import _lib
+    ms, kind = ctypes.c_double(), ctypes.c_int()
+    _lib.lib.viterbi_last_timing(ctypes.byref(ms), ctypes.byref(kind))
+    return kind.value
+
+
+@pytest.mark.parametrize("p", ['r', 't'])
+def test_viterbi_golden_gpu(p):
+    g = load("viterbi")
+    S, N = g[p + '_logD'].shape
+    path = _gpu()(S, N, g[p + '_logD'], g[p + '_prior'], g[p + '_logT'])
+    assert path.dtype == np.int64
+    np.testing.assert_array_equal(path, g[p + '_path'])
+    np.testing.assert_array_equal(path, g[p + '_path_naive'])
+    from pyfasst_amd.SeparateLeadStereo.tracking import tracking
+    np.testing.assert_array_equal(
+        tracking.viterbiTrackingArray(g[p + '_logD'], g[p + '_prior'], g[p + '_logT']),
+        g[p + '_path'])
+
+
+def test_run_viterbi_golden_gpu(tmp_path):
+    """SeparateLeadProcess.runViterbi: transitions, log-density, tracker on NF0
+    of the NF0 + 1 states, melody frequencies -- as the reference's."""
+    from pyfasst_amd.SeparateLeadStereo.SeparateLeadStereoTF import SeparateLeadProcess
+    g = load("viterbi")
+    HF0 = g['m_HF0']
+    NF0, N = HF0.shape
+    proc = SeparateLeadProcess(
+        SIMMParams={'HF0': HF0, 'NF0': NF0, 'chirpPerF0': 1, 'minF0': 100., 'maxF0': 800.,
+                    'F0Table': 100. * 2 ** (np.arange(NF0) / 12.), 'stepNotes': 4},
+        trackingParams={'minF0search': 100., 'maxF0search': 800.}, N=N,
+        files={'pitch_output_file': str(tmp_path / "pitch.txt")}, stftParams={'hopsize': 256.},
+        fs=8000.)
+    proc.runViterbi()
+    np.testing.assert_array_equal(proc.indexBestPath, g['m_path'])
+    np.testing.assert_array_equal(proc.freqMelody, g['m_freq'])
+    assert (tmp_path / "pitch.txt").exists()
+
+
+@pytest.mark.parametrize("S,N,seed,kind", [(300, 400, 0, 1), (1093, 160, 1, 1), (138, 50, 2, 1),
+                                          (137, 50, 3, 0)])
+def test_viterbi_large_vs_oracle(S, N, seed, kind):
+    """Both kernel paths around the LDS-resident size (S <= 137: one workgroup;
+    beyond: one launch per frame), vs the oracle."""
+    rs = np.random.RandomState(seed)
+    logD = np.log(rs.gamma(0.5, 1.0, size=(S + 1, N)))
+    logT, prior = V.melody_transitions(S, 16)
+    path = _gpu()(S, N, logD, prior, logT)
+    assert _kind() == kind
+    np.testing.assert_array_equal(path, V.viterbi_tracking(S, N, logD, prior, logT))
+
+
+def test_viterbi_nan_and_inf_rules():
+    """The pyx's strict '>' scan: NaN candidates never win, a NaN at s' = 0
+    sticks; -inf everywhere keeps state 0; exact ties keep the first state."""
+    rs = np.random.RandomState(3)
+    for S, N in ((12, 30), (200, 20)):
+        logD = rs.randint(-2, 1, size=(S, N)).astype(float)
+        logT = rs.randint(-2, 1, size=(S, S)).astype(float)
+        logT[rs.rand(S, S) < 0.3] = -np.inf
+        logT[0, rs.rand(S) < 0.2] = np.nan        # NaN from state 0
+        logT[5, :] = np.nan                         # NaN from a later state
+        logD[:, 7] = -np.inf                        # an impossible frame
+        prior = np.zeros(S)
+        with np.errstate(invalid='ignore'):
+            ref = V.viterbi_tracking(S, N, logD, prior, logT)
+        np.testing.assert_array_equal(_gpu()(S, N, logD, prior, logT), ref)
+
+
+def test_viterbi_strided_inputs():
+    """Row pitches larger than the used block (the pipeline's NF0 + 1 rows)."""
+    rs = np.random.RandomState(4)
+    big = np.log(rs.gamma(1.0, 1.0, size=(50, 70)))
+    logT, prior = V.melody_transitions(40, 4)
+    path = _gpu()(40, 60, big, prior, logT)
+    np.testing.assert_array_equal(path, V.viterbi_tracking(40, 60, big, prior, logT))
+
+
+def test_viterbi_bad_shape_raises():
+    with pytest.raises(ValueError):
+        _gpu()(10, 5, np.zeros((9, 5)), np.zeros(10), np.zeros((10, 10)))

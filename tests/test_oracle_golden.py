@@ -147,3 +147,21 @@ def test_lead_golden():
         np.testing.assert_array_equal(y, g['est_' + name])
     voc = np.array(np.round(np.array([g['est_vR'], g['est_vL']]).T), dtype=np.int16)
     np.testing.assert_array_equal(voc, g['voc_wav'])
+
+
+def test_viterbi_golden():
+    """Viterbi tracker (tracking.py / _tracking.pyx) and runViterbi's inputs."""
+    import viterbi_ref as V
+    g = load("viterbi")
+    for p in ('r', 't'):
+        S, N = g[p + '_logD'].shape
+        path = V.viterbi_tracking(S, N, g[p + '_logD'], g[p + '_prior'], g[p + '_logT'])
+        np.testing.assert_array_equal(path, g[p + '_path'])
+        np.testing.assert_array_equal(path, g[p + '_path_naive'])
+    logT, prior = V.melody_transitions(64, 4)
+    np.testing.assert_array_equal(logT, g['m_logT'])
+    np.testing.assert_array_equal(prior, g['m_prior'])
+    np.testing.assert_array_equal(V.melody_log_density(g['m_HF0']), g['m_logD'])
+    S = int(g['m_S'])
+    path = V.viterbi_tracking(S, g['m_HF0'].shape[1], g['m_logD'], g['m_prior'], g['m_logT'])
+    np.testing.assert_array_equal(path, g['m_path'])

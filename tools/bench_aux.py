@@ -9,6 +9,9 @@
                     hop 512: FFTLen 8192, 5 octaves x 48 bins + 1980 linear
                     bins) on a signal of T = 10000 STFT frames (the C3 clip
                     length): forward and inverse transforms/s, device time
+  --workload viterbi  melody tracking (_tracking.pyx:11-93) at config 5:
+                    S = 1092 F0 states, N = 20000 frames (runViterbi's
+                    transitions, stepNotes 16): tracks/s, device time
 
 Inputs are synthetic and resident in HBM before the timed region; the timed
 region is `steps` iterations of the update loop (simm_run / nmf_run, which
@@ -120,13 +123,45 @@ def bench_cqt(steps, warmup, fs=44100, wlen=4096, hop=512, T=10000, seed=0):
             "roundtrip_rel_err": float(np.abs(y - x).max() / np.abs(x).max())}
 
 
+def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
+    from pyfasst_amd import _lib
+    from pyfasst_amd.SeparateLeadStereo.tracking._tracking import viterbiTracking
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import viterbi_ref as V
+    rs = np.random.RandomState(seed)
+    logD = np.log(rs.gamma(0.3, 1.0, size=(S + 1, N)))
+    logT, prior = V.melody_transitions(S, 16)
+    ms = []
+    for i in range(warmup + steps):
+        viterbiTracking(S, N, logD, prior, logT)
+        m, k = ctypes.c_double(), ctypes.c_int()
+        _lib.lib.viterbi_last_timing(ctypes.byref(m), ctypes.byref(k))
+        if i >= warmup:
+            ms.append(m.value)
+    dm = float(np.median(ms))
+    # CPU: the oracle restatement of the pyx recursion on a bounded sample
+    n_cpu = 40
+    t0 = time.perf_counter()
+    V.viterbi_tracking(S, n_cpu, logD, prior, logT)
+    cpu_s = (time.perf_counter() - t0) / (n_cpu - 1) * (N - 1)
+    return {"metric": "Viterbi melody tracks/sec (config 5 size, device time)",
+            "value": round(1e3 / dm, 3), "unit": "tracks/s", "device_ms": round(dm, 2),
+            "us_per_frame": round(dm * 1e3 / N, 3), "steps": steps, "warmup": warmup,
+            "dtype": "f64", "data": "synthetic log-gamma densities, RandomState(0)",
+            "config": {"workload": "viterbiTracking S=%d N=%d (max-plus S^2 per frame)" % (S, N)},
+            "maxplus_gops": round(float(S) * S * (N - 1) / (dm * 1e-3) / 1e9, 1),
+            "cpu_baseline": {"value": round(1.0 / cpu_s, 5), "unit": "tracks/s", "cores": 1,
+                             "kind": "port", "sample": "oracle/viterbi_ref.py, %d frames, "
+                             "scaled to N=%d" % (n_cpu, N)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("simm", "nmf", "cqt"), required=True)
+    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi"), required=True)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
-    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt}[a.workload]
+    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt, "viterbi": bench_viterbi}[a.workload]
     print(json.dumps(fn(a.steps, a.warmup)), flush=True)
 
 
