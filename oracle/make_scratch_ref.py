@@ -146,6 +146,24 @@ PATCHES = [
     ("SeparateLeadStereo/tracking/tracking.py", r"bestStatePath = zeros\(numberOfFrames\)",
      "bestStatePath = zeros(numberOfFrames, dtype=int)"),
     ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"np\.Inf\b", "np.inf"),
+    # SIMM dictionaries (separateLeadFunctions.py:696-1146): numpy < 1.13 let
+    # rfft drop the imaginary part of the complex odgd (ComplexWarning) and
+    # compared an array window with a string to False; float sizes
+    ("tftransforms/stft.py", r"STFT\[:,n\] = np\.fft\.rfft\(frameToProcess, np\.int32\(nfft\)\)",
+     "STFT[:,n] = np.fft.rfft(np.real(frameToProcess), np.int32(nfft))"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"    if analysisWindowType=='sinebell':\n",
+     "    if not isinstance(analysisWindowType, str):\n        analysisWindow = analysisWindowType\n"
+     "    elif analysisWindowType=='sinebell':\n"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"for fundamentalFrequency in np\.arange\(numberOfF0\):",
+     "for fundamentalFrequency in np.arange(int(numberOfF0)):"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"WF0 = np\.zeros\(\[transform\.freqbins,\n\s+numberElementsInWF0\],",
+     "WF0 = np.zeros([int(transform.freqbins), int(numberElementsInWF0)],"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"prototypeSineWindow = hann\(lengthSineWindow\)",
+     "prototypeSineWindow = hann(int(lengthSineWindow))"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"bigWindow = np\.zeros\(\[sizeBigWindow \* 2, 1\]\)",
+     "bigWindow = np.zeros([int(sizeBigWindow * 2), 1])"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"bigWindow\[\(sizeBigWindow - lengthSineWindow / 2\.0\):\\\n\s+\(sizeBigWindow \+ lengthSineWindow / 2\.0\)\]",
+     "bigWindow[int(sizeBigWindow - lengthSineWindow / 2.0):int(sizeBigWindow + lengthSineWindow / 2.0)]"),
 ]
 
 

@@ -1,5 +1,5 @@
-"""SIMM-pipeline STFT / iSTFT on the GPU (reference:
-SeparateLeadStereo/separateLeadFunctions.py:90-233).
+"""SIMM-pipeline STFT / iSTFT and dictionaries on the GPU (reference:
+SeparateLeadStereo/separateLeadFunctions.py:90-233, :696-886, :1074-1146).
 
 These differ from tftransforms/stft.py: `stft` takes a start/stop frame range
 and pads half a window at both ends (:90-161); `istft` keeps the leading half
@@ -14,7 +14,7 @@ from .. import _lib
 from .._lib import check, dptr, lib
 from ..tools.utils import sinebell
 
-__all__ = ["sinebell", "stft", "istft"]
+__all__ = ["sinebell", "stft", "istft", "generate_WF0_TR_chirped", "generateHannBasis"]
 
 
 def _dev(device):
@@ -72,3 +72,115 @@ def istft(X, analysisWindow=None, window=sinebell(2048), hopsize=256.0, nfft=204
     if originalDataLen is not None:
         y = y[:originalDataLen]
     return y
+
+
+# ---------------------------------------------------------------- dictionaries
+def _odgd_amplitudes(F0, Ot, partialMax):
+    """KLGLOTT88 partial amplitudes, the reference's expression
+    (separateLeadFunctions.py:916-930); host-side parameters of the GPU synthesis."""
+    frequency_numbers = np.arange(1, partialMax + 1)
+    temp_array = 1j * 2.0 * np.pi * frequency_numbers * Ot
+    return (F0 * 27 / 4 * (np.exp(-temp_array) + (2 * (1 + 2 * np.exp(-temp_array)) / temp_array) -
+                           (6 * (1 - np.exp(-temp_array)) / (temp_array ** 2))) / temp_array)
+
+
+def generate_WF0_TR_chirped(transform, minF0, maxF0, stepNotes=4, Ot=0.5, perF0=1,
+                            depthChirpInSemiTone=0.5, loadWF0=True, verbose=False,
+                            device=None):
+    """F0Table, WF0, transform = generate_WF0_TR_chirped(...)
+    (separateLeadFunctions.py:696-886).
+
+    For the STFT transform (SeparateLeadProcess' default tfrepresentation
+    'stft'), WF0[:, j] = |STFT(odgd_j)[:, middle frame]|^2 is synthesised on
+    the GPU (dict_wf0_stft, include/fasst_dict.h).  The cache file holds
+    F0Table and WF0 only (the reference also pickles the transform object).
+    The CQT / MinQT variants feed the complex odgd into those transforms;
+    they are outside the GPU path (NotImplementedError)."""
+    import os
+    if hasattr(transform, 'octaveNr') or hasattr(transform, 'cqtkernel'):
+        raise NotImplementedError("generate_WF0_TR_chirped with a CQT/MinQT transform is "
+                                  "outside the GPU path (the STFT transform is supported)")
+    lengthWindow = (transform.freqbins - 1) * 2 * 2
+    filename = ''.join(['wf0gpu_%s_' % transform.transformname, '_minF0-', str(minF0),
+                        '_maxF0-', str(maxF0), '_stepNotes-', str(int(stepNotes)),
+                        '_Ot-', str(Ot), '_perF0-', str(int(perF0)),
+                        '_depthChirp-', str(depthChirpInSemiTone),
+                        '_lengthWindow-%d' % lengthWindow, '_fs-%s' % str(transform.fs),
+                        '_ftlen-%d' % transform.ftlen, '_hop-%d' % transform.fthop,
+                        '_win-%s' % getattr(transform.winFunc, '__name__', 'w'), '.npz'])
+    if os.path.isfile(filename) and loadWF0:
+        struc = np.load(filename)
+        return struc['F0Table'], struc['WF0'], transform
+    minF0, maxF0 = np.double(minF0), np.double(maxF0)
+    Fs, stepNotes = np.double(transform.fs), np.double(stepNotes)
+    numberOfF0 = np.ceil(12.0 * stepNotes * np.log2(maxF0 / minF0)) + 1
+    F0Table = minF0 * (2 ** (np.arange(numberOfF0, dtype=np.double) / (12 * stepNotes)))
+    # columns: the F0 comb, then perF0 - 1 chirps around it (:829-879)
+    f1, f2, amps = [], [], []
+    for i in range(int(numberOfF0)):
+        F0 = F0Table[i]
+        f1.append(F0)
+        f2.append(F0)
+        amps.append(_odgd_amplitudes(F0, np.double(Ot), np.floor((Fs / 2) / F0)))
+        for c in range(perF0 - 1):
+            F2 = F0 * (2 ** ((c + 1.0) * depthChirpInSemiTone / (12.0 * (perF0 - 1.0))))
+            F1 = 2.0 * F0 - F2
+            f1.append(np.double(F1))
+            f2.append(np.double(F2))
+            amps.append(_odgd_amplitudes(np.double(F1 + F2) / 2.0, np.double(Ot),
+                                         np.floor((Fs / 2) / np.max([F1, F2]))))
+    ncol = len(f1)
+    npart = np.array([a.size for a in amps], dtype=np.int32)
+    pmax = max(1, int(npart.max()))
+    A = np.zeros((ncol, pmax), dtype=np.complex128)
+    for j, a in enumerate(amps):
+        A[j, :a.size] = a
+    # the middle frame of the transform's STFT of an lengthWindow-sample
+    # signal (STFT.computeTransform, :838-847 with stft.py:3-69, :383-385)
+    hop = int(transform.fthop)
+    nfr = int(np.ceil(lengthWindow / np.double(hop))) + 2
+    time_stamps = np.arange(nfr) * hop / np.double(transform.fs)
+    time_stamps *= transform.fs
+    mid = int(np.argmin((lengthWindow / 2. - time_stamps) ** 2))
+    window = np.ascontiguousarray(transform.window, dtype=np.float64)
+    frame_start = mid * hop - window.size // 2
+    WF0 = np.empty((transform.freqbins, ncol))
+    f1a, f2a = np.ascontiguousarray(f1, dtype=np.float64), np.ascontiguousarray(f2, dtype=np.float64)
+    dev = _dev(device if device is not None else getattr(transform, 'device', None))
+    check(lib.dict_wf0_stft(dev, ncol, dptr(f1a), dptr(f2a), _lib.iptr(npart), pmax, dptr(A),
+                            float(Fs), int(lengthWindow), dptr(window), window.size,
+                            int(transform.ftlen), int(frame_start), dptr(WF0)), "dict_wf0_stft")
+    try:
+        np.savez(filename, F0Table=F0Table, WF0=WF0)
+    except OSError:
+        pass
+    return F0Table, WF0, transform
+
+
+def generateHannBasis(numberFrequencyBins, sizeOfFourier, Fs, frequencyScale='linear',
+                      numberOfBasis=20, overlap=.75):
+    """WGAMMA: overlapping Hann bumps along the frequency axis
+    (separateLeadFunctions.py:1074-1146; a few hundred host-side numbers)."""
+    if frequencyScale != 'linear':
+        print("The desired feature for frequencyScale is not recognized yet...")
+        return 0
+    numberOfWindowsForUnit = np.ceil(1.0 / (1.0 - overlap))
+    overlap = 1.0 - 1.0 / np.double(numberOfWindowsForUnit)
+    lengthSineWindow = np.ceil(numberFrequencyBins / ((1.0 - overlap) * (numberOfBasis - 1) + 1 -
+                                                      2.0 * overlap))
+    lengthSineWindow = 2.0 * np.floor(lengthSineWindow / 2.0)
+    mappingFrequency = np.arange(numberFrequencyBins)
+    sizeBigWindow = 2.0 * numberFrequencyBins
+    firstWindowCenter = -numberOfWindowsForUnit + 1
+    lastWindowCenter = numberOfBasis - numberOfWindowsForUnit + 1
+    sineCenters = np.round(np.arange(firstWindowCenter, lastWindowCenter) * (1 - overlap) *
+                           np.double(lengthSineWindow) + lengthSineWindow / 2.0)
+    prototypeSineWindow = np.hanning(int(lengthSineWindow))
+    bigWindow = np.zeros([int(sizeBigWindow * 2), 1])
+    bigWindow[int(sizeBigWindow - lengthSineWindow / 2.0):
+              int(sizeBigWindow + lengthSineWindow / 2.0)] = np.vstack(prototypeSineWindow)
+    WGAMMA = np.zeros([numberFrequencyBins, numberOfBasis])
+    for p in np.arange(numberOfBasis):
+        WGAMMA[:, p] = np.hstack(bigWindow[np.int32(mappingFrequency - sineCenters[p] +
+                                                    sizeBigWindow)])
+    return WGAMMA

@@ -1,6 +1,6 @@
 """ctypes binding of libfasst_hip.so (declared in include/fasst_hip.h,
-include/fasst_simm.h, include/fasst_nmf.h, include/fasst_cqt.h and
-include/fasst_viterbi.h).
+include/fasst_simm.h, include/fasst_nmf.h, include/fasst_cqt.h,
+include/fasst_viterbi.h and include/fasst_dict.h).
 
 The product path has no CPU fallback: if the HIP library is missing this
 module raises at import time, and every compute call raises if the device
@@ -95,6 +95,11 @@ SIGNATURES = {
     "viterbi_tracking": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp,
                                         ctypes.c_long, _dp, _dp, ctypes.c_long, _llp]),
     "viterbi_last_timing": (ctypes.c_int, [_dp, _ip]),
+    # include/fasst_dict.h
+    "dict_wf0_stft": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _ip, ctypes.c_int, _dp,
+                                     ctypes.c_double, ctypes.c_int, _dp, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_long, _dp]),
+    "dict_last_ms": (ctypes.c_int, [_dp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

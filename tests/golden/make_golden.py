@@ -369,6 +369,37 @@ def run_viterbi():
     print("viterbi", {k: np.shape(v) for k, v in out.items() if 'path' in k})
 
 
+def run_wf0():
+    """SIMM dictionaries: generate_WF0_TR_chirped with the STFT transform
+    SeparateLeadProcess.computeWF0 builds for tfrepresentation='stft'
+    (SeparateLeadStereoTF.py:646-681), with and without chirps, and
+    generateHannBasis (separateLeadFunctions.py:1074-1146)."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    os.chdir("/tmp")        # the reference writes its .npz cache to the cwd
+    import numpy as np
+    from pyfasst.SeparateLeadStereo import separateLeadFunctions as slf
+    from pyfasst.tftransforms import tft
+    from pyfasst.tools.utils import sqrt_blackmanharris
+    out = {}
+    for tag, (fs, nft, minF0, maxF0, stepNotes, perF0) in {
+            'a': (8000, 256, 100, 800, 4, 1), 'b': (8000, 512, 150, 600, 2, 3),
+            'c': (16000, 256, 60, 1000, 1, 1)}.items():
+        t = tft.tftransforms['stft'](fmin=25, fmax=18000, bins=48, fs=fs, linFTLen=nft,
+                                     atomHopFactor=0.25, winFunc=sqrt_blackmanharris, perfRast=1)
+        F0Table, WF0, _ = slf.generate_WF0_TR_chirped(
+            transform=t, minF0=minF0, maxF0=maxF0, stepNotes=stepNotes, Ot=0.5, perF0=perF0,
+            depthChirpInSemiTone=0.5, loadWF0=False)
+        out['F0Table_' + tag], out['WF0_' + tag] = F0Table, WF0
+    for tag, (F, nft, fs, P, ov) in {'h1': (129, 256, 8000, 10, 0.75),
+                                     'h2': (257, 512, 16000, 30, 0.5),
+                                     'h3': (2049, 4096, 44100, 30, 0.75)}.items():
+        out['WGAMMA_' + tag] = slf.generateHannBasis(F, nft, fs, numberOfBasis=P, overlap=ov)
+    np.savez_compressed(os.path.join(HERE, "wf0.npz"), **out)
+    print("wf0", {k: np.shape(v) for k, v in out.items()})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -392,12 +423,12 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--case":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
-         "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi}.get(
+         "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
-    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi"] + list(CASES))
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

@@ -1,0 +1,82 @@
+"""SIMM dictionaries on the GPU vs the reference (tests/golden/wf0.npz) and
+the oracle (oracle/dict_ref.py).
+
+WF0 columns are power spectra of a synthesised harmonic comb: the GPU
+evaluates the reference's phase expression in the same double operations but
+with its own sincos and a radix-2 FFT, so it is held to 1e-10 of each
+column's peak (north_star's bar is 1e-4).  WGAMMA is host-side and exact.
+"""
+import numpy as np
+import pytest
+
+import dict_ref as D
+from helpers import load
+
+pytestmark = pytest.mark.gpu
+
+CASES = {'a': (8000, 256, 100, 800, 4, 1), 'b': (8000, 512, 150, 600, 2, 3),
+         'c': (16000, 256, 60, 1000, 1, 1)}
+
+
+def _stft(fs, nft):
+    from pyfasst_amd.tftransforms.stft import STFT
+    from pyfasst_amd.tools.utils import sqrt_blackmanharris
+    return STFT(linFTLen=nft, atomHopFactor=0.25, winFunc=sqrt_blackmanharris, fs=fs)
+
+
+def _colrel(a, b):
+    return float(np.max(np.abs(a - b) / np.max(np.abs(b), axis=0)))
+
+
+@pytest.mark.parametrize("tag", sorted(CASES))
+def test_wf0_golden_gpu(tag, tmp_path, monkeypatch):
+    from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
+    monkeypatch.chdir(tmp_path)
+    g = load("wf0")
+    fs, nft, minF0, maxF0, stepNotes, perF0 = CASES[tag]
+    F0Table, WF0, _ = slf.generate_WF0_TR_chirped(_stft(fs, nft), minF0, maxF0,
+                                                  stepNotes=stepNotes, perF0=perF0,
+                                                  loadWF0=False)
+    np.testing.assert_array_equal(F0Table, g['F0Table_' + tag])
+    assert WF0.shape == g['WF0_' + tag].shape
+    assert _colrel(WF0, g['WF0_' + tag]) < 1e-10
+    # normalised as computeWF0 does (SeparateLeadStereoTF.py:676)
+    n1, n2 = WF0 / WF0.sum(axis=0), g['WF0_' + tag] / g['WF0_' + tag].sum(axis=0)
+    assert _colrel(n1, n2) < 1e-10
+    # the cache round trip returns the same arrays
+    F0b, WF0b, _ = slf.generate_WF0_TR_chirped(_stft(fs, nft), minF0, maxF0, stepNotes=stepNotes,
+                                               perF0=perF0, loadWF0=True)
+    np.testing.assert_array_equal(WF0b, WF0)
+
+
+def test_wf0_config5_size_vs_oracle(tmp_path, monkeypatch):
+    """The config-5 dictionary geometry (44.1 kHz, NFT 4096, minF0 39, maxF0
+    2000, stepNotes 16: 1092 combs of up to 565 partials) on a subset of F0s
+    checked against the oracle."""
+    from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
+    monkeypatch.chdir(tmp_path)
+    t = _stft(44100, 4096)
+    F0Table, WF0, _ = slf.generate_WF0_TR_chirped(t, 39, 2000, stepNotes=16, loadWF0=False)
+    assert WF0.shape == (2049, 1092)
+    for i in (0, 1, 500, 1091):
+        odgd = D.generate_odgd(F0Table[i], 44100, lengthOdgd=8192)
+        ref = D.stft_mid_frame_power(odgd, t.window, t.fthop, 4096, 44100)
+        assert np.max(np.abs(WF0[:, i] - ref)) / np.max(ref) < 1e-10
+
+
+def test_hann_basis_exact():
+    from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
+    g = load("wf0")
+    for tag, (F, nft, fs, P, ov) in {'h1': (129, 256, 8000, 10, 0.75),
+                                     'h2': (257, 512, 16000, 30, 0.5),
+                                     'h3': (2049, 4096, 44100, 30, 0.75)}.items():
+        np.testing.assert_array_equal(slf.generateHannBasis(F, nft, fs, numberOfBasis=P,
+                                                            overlap=ov), g['WGAMMA_' + tag])
+
+
+def test_wf0_cqt_transform_not_on_gpu_path():
+    from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
+    from pyfasst_amd.tftransforms.minqt import MinQTransfo
+    t = MinQTransfo(fmin=100, fmax=3000, bins=12, fs=8000, linFTLen=256, perfRast=1)
+    with pytest.raises(NotImplementedError):
+        slf.generate_WF0_TR_chirped(t, 100, 800)

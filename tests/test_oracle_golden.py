@@ -165,3 +165,23 @@ def test_viterbi_golden():
     S = int(g['m_S'])
     path = V.viterbi_tracking(S, g['m_HF0'].shape[1], g['m_logD'], g['m_prior'], g['m_logT'])
     np.testing.assert_array_equal(path, g['m_path'])
+
+
+def test_wf0_dictionaries_golden():
+    """generate_WF0_TR_chirped (STFT transform) and generateHannBasis."""
+    import dict_ref as D
+    from cqt_ref import sqrt_blackmanharris
+    g = load("wf0")
+    for tag, (fs, nft, minF0, maxF0, stepNotes, perF0) in {
+            'a': (8000, 256, 100, 800, 4, 1), 'b': (8000, 512, 150, 600, 2, 3),
+            'c': (16000, 256, 60, 1000, 1, 1)}.items():
+        F0Table, WF0 = D.generate_wf0_tr_chirped_stft(
+            nft, int(nft * 0.25), sqrt_blackmanharris(nft), fs, minF0, maxF0, stepNotes,
+            perF0=perF0)
+        np.testing.assert_array_equal(F0Table, g['F0Table_' + tag])
+        np.testing.assert_array_equal(WF0, g['WF0_' + tag])
+    for tag, (F, nft, fs, P, ov) in {'h1': (129, 256, 8000, 10, 0.75),
+                                     'h2': (257, 512, 16000, 30, 0.5),
+                                     'h3': (2049, 4096, 44100, 30, 0.75)}.items():
+        np.testing.assert_array_equal(D.generate_hann_basis(F, nft, fs, numberOfBasis=P, overlap=ov),
+                                      g['WGAMMA_' + tag])

@@ -9,6 +9,9 @@
                     hop 512: FFTLen 8192, 5 octaves x 48 bins + 1980 linear
                     bins) on a signal of T = 10000 STFT frames (the C3 clip
                     length): forward and inverse transforms/s, device time
+  --workload wf0    SIMM source dictionary generate_WF0_TR_chirped at config
+                    5 (44.1 kHz, NFT 4096, 1092 KLGLOTT88 combs, STFT middle
+                    frame): device time per dictionary
   --workload viterbi  melody tracking (_tracking.pyx:11-93) at config 5:
                     S = 1092 F0 states, N = 20000 frames (runViterbi's
                     transitions, stepNotes 16): tracks/s, device time
@@ -123,6 +126,45 @@ def bench_cqt(steps, warmup, fs=44100, wlen=4096, hop=512, T=10000, seed=0):
             "roundtrip_rel_err": float(np.abs(y - x).max() / np.abs(x).max())}
 
 
+def bench_wf0(steps, warmup):
+    import tempfile
+    from pyfasst_amd import _lib
+    from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
+    from pyfasst_amd.tftransforms.stft import STFT
+    from pyfasst_amd.tools.utils import sqrt_blackmanharris
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dict_ref as D
+    os.chdir(tempfile.mkdtemp())
+    t = STFT(linFTLen=4096, atomHopFactor=0.25, winFunc=sqrt_blackmanharris, fs=44100)
+    ms = []
+    for i in range(warmup + steps):
+        F0Table, WF0, _ = slf.generate_WF0_TR_chirped(t, 39, 2000, stepNotes=16, loadWF0=False)
+        m = ctypes.c_double()
+        _lib.lib.dict_last_ms(ctypes.byref(m))
+        if i >= warmup:
+            ms.append(m.value)
+    dm = float(np.median(ms))
+    # CPU: the oracle (the reference's outer-product synthesis) on 8 of the 1092 F0s
+    idx = np.linspace(0, F0Table.size - 1, 8).astype(int)
+    t0 = time.perf_counter()
+    for i in idx:
+        D.stft_mid_frame_power(D.generate_odgd(F0Table[i], 44100, lengthOdgd=8192), t.window,
+                               t.fthop, 4096, 44100)
+    cpu_s = (time.perf_counter() - t0) / idx.size * F0Table.size
+    partials = sum(int(np.floor(22050.0 / f)) for f in F0Table)
+    return {"metric": "SIMM WF0 dictionaries/sec (config 5, device time)",
+            "value": round(1e3 / dm, 3), "unit": "dictionaries/s", "device_ms": round(dm, 3),
+            "steps": steps, "warmup": warmup, "dtype": "f64",
+            "config": {"workload": "generate_WF0_TR_chirped STFT NFT=4096 fs=44100 minF0=39 "
+                                   "maxF0=2000 stepNotes=16: %d combs, %d partials, 4096-sample "
+                                   "frames" % (F0Table.size, partials)},
+            "partial_samples_per_s": round(partials * 4096 / (dm * 1e-3) / 1e9, 2),
+            "cpu_baseline": {"value": round(1.0 / cpu_s, 5), "unit": "dictionaries/s",
+                             "cores": 1, "kind": "port",
+                             "sample": "oracle/dict_ref.py on 8 of the %d F0s, scaled"
+                                       % F0Table.size}}
+
+
 def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
     from pyfasst_amd import _lib
     from pyfasst_amd.SeparateLeadStereo.tracking._tracking import viterbiTracking
@@ -157,11 +199,11 @@ def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi"), required=True)
+    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi", "wf0"), required=True)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
-    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt, "viterbi": bench_viterbi}[a.workload]
+    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt, "viterbi": bench_viterbi, "wf0": bench_wf0}[a.workload]
     print(json.dumps(fn(a.steps, a.warmup)), flush=True)
 
 
