@@ -567,3 +567,49 @@ def nmf_decomp_init(SX, nbComps=10, niter=10, Winit=None, Hinit=None, updateW=Tr
             den = np.dot(1 / np.maximum(hat, EPS), W)
             H *= num / np.maximum(den, EPS)
     return W, H.T
+
+
+# ----------------------------------------------------------------------------
+# audioModel.py:2091-2222: spectral components initialised by IS-NMF of the
+# channel-averaged power Cx
+def _mono_power(model):
+    nc = 2
+    Cx = np.copy(np.real(model.Cx[0]))
+    Cx += np.real(model.Cx[2])
+    return Cx / np.double(nc)
+
+
+def init_nmf_indiv(model, niter=10, updateFreqBasis=True, updateTimeWeight=True,
+                   rng=np.random):
+    """initialize_all_spec_comps_with_NMF_indiv (audioModel.py:2118-2177)"""
+    nb = [sc['factor'][0]['FB'].shape[1] for sc in model.spec_comps.values()]
+    tot = int(np.sum(nb))
+    FBinit = np.zeros([model.nbFreqsSigRepr, tot])
+    TWinit = np.zeros([tot, model.nbFramesSigRepr])
+    for k, sc in model.spec_comps.items():
+        a = int(np.sum(nb[:k]))
+        FBinit[:, a:a + nb[k]] = sc['factor'][0]['FB']
+        TWinit[a:a + nb[k]] = sc['factor'][0]['TW']
+    W, H = nmf_decomp_init(_mono_power(model), nbComps=tot, niter=niter, Winit=FBinit,
+                           Hinit=TWinit, updateW=updateFreqBasis, updateH=updateTimeWeight,
+                           rng=rng)
+    for k, sc in model.spec_comps.items():
+        a = int(np.sum(nb[:k]))
+        if updateFreqBasis:
+            sc['factor'][0]['FB'] = np.maximum(W[:, a:a + nb[k]], EPS)
+        if updateTimeWeight:
+            sc['factor'][0]['TW'] = np.maximum(H[a:a + nb[k]], EPS)
+    model.renormalize_parameters(rng=rng)
+
+
+def init_nmf_same(model, niter=10, rng=np.random):
+    """initialize_all_spec_comps_with_NMF_same (audioModel.py:2179-2222)"""
+    nb = [sc['factor'][0]['FB'].shape[1] for sc in model.spec_comps.values()]
+    W, H = nmf_decomposition(_mono_power(model), nbComps=int(np.max(nb)), niter=niter, rng=rng)
+    order = np.argsort(H.sum(axis=1))[::-1]
+    W, H = W[:, order], H[order]
+    for sc in model.spec_comps.values():
+        n = sc['factor'][0]['FB'].shape[1]
+        sc['factor'][0]['FB'][:] = W[:, :n]
+        sc['factor'][0]['TW'][:] = H[:n]
+    model.renormalize_parameters(rng=rng)

@@ -164,6 +164,9 @@ PATCHES = [
      "bigWindow = np.zeros([int(sizeBigWindow * 2), 1])"),
     ("SeparateLeadStereo/separateLeadFunctions.py", r"bigWindow\[\(sizeBigWindow - lengthSineWindow / 2\.0\):\\\n\s+\(sizeBigWindow \+ lengthSineWindow / 2\.0\)\]",
      "bigWindow[int(sizeBigWindow - lengthSineWindow / 2.0):int(sizeBigWindow + lengthSineWindow / 2.0)]"),
+    # NMF initialisation (audioModel.py:2118-2177): float slice bounds
+    ("audioModel.py", r"ind_start = np\.sum\(nbSpecComps\[:spec_ind\]\)",
+     "ind_start = int(np.sum(nbSpecComps[:spec_ind]))"),
 ]
 
 

@@ -321,6 +321,66 @@ class FASST(object):
         if mask:
             self._restart_tw(mask, order)
 
+    # ---------------------------------------------------------------- NMF init
+    def _mono_power(self):
+        """Channel-averaged power sum_c Re Cx[c, c] / nc (audioModel.py:2150-2158)."""
+        nc = self.audioObject.channels
+        Cx = np.copy(np.real(self.Cx[0]))
+        Cx += np.real(self.Cx[2])
+        Cx /= np.double(nc)
+        return Cx
+
+    def initialize_all_spec_comps_with_NMF(self, sameInitAll=False, **kwargs):
+        """IS-NMF of the mono power initialises FB / TW (audioModel.py:2091-2116);
+        the NMF iterations and the renormalisation run on the GPU."""
+        if sameInitAll:
+            return self.initialize_all_spec_comps_with_NMF_same(**kwargs)
+        return self.initialize_all_spec_comps_with_NMF_indiv(**kwargs)
+
+    def initialize_all_spec_comps_with_NMF_indiv(self, niter=10, updateFreqBasis=True,
+                                                 updateTimeWeight=True, **kwargs):
+        """One NMF over all components, started from the current FB / TW
+        (audioModel.py:2118-2177)."""
+        from .tools.nmf import NMF_decomp_init
+        nbSpecComps = [sc['factor'][0]['FB'].shape[1] for sc in self.spec_comps.values()]
+        total = int(np.sum(nbSpecComps))
+        FBinit = np.zeros([self.nbFreqsSigRepr, total])
+        TWinit = np.zeros([total, self.nbFramesSigRepr])
+        for k, sc in self.spec_comps.items():
+            a = int(np.sum(nbSpecComps[:k]))
+            FBinit[:, a:a + nbSpecComps[k]] = sc['factor'][0]['FB']
+            TWinit[a:a + nbSpecComps[k]] = sc['factor'][0]['TW']
+        W, H = NMF_decomp_init(SX=self._mono_power(), nbComps=total, niter=niter,
+                               verbose=self.verbose, Winit=FBinit, Hinit=TWinit,
+                               updateW=updateFreqBasis, updateH=updateTimeWeight,
+                               device=self.device)
+        for k, sc in self.spec_comps.items():
+            a = int(np.sum(nbSpecComps[:k]))
+            if updateFreqBasis:
+                sc['factor'][0]['FB'] = np.maximum(W[:, a:a + nbSpecComps[k]], eps)
+            if updateTimeWeight:
+                sc['factor'][0]['TW'] = np.maximum(H[a:a + nbSpecComps[k]], eps)
+        self.renormalize_parameters()
+
+    def initialize_all_spec_comps_with_NMF_same(self, niter=10, **kwargs):
+        """One NMF, the same W / H (most energetic first) for every component
+        (audioModel.py:2179-2222)."""
+        from .tools.nmf import NMF_decomposition
+        if not np.all([len(sc['factor']) == 1 for sc in self.spec_comps.values()]):
+            raise NotImplementedError("NMF init not implemented for multi factor models.")
+        nbSpecComps = [sc['factor'][0]['FB'].shape[1] for sc in self.spec_comps.values()]
+        W, H = NMF_decomposition(SX=self._mono_power(), verbose=self.verbose,
+                                 nbComps=int(np.max(nbSpecComps)), niter=niter,
+                                 device=self.device)
+        indexSort = np.argsort(H.sum(axis=1))[::-1]
+        W = W[:, indexSort]
+        H = H[indexSort]
+        for sc in self.spec_comps.values():
+            n = sc['factor'][0]['FB'].shape[1]
+            sc['factor'][0]['FB'][:] = W[:, :n]
+            sc['factor'][0]['TW'][:] = H[:n]
+        self.renormalize_parameters()
+
     # ---------------------------------------------------------------- separation
     def separate_spat_comps(self, dir_results=None, suffix=None):
         """One source per spatial component (audioModel.py:1063-1086)."""

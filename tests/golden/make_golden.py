@@ -400,6 +400,43 @@ def run_wf0():
     print("wf0", {k: np.shape(v) for k, v in out.items()})
 
 
+def run_nmfinit(same):
+    """initialize_all_spec_comps_with_NMF (audioModel.py:2091-2222) on a
+    seeded model, then 2 GEM iterations from that initial state."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    import scipy.io.wavfile as wf
+    import pyfasst.audioModel as am
+    name = "nmfinit_same" if same else "nmfinit_indiv"
+    data = synth_wav(4000, 8000, 77 if same else 78)
+    wav = "/tmp/golden_%s.wav" % name
+    wf.write(wav, 8000, data)
+    np.random.seed(0)
+    m = am.MultiChanNMFConv(wav, nbComps=3, nbNMFComps=4, spatial_rank=2, verbose=0,
+                            iter_num=2, wlen=256, hopsize=64)
+    m.makeItConvolutive()
+    out = {'wav': data, 'fs': np.array(8000)}
+    np.random.seed(5)
+    if same:
+        m.initialize_all_spec_comps_with_NMF(sameInitAll=True, niter=4)
+    else:
+        m.initialize_all_spec_comps_with_NMF(sameInitAll=False, niter=4,
+                                             updateFreqBasis=True, updateTimeWeight=True)
+    for k, comp in m.spec_comps.items():
+        out['init_FB_%d' % k] = np.array(comp['factor'][0]['FB'])
+        out['init_TW_%d' % k] = np.array(comp['factor'][0]['TW'])
+    for j, sc in m.spat_comps.items():
+        out['init_params_%d' % j] = np.array(sc['params'])
+    out['logliks'] = np.real(m.estim_param_a_post_model())
+    for k, comp in m.spec_comps.items():
+        out['final_FB_%d' % k] = np.array(comp['factor'][0]['FB'])
+        out['final_TW_%d' % k] = np.array(comp['factor'][0]['TW'])
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, out['logliks'])
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -423,12 +460,14 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--case":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
-         "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0}.get(
+         "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0, "nmfinit_same": lambda: run_nmfinit(True),
+         "nmfinit_indiv": lambda: run_nmfinit(False)}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
-    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0"] + list(CASES))
+    names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0", "nmfinit_same",
+                              "nmfinit_indiv"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

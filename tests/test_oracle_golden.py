@@ -185,3 +185,29 @@ def test_wf0_dictionaries_golden():
                                      'h3': (2049, 4096, 44100, 30, 0.75)}.items():
         np.testing.assert_array_equal(D.generate_hann_basis(F, nft, fs, numberOfBasis=P, overlap=ov),
                                       g['WGAMMA_' + tag])
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_nmf_init_golden(same):
+    """initialize_all_spec_comps_with_NMF (audioModel.py:2091-2222), then EM."""
+    name = "nmfinit_same" if same else "nmfinit_indiv"
+    g = load(name)
+    x, _ = R.read_scaled(g['wav'])
+    X = [R.stft(x[:, c], np.hanning(256), 64, 256) for c in range(2)]
+    m = R.RefFASST(iter_num=2)
+    m.set_transform(X)
+    np.random.seed(0)
+    R.init_nmf_inst(m, 3, 4, 2)
+    R.make_convolutive(m)
+    np.random.seed(5)
+    if same:
+        R.init_nmf_same(m, niter=4)
+    else:
+        R.init_nmf_indiv(m, niter=4)
+    for k in range(3):
+        np.testing.assert_array_equal(m.spec_comps[k]['factor'][0]['FB'], g['init_FB_%d' % k])
+        np.testing.assert_array_equal(m.spec_comps[k]['factor'][0]['TW'], g['init_TW_%d' % k])
+        np.testing.assert_array_equal(np.array(m.spat_comps[k]['params']), g['init_params_%d' % k])
+    np.testing.assert_array_equal(m.estim_param_a_post_model(), g['logliks'])
+    for k in range(3):
+        np.testing.assert_array_equal(m.spec_comps[k]['factor'][0]['FB'], g['final_FB_%d' % k])
