@@ -167,6 +167,29 @@ PATCHES = [
     # NMF initialisation (audioModel.py:2118-2177): float slice bounds
     ("audioModel.py", r"ind_start = np\.sum\(nbSpecComps\[:spec_ind\]\)",
      "ind_start = int(np.sum(nbSpecComps[:spec_ind]))"),
+    # lead/accompaniment pipeline (SeparateLeadStereoTF.py:959-1897): py2
+    # integer division on numpy ints, np.int, float slice bounds
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"nChunks = totFrames / maxFrames \+ 1",
+     "nChunks = totFrames // maxFrames + 1"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"maxFrames = np\.int\(np\.ceil\(np\.double\(totFrames\)/nChunks\)\)",
+     "maxFrames = int(np.ceil(np.double(totFrames)/nChunks))"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"nChunks = totFrames/maxFrames \n",
+     "nChunks = totFrames//maxFrames \n"),
+    ("SeparateLeadStereo/SIMM/SIMM.py", r"F0Table\[np\.array\(imgYticks\)/chirpPerF0\]",
+     "F0Table[np.array(imgYticks)//chirpPerF0]"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"F0Table\[np\.array\(imgYticks\)/\n(\s+)self\.SIMMParams\['chirpPerF0'\]",
+     r"F0Table[np.array(imgYticks)//\n\1self.SIMMParams['chirpPerF0']"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"np\.ones\(chirpPerF0", "_ones_i(chirpPerF0"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"\neps = 10 \*\* -9\n",
+     "\neps = 10 ** -9\n_ones_i = lambda n, **kw: np.ones(int(n), **kw)  # py2 float sizes\n"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"overlapSamp = wlen - hopsize\n",
+     "overlapSamp = int(wlen - hopsize)\n"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"data = np\.zeros\(\[nuDataLen, 2\], np\.int16\)",
+     "data = np.zeros([int(nuDataLen), 2], np.int16)"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"start = cumulframe - wlen \+ hopsize\n",
+     "start = int(cumulframe - wlen + hopsize)\n"),
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"'stft': self\.stftParams\['windowSizeInSamples'\] / 2,",
+     "'stft': self.stftParams['windowSizeInSamples'] // 2,"),
 ]
 
 

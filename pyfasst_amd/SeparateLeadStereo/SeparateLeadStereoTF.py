@@ -51,32 +51,359 @@ def separate_lead_stfts(SIMMParams, XR, XL, device=None):
     return tuple(outs)
 
 
-class SeparateLeadProcess(object):
-    """Holds the state `writeSeparatedSignals` reads (SeparateLeadStereoTF.py
-    :1762-1871): SIMMParams, stftParams, XR, XL, files, fs, scaleData,
-    dataType, tfrepresentation ('stft' only on this path)."""
+knownTransfos = ['stft', 'hybridcqt', 'minqt', 'cqt', 'mqt']   # SeparateLeadStereoTF.py:33
 
-    def __init__(self, SIMMParams=None, stftParams=None, XR=None, XL=None, files=None,
-                 fs=44100, scaleData=1.0, dataType=np.int16, tfrepresentation='stft',
-                 trackingParams=None, N=None, verbose=False, device=None):
-        self.SIMMParams = SIMMParams
-        self.stftParams = stftParams
-        self.XR, self.XL = XR, XL
-        self.files = files or {}
-        self.fs = fs
-        self.scaleData = scaleData
-        self.dataType = dataType
-        self.tfrepresentation = tfrepresentation
-        self.trackingParams = trackingParams or {'minF0search': None, 'maxF0search': None}
-        if N is not None:
-            self.N = N
-        self.verbose = verbose
+
+class SeparateLeadProcess(object):
+    """Lead / accompaniment separation process (SeparateLeadStereoTF.py:36-1897).
+
+    Built like the reference from a WAV file name and its keyword arguments
+    (:263-540): the STFTs, the KLGLOTT88 source dictionary WF0 and the
+    Hann filter basis are computed at construction; `autoMelSepAndWrite`
+    (:1142-1148) runs the chunked pipeline -- mono SIMM per chunk for HF0,
+    Viterbi melody, stereo SIMM per chunk with the Wiener-mask separation
+    of each chunk, overlap-add of the chunk WAVs.  Every SIMM iteration,
+    STFT / iSTFT, mask, the dictionary synthesis and the Viterbi recursion
+    run on the GPU; chunk bookkeeping and WAV I/O are host-side, as in the
+    reference.  tfrepresentation 'stft' only (the CQT variants feed complex
+    signals into the CQT: NotImplementedError), initHF00 'random' only.
+
+    Addition: with inputAudioFilename=None the state that
+    writeSeparatedSignals / runViterbi read can be given directly
+    (SIMMParams, stftParams, XR, XL, files, fs, scaleData, dataType,
+    trackingParams, N)."""
+
+    def __init__(self, inputAudioFilename=None, windowSize=0.0464, hopsize=None, NFT=None,
+                 nbIter=10, numCompAccomp=40, minF0=39, maxF0=2000, stepNotes=16,
+                 chirpPerF0=1, K_numFilters=4, P_numAtomFilters=30, imageCanvas=None,
+                 wavCanvas=None, progressBar=None, verbose=True, outputDirSuffix='/',
+                 minF0search=None, maxF0search=None, tfrepresentation='stft', cqtfmax=4000,
+                 cqtfmin=50, cqtbins=48, cqtWinFunc=None, cqtAtomHopFactor=0.25,
+                 initHF00='random', freeMemory=True, device=None, SIMMParams=None,
+                 stftParams=None, XR=None, XL=None, files=None, fs=44100, scaleData=1.0,
+                 dataType=np.int16, trackingParams=None, N=None):
         self.device = device
+        self.verbose = verbose
+        if inputAudioFilename is None:
+            self.SIMMParams = SIMMParams
+            self.stftParams = stftParams
+            self.XR, self.XL = XR, XL
+            self.files = files or {}
+            self.fs = fs
+            self.scaleData = scaleData
+            self.dataType = dataType
+            self.tfrepresentation = tfrepresentation
+            self.trackingParams = trackingParams or {'minF0search': None, 'maxF0search': None}
+            if N is not None:
+                self.N = N
+            return
+        import os
+        from ..tools.utils import sqrt_blackmanharris
+        self.files = {}
+        self.SIMMParams = {}
+        self.stftParams = {}
+        tfrepresentation = tfrepresentation.lower()
+        if tfrepresentation not in knownTransfos:
+            raise AttributeError("The desired Time-Freq representation " + tfrepresentation +
+                                 " is not a recognized one.\nPlease choose from " +
+                                 str(knownTransfos))
+        if tfrepresentation != 'stft':
+            raise NotImplementedError("tfrepresentation %r: only 'stft' runs on the GPU path"
+                                      % tfrepresentation)
+        if initHF00 != 'random':
+            raise NotImplementedError("initHF00=%r (per-frame NNLS) is outside the GPU path"
+                                      % initHF00)
+        self.tfrepresentation = tfrepresentation
+        self.stftParams['cqtfmin'] = cqtfmin
+        self.stftParams['cqtfmax'] = cqtfmax
+        self.stftParams['cqtbins'] = cqtbins
+        self.stftParams['cqtWinFunc'] = cqtWinFunc if cqtWinFunc is not None else sqrt_blackmanharris
+        self.stftParams['cqtAtomHopFactor'] = cqtAtomHopFactor
+        self.files['inputAudioFilename'] = str(inputAudioFilename)
+        self.imageCanvas = imageCanvas
+        self.wavCanvas = wavCanvas
+        self.displayEvolution = False
+        if inputAudioFilename[-4:] != ".wav":
+            raise ValueError("File not WAV file? Only WAV format support, for now...")
+        # output files (:352-373)
+        self.files['outputDirSuffix'] = outputDirSuffix
+        self.files['outputDir'] = ('/'.join(self.files['inputAudioFilename'].split('/')[:-1]) +
+                                   '/' + self.files['outputDirSuffix'] + '/')
+        if not os.path.isdir(self.files['outputDir']):
+            os.mkdir(self.files['outputDir'])
+        self.files['pathBaseName'] = (self.files['outputDir'] +
+                                      self.files['inputAudioFilename'].split('/')[-1][:-4])
+        self.files['mus_output_file'] = str(self.files['pathBaseName'] + '_acc.wav')
+        self.files['voc_output_file'] = str(self.files['pathBaseName'] + '_lead.wav')
+        self.files['pitch_output_file'] = str(self.files['pathBaseName'] + '_pitches.txt')
+        # data scaling (:392-410)
+        self.fs, data = wav.read(self.files['inputAudioFilename'])
+        self.scaleData = 1.2 * np.abs(data).max()
+        self.dataType = data.dtype
+        data = np.double(data) / self.scaleData
+        if data.shape[0] == data.size:
+            data = np.vstack([data, data]).T
+            self.numberChannels = 1
+        if data.shape[1] != 2:
+            data = data[:, 0:2]
+            self.numberChannels = data.shape[1]
+        # STFT parameters (:413-429)
+        self.stftParams['windowSizeInSamples'] = slf.nextpow2(np.round(windowSize * self.fs))
+        if hopsize is None:
+            self.stftParams['hopsize'] = self.stftParams['windowSizeInSamples'] / 8.
+        else:
+            self.stftParams['hopsize'] = np.double(hopsize)
+        if NFT is None:
+            self.stftParams['NFT'] = self.stftParams['windowSizeInSamples']
+        else:
+            self.stftParams['NFT'] = NFT
+        self.stftParams['offsets'] = {'stft': self.stftParams['windowSizeInSamples'] // 2,
+                                      'minqt': 0, 'mqt': 0, 'hybridcqt': 0, 'cqt': 0}
+        self.SIMMParams['niter'] = nbIter
+        self.SIMMParams['R'] = numCompAccomp
+        del data
+        self.SIMMParams['minF0'] = minF0
+        self.SIMMParams['maxF0'] = maxF0
+        self.F = self.stftParams['NFT'] // 2 + 1
+        self.SIMMParams['stepNotes'] = stepNotes
+        self.SIMMParams['K'] = K_numFilters
+        self.SIMMParams['P'] = P_numAtomFilters
+        self.SIMMParams['chirpPerF0'] = chirpPerF0
+        self.scopeAllowedHF0 = 4.0 / 1.0
+        self.SIMMParams['initHF00'] = initHF00
+        self.computeWF0()
+        self.SIMMParams['WGAMMA'] = slf.generateHannBasis(
+            numberFrequencyBins=self.F, sizeOfFourier=self.stftParams['NFT'], Fs=self.fs,
+            frequencyScale='linear', numberOfBasis=self.SIMMParams['P'], overlap=.75)
+        self.trackingParams = {'minF0search': self.SIMMParams['minF0'],
+                               'maxF0search': self.SIMMParams['maxF0']}
+        if minF0search is not None:
+            self.trackingParams['minF0search'] = minF0search
+        if maxF0search is not None:
+            self.trackingParams['maxF0search'] = maxF0search
+        self.freeMemory = freeMemory
+
+    # ---------------------------------------------------------------- setup
+    def computeWF0(self):
+        """Source dictionary on the GPU (SeparateLeadStereoTF.py:587-700, the
+        'stft' branch: STFT transform + generate_WF0_TR_chirped)."""
+        from ..tftransforms.stft import STFT
+        self.mqt = STFT(linFTLen=self.stftParams['NFT'],
+                        atomHopFactor=self.stftParams['cqtAtomHopFactor'],
+                        winFunc=self.stftParams['cqtWinFunc'], fs=self.fs, device=self.device)
+        self.SIMMParams['F0Table'], WF0, self.mqt = slf.generate_WF0_TR_chirped(
+            transform=self.mqt, minF0=self.SIMMParams['minF0'], maxF0=self.SIMMParams['maxF0'],
+            stepNotes=self.SIMMParams['stepNotes'], Ot=0.5,
+            perF0=self.SIMMParams['chirpPerF0'], depthChirpInSemiTone=0.5, loadWF0=True,
+            verbose=self.verbose, device=self.device)
+        self.SIMMParams['WF0'] = WF0 / np.sum(WF0, axis=0)
+        self.SIMMParams['NF0'] = self.SIMMParams['F0Table'].size
+        self.F = WF0.shape[0]
+
+    def _read(self):
+        _, data = wav.read(self.files['inputAudioFilename'])
+        return np.double(data) / self.scaleData
+
+    def _stft(self, x, start, stop):
+        return slf.stft(x, fs=self.fs, hopsize=self.stftParams['hopsize'],
+                        window=slf.sinebell(self.stftParams['windowSizeInSamples']),
+                        nfft=self.stftParams['NFT'], start=start, stop=stop,
+                        device=self.device)[0]
+
+    def computeMonoX(self, start=0, stop=None):
+        """max(|STFT(mean of channels)|^2, 1e-8) for frames start:stop (:702-739)."""
+        data = self._read()
+        if len(data.shape) > 1 and data.shape[1] > 1:
+            data = data.mean(axis=1)
+        X = self._stft(data, start, stop)
+        self.F, _ = X.shape
+        return np.maximum(np.abs(X) ** 2, 10 ** -8)
+
+    def computeStereoX(self, start=0, stop=None):
+        """Complex STFTs XR, XL for frames start:stop (:761-841)."""
+        data = self._read()
+        starttime = start * self.stftParams['hopsize']
+        stoptime = stop * self.stftParams['hopsize'] if stop is not None else data.shape[0]
+        self.originalDataLen = stoptime - starttime
+        if len(data.shape) > 1:
+            self.XR = self._stft(data[:, 0], start, stop)
+        else:
+            self.XR = self._stft(data, start, stop)
+        if len(data.shape) > 1 and data.shape[1] > 1:
+            self.XL = self._stft(data[:, 1], start, stop)
+        else:
+            self.XL = self.XR
+        self.F, _ = self.XR.shape
+
+    def computeStereoSX(self, start=0, stop=None):
+        """max(|STFT|^2, 1e-8) of each channel, frames start:stop (:843-917)."""
+        data = self._read()
+        starttime = start * self.stftParams['hopsize']
+        stoptime = stop * self.stftParams['hopsize'] if stop is not None else data.shape[0]
+        self.originalDataLen = stoptime - starttime
+        XR = self._stft(data[:, 0] if len(data.shape) > 1 else data, start, stop)
+        SXR = np.maximum(np.abs(XR) ** 2, 1e-8)
+        if len(data.shape) > 1 and data.shape[1] > 1:
+            SXL = np.maximum(np.abs(self._stft(data[:, 1], start, stop)) ** 2, 1e-8)
+        else:
+            SXL = SXR
+        self.F, _ = SXR.shape
+        return SXR, SXL
+
+    def checkChunkSize(self, maxFrames):
+        """Chunking of the frames (:1880-1897), py2 integer divisions kept."""
+        totFrames = np.int32(self.computeNFrames())
+        nChunks = totFrames // maxFrames + 1
+        if (totFrames - (nChunks - 1) * maxFrames <
+                self.stftParams['windowSizeInSamples'] / self.stftParams['hopsize']):
+            maxFrames = int(np.ceil(np.double(totFrames) / nChunks))
+            nChunks = totFrames // maxFrames
+        return totFrames, nChunks, maxFrames
+
+    # ---------------------------------------------------------------- pipeline
+    def autoMelSepAndWrite(self, maxFrames=1000):
+        """Fully automated melody estimation and separation (:1142-1148)."""
+        self.estimHF0(maxFrames=maxFrames)
+        self.runViterbi()
+        self.initiateHF0WithIndexBestPath()
+        self.estimStereoSIMMParamsWriteSeps(maxFrames=maxFrames)
+
+    def estimHF0(self, R=1, maxFrames=1000):
+        """HF0 of the whole excerpt by mono SIMM on chunks (:959-1072)."""
+        from .SIMM import SIMM
+        totFrames, nChunks, maxFrames = self.checkChunkSize(maxFrames)
+        P = self.SIMMParams
+        P['HF0'] = np.zeros([P['NF0'] * P['chirpPerF0'], totFrames])
+        for n in range(nChunks):
+            start = n * maxFrames
+            stop = np.minimum((n + 1) * maxFrames, totFrames)
+            SX = self.computeMonoX(start=start, stop=stop)
+            HGAMMA, HPHI, HF0, HM, WM, recoError1 = SIMM.SIMM(
+                SX, WF0=P['WF0'], WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
+                numberOfAccompanimentSpectralShapes=R, HGAMMA0=None, HPHI0=None, HF00=None,
+                WM0=None, HM0=None, numberOfIterations=P['niter'], updateRulePower=1.,
+                stepNotes=P['stepNotes'], lambdaHF0=0.0 / (1.0 * SX.max()), alphaHF0=0.9,
+                verbose=self.verbose, F0Table=P['F0Table'], chirpPerF0=P['chirpPerF0'],
+                device=self.device)
+            P['HF0'][:, start:stop] = np.copy(HF0)
+            del SX
+
+    def initiateHF0WithIndexBestPath(self):
+        """HF00: the melody's neighbourhood set to max HF0 (:1321-1368)."""
+        NF0 = self.SIMMParams['NF0']
+        chirpPerF0 = self.SIMMParams['chirpPerF0']
+        stepNotes = self.SIMMParams['stepNotes']
+        HF00 = np.zeros([NF0 * chirpPerF0, self.N])
+        scope = self.scopeAllowedHF0
+        width = int(chirpPerF0 * (2 * np.floor(stepNotes / scope) + 1))
+        dim1index = np.array(np.maximum(np.minimum(
+            np.outer(self.indexBestPath, np.ones(width)) +
+            np.outer(np.ones(self.N), np.arange(-chirpPerF0 * np.floor(stepNotes / scope),
+                                                chirpPerF0 * (np.floor(stepNotes / scope) + 1))),
+            chirpPerF0 * NF0 - 1), 0), dtype=int)
+        dim1index = dim1index[self.indexBestPath != 0, :]
+        dim1index = dim1index.reshape(1, dim1index.size)
+        dim2index = np.outer(np.arange(self.N), np.ones(width, dtype=int))
+        dim2index = dim2index[self.indexBestPath != 0, :]
+        dim2index = dim2index.reshape(1, dim2index.size)
+        HF00[dim1index, dim2index] = self.SIMMParams['HF0'].max()
+        HF00[:, self.indexBestPath == (NF0 - 1)] = 0.0
+        HF00[:, self.indexBestPath == 0] = 0.0
+        self.SIMMParams['HF00'] = HF00
+
+    def estimStereoSIMMParamsWriteSeps(self, maxFrames=1000):
+        """Stereo SIMM per chunk, writing each chunk's separation, then the
+        overlap-add of the chunks (:1370-1467)."""
+        from .SIMM import SIMM
+        totFrames, nChunks, maxFrames = self.checkChunkSize(maxFrames)
+        P = self.SIMMParams
+        P['HGAMMA'] = None
+        for n in range(nChunks):
+            start = n * maxFrames
+            stop = np.minimum((n + 1) * maxFrames, totFrames)
+            SXR, SXL = self.computeStereoSX(start=start, stop=stop)
+            HF00 = np.zeros([P['NF0'] * P['chirpPerF0'], SXR.shape[1]])
+            startinHF00, stopinHF00 = 0, stop - start
+            HF00[:, startinHF00:stopinHF00] = P['HF00'][:, start:stop]
+            (alphaR, alphaL, HGAMMA, HPHI, HF0, betaR, betaL, HM, WM,
+             recoError2) = SIMM.Stereo_SIMM(
+                SXR, SXL, WF0=P['WF0'], WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
+                numberOfAccompanimentSpectralShapes=P['R'], HGAMMA0=P['HGAMMA'], HPHI0=None,
+                HF00=HF00, WM0=None, HM0=None, numberOfIterations=P['niter'],
+                updateRulePower=1.0, stepNotes=P['stepNotes'],
+                lambdaHF0=0.0 / (1.0 * SXR.max()), alphaHF0=0.9, verbose=self.verbose,
+                displayEvolution=False, device=self.device)
+            P['HGAMMA'], P['HPHI'], P['HF0'], P['HM'], P['WM'] = HGAMMA, HPHI, HF0, HM, WM
+            P['alphaR'], P['alphaL'], P['betaR'], P['betaL'] = alphaR, alphaL, betaR, betaL
+            P['HF00'][:, start:stop] = np.copy(HF0[:, startinHF00:stopinHF00])
+            del SXR, SXL, HF00
+            self.computeStereoX(start=start, stop=stop)
+            self.writeSeparatedSignals(suffix='%05d.wav' % n)
+            del self.XR, self.XL
+            if self.freeMemory:
+                for key in ('HM', 'HF0', 'HPHI', 'alphaR', 'alphaL', 'betaR', 'betaL'):
+                    del P[key]
+        self.overlapAddChunks(nChunks=nChunks, suffixIsSUIMM='.wav')
+
+    def overlapAddChunks(self, nChunks, suffixIsSUIMM='.wav'):
+        """Concatenate the chunk WAVs with their overlaps (:1469-1583): for the
+        STFT the overlap is rectangular (ones); int16 arithmetic as the
+        reference's."""
+        import os
+        wlen = self.stftParams['windowSizeInSamples']
+        offsetTF = self.stftParams['offsets'][self.tfrepresentation]
+        hopsize = self.stftParams['hopsize']
+        overlapSamp = int(wlen - hopsize)
+        overlapFunc = np.ones(overlapSamp)
+        nuDataLen = int(self.totFrames * hopsize + 2 * wlen)
+        for key in ('voc_output_file', 'mus_output_file'):
+            data = np.zeros([nuDataLen, 2], np.int16)
+            cumulframe = 0
+            for n in range(nChunks):
+                fname = self.files[key][:-4] + '%05d%s' % (n, suffixIsSUIMM)
+                _, datatmp = wav.read(fname)
+                datatype = type(datatmp[0][0])
+                if n == 0 and nChunks != 1:
+                    datatmp[-overlapSamp:, 0] = datatype(datatmp[-overlapSamp:, 0] * overlapFunc)
+                    datatmp[-overlapSamp:, 1] = datatype(datatmp[-overlapSamp:, 1] * overlapFunc)
+                    lendatatmp = datatmp.shape[0] - offsetTF
+                    data[:lendatatmp, :] = np.copy(datatmp[offsetTF:, :])
+                    cumulframe = lendatatmp
+                elif nChunks != 1:
+                    if n != nChunks - 1:
+                        datatmp[-overlapSamp:, 0] = datatype(datatmp[-overlapSamp:, 0] *
+                                                             overlapFunc)
+                        datatmp[-overlapSamp:, 1] = datatype(datatmp[-overlapSamp:, 1] *
+                                                             overlapFunc)
+                    datatmp[:overlapSamp, 0] = datatype(datatmp[:overlapSamp, 0] *
+                                                        overlapFunc[::-1])
+                    datatmp[:overlapSamp, 1] = datatype(datatmp[:overlapSamp, 1] *
+                                                        overlapFunc[::-1])
+                    start = int(cumulframe - wlen + hopsize)
+                    lendatatmp = datatmp.shape[0]
+                    stop = start + lendatatmp
+                    data[start:stop, :] += datatmp
+                    cumulframe = stop
+                else:
+                    lendatatmp = datatmp.shape[0] - offsetTF
+                    data[:lendatatmp] = datatmp[offsetTF:, :]
+                os.remove(fname)
+            wav.write(self.files[key][:-4] + suffixIsSUIMM, self.fs, data[:self.lengthData, :])
 
     def computeNFrames(self):
-        """Number of frames; here the caller provides N (or HF0 defines it)."""
+        """Total number of frames (:741-759); in the state-injection mode the
+        caller provides N (or HF0 defines it)."""
+        if 'inputAudioFilename' in self.files:
+            if not hasattr(self, 'totFrames'):
+                _, data = wav.read(self.files['inputAudioFilename'])
+                self.lengthData = data.shape[0]
+                self.totFrames = np.int32(np.ceil((self.lengthData - 0) /
+                                                  self.stftParams['hopsize'] + 1) + 1)
+                self.N = self.totFrames
+            return self.totFrames
         if not hasattr(self, 'N'):
             self.N = np.asarray(self.SIMMParams['HF0']).shape[1]
+        return self.N
 
     def runViterbi(self):
         """Melody line by Viterbi decoding of HF0 (SeparateLeadStereoTF.py:1150-1319)."""

@@ -12,9 +12,9 @@ import numpy as np
 
 from .. import _lib
 from .._lib import check, dptr, lib
-from ..tools.utils import sinebell
+from ..tools.utils import nextpow2, sinebell
 
-__all__ = ["sinebell", "stft", "istft", "generate_WF0_TR_chirped", "generateHannBasis"]
+__all__ = ["nextpow2", "sinebell", "stft", "istft", "generate_WF0_TR_chirped", "generateHannBasis"]
 
 
 def _dev(device):

@@ -437,6 +437,56 @@ def run_nmfinit(same):
     print(name, out['logliks'])
 
 
+def run_pipeline():
+    """The full lead/accompaniment pipeline SeparateLeadProcess(...)
+    .autoMelSepAndWrite(maxFrames) (SeparateLeadStereoTF.py:263-540,
+    1142-1148: chunked mono SIMM -> Viterbi melody -> chunked stereo SIMM with
+    per-chunk Wiener masks -> overlap-add of the chunk WAVs) on a short
+    seeded stereo signal, 3 chunks.  The Cython tracker is called with its
+    5-argument signature, so it is served by the reference's pure-Python
+    twin (tracking.py) on the first NF0 states, as _tracking.pyx does."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import shutil
+    import numpy as np
+    import scipy.io.wavfile as wf
+    from pyfasst.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    from pyfasst.SeparateLeadStereo.tracking import tracking as TR
+
+    def tracker(S_, N_, logD, prior, logT, verbose=False):
+        return TR.viterbiTrackingArray(logD[:S_, :N_], prior[:S_], logT[:S_, :S_])
+    SL.viterbiTrackingArray = tracker
+    work = "/tmp/golden_pipeline"
+    shutil.rmtree(work, ignore_errors=True)
+    os.makedirs(work)
+    os.chdir(work)
+    rs = np.random.RandomState(61)
+    fs, n = 8000, 9000
+    t = np.arange(n) / float(fs)
+    f0 = 220 * 2 ** (np.floor(t * 2) / 12.)                 # a stepped melody
+    lead = sum(np.sin(2 * np.pi * h * np.cumsum(f0) / fs) / h for h in range(1, 8))
+    acc = np.convolve(rs.randn(n), np.ones(9) / 9., mode='same') * 0.7
+    x = np.stack([0.7 * lead + 0.4 * acc, 0.5 * lead + 0.6 * np.roll(acc, 5)], axis=1)
+    x = (x / np.abs(x).max() * 12000).astype(np.int16)
+    wav = os.path.join(work, "mix.wav")
+    wf.write(wav, fs, x)
+    np.random.seed(3)
+    proc = SL.SeparateLeadProcess(wav, windowSize=0.0464, nbIter=3, numCompAccomp=6, minF0=100,
+                                  maxF0=800, stepNotes=4, K_numFilters=3, P_numAtomFilters=10,
+                                  verbose=False, outputDirSuffix='out')
+    proc.autoMelSepAndWrite(maxFrames=60)
+    out = {'wav': x, 'fs': np.array(fs), 'WF0': proc.SIMMParams['WF0'],
+           'WGAMMA': proc.SIMMParams['WGAMMA'], 'F0Table': proc.SIMMParams['F0Table'],
+           'indexBestPath': np.array(proc.indexBestPath), 'freqMelody': np.array(proc.freqMelody),
+           'HF00': proc.SIMMParams['HF00'], 'totFrames': np.array(proc.totFrames),
+           'lead': wf.read(proc.files['voc_output_file'])[1],
+           'acc': wf.read(proc.files['mus_output_file'])[1],
+           'pitches': np.loadtxt(proc.files['pitch_output_file'])}
+    np.savez_compressed(os.path.join(HERE, "pipeline.npz"), **out)
+    print("pipeline", {k: np.shape(v) for k, v in out.items()})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -461,13 +511,13 @@ if __name__ == "__main__":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
          "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0, "nmfinit_same": lambda: run_nmfinit(True),
-         "nmfinit_indiv": lambda: run_nmfinit(False)}.get(
+         "nmfinit_indiv": lambda: run_nmfinit(False), "pipeline": run_pipeline}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
     names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0", "nmfinit_same",
-                              "nmfinit_indiv"] + list(CASES))
+                              "nmfinit_indiv", "pipeline"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])
