@@ -4,17 +4,25 @@
 //   opA[m][k] = TA ? A[k*lda + m] : A[m*lda + k]
 //   opB[k][n] = TB ? B[n*ldb + k] : B[k*ldb + n]
 //
-// 64x64 block tile, BK = 16, 4 waves of 32x32 (2x2 v_mfma_f64_16x16x4f64
-// tiles each).  A and B tiles are staged k-major in LDS (row pitch 80
-// doubles: the two 16-lane row groups of a ds_read_b64 half-wave land on
-// disjoint banks).  Split-K along gridDim.z writes partial C slabs
-// (C + z*slab) that k_gemm_reduce sums in fixed order (deterministic).
+// Block = 4 waves as a WG_M x WG_N grid (2 x 2, or 1 x 4 / 4 x 1 for the
+// skinny R = 40 accompaniment GEMMs); a wave owns a (16 WT_M) x (16 WT_N)
+// tile of every C_b as WT_M x WT_N x NB v_mfma_f64_16x16x4f64 accumulators
+// (<= 16, i.e. <= 64 doubles per lane), so the block tile is
+// BM = 16 WG_M WT_M by BN = 16 WG_N WT_N per operand.  K advances in chunks of BK = 16 staged k-major in LDS, double
+// buffered: the next chunk's global loads are in flight in registers while
+// the MFMAs consume the current chunk, then land in the other LDS buffer
+// (one barrier per chunk).  LDS row pitches are 16 mod 32 doubles (gpitch).
+// Split-K along gridDim.z writes partial C slabs (C + z*slab) that
+// k_gemm_reduce sums in fixed order (deterministic).
 #pragma once
 #include "fasst_common.h"
 
 namespace fasst {
 
-constexpr int kGBM = 64, kGBN = 64, kGBK = 16, kGLD = 80;
+constexpr int kGBK = 16;
+// LDS row pitch (doubles) for a tile width x: == 16 (mod 32), so the two
+// 16-lane row groups of a ds_read_b64 half-wave land on disjoint banks
+constexpr int gpitch(int x) { return x + ((16 - x % 32) + 32) % 32; }
 
 struct GemmArgs {
   const double *A;
@@ -30,90 +38,139 @@ __device__ __forceinline__ fasst::d4 gmfma(double a, double b, fasst::d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <bool TA, bool TB, int NB>
-__global__ __launch_bounds__(256) void k_gemm(const GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) double sA[kGBK * kGLD];
-  __shared__ __attribute__((aligned(16))) double sB[NB][kGBK * kGLD];
+template <bool TA, bool TB, int NB, int WGM, int WTM, int WTN>
+__global__ __launch_bounds__(256, 2) void k_gemm(const GemmArgs g) {
+  constexpr int WGN = 4 / WGM;
+  static_assert(WGM * WGN == 4 && NB * WTM * WTN <= 16, "wave grid / accumulator budget");
+  constexpr int BM = 16 * WGM * WTM, BN = 16 * WGN * WTN;
+  constexpr int PA = gpitch(BM), PB = gpitch(BN);        // LDS row pitches (doubles)
+  constexpr int LA = kGBK * BM / 256, LB = NB * kGBK * BN / 256;  // loads per thread
+  static_assert(kGBK * BM % 256 == 0 && NB * kGBK * BN % 256 == 0, "tile / thread mismatch");
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double *sA0 = smem, *sB0 = smem + kGBK * PA;
+  double *sA1 = sB0 + NB * kGBK * PB, *sB1 = sA1 + kGBK * PA;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fl = lane & 15, tq = lane >> 4;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.y * kGBM, n0 = blockIdx.x * kGBN;
+  const int wm = wv / WGN, wn = wv % WGN;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int kb = blockIdx.z * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
-  fasst::d4 acc[NB][2][2];
+  fasst::d4 acc[NB][WTM][WTN];
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WTM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[b][i][j] = fasst::d4{0.0, 0.0, 0.0, 0.0};
+      for (int j = 0; j < WTN; ++j) acc[b][i][j] = fasst::d4{0.0, 0.0, 0.0, 0.0};
 
-  for (int k0 = kb; k0 < ke; k0 += kGBK) {
-    // stage A tile as sA[k][m]
+  double ra[LA], rb[LB];
+  // global -> registers for the chunk starting at k0 (coalesced along the
+  // contiguous dimension of each operand, zero outside the matrices)
+  auto gload = [&](int k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < LA; ++q) {
       const int idx = tid + 256 * q;
       int k, m;
       if (TA) {
-        k = idx >> 6;
-        m = idx & 63;
+        k = idx / BM;
+        m = idx % BM;
       } else {
-        m = idx >> 4;
-        k = idx & 15;
+        m = idx / kGBK;
+        k = idx % kGBK;
       }
       const int gm = m0 + m, gk = k0 + k;
-      double v = 0.0;
-      if (gm < g.M && gk < ke) v = TA ? g.A[(size_t)gk * g.lda + gm] : g.A[(size_t)gm * g.lda + gk];
-      sA[k * kGLD + m] = v;
+      ra[q] = (gm < g.M && gk < ke) ? (TA ? g.A[(size_t)gk * g.lda + gm] : g.A[(size_t)gm * g.lda + gk])
+                                    : 0.0;
     }
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int idx = tid + 256 * q;
-        int k, n;
-        if (TB) {
-          n = idx >> 4;
-          k = idx & 15;
-        } else {
-          k = idx >> 6;
-          n = idx & 63;
-        }
-        const int gn = n0 + n, gk = k0 + k;
-        double v = 0.0;
-        if (gn < g.N && gk < ke)
-          v = TB ? g.B[b][(size_t)gn * g.ldb + gk] : g.B[b][(size_t)gk * g.ldb + gn];
-        sB[b][k * kGLD + n] = v;
+    for (int q = 0; q < LB; ++q) {
+      const int idx = tid + 256 * q;
+      const int b = idx / (kGBK * BN), r = idx % (kGBK * BN);
+      int k, n;
+      if (TB) {
+        n = r / kGBK;
+        k = r % kGBK;
+      } else {
+        k = r / BN;
+        n = r % BN;
       }
-    __syncthreads();
+      const int gn = n0 + n, gk = k0 + k;
+      const double *Bb = g.B[b];
+      rb[q] = (gn < g.N && gk < ke) ? (TB ? Bb[(size_t)gn * g.ldb + gk] : Bb[(size_t)gk * g.ldb + gn])
+                                    : 0.0;
+    }
+  };
+  auto sstore = [&](double *sA, double *sB) {
+#pragma unroll
+    for (int q = 0; q < LA; ++q) {
+      const int idx = tid + 256 * q;
+      int k, m;
+      if (TA) {
+        k = idx / BM;
+        m = idx % BM;
+      } else {
+        m = idx / kGBK;
+        k = idx % kGBK;
+      }
+      sA[k * PA + m] = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      const int idx = tid + 256 * q;
+      const int b = idx / (kGBK * BN), r = idx % (kGBK * BN);
+      int k, n;
+      if (TB) {
+        n = r / kGBK;
+        k = r % kGBK;
+      } else {
+        k = r / BN;
+        n = r % BN;
+      }
+      sB[b * kGBK * PB + k * PB + n] = rb[q];
+    }
+  };
+
+  const int nch = (ke - kb + kGBK - 1) / kGBK;
+  if (nch > 0) {
+    gload(kb);
+    sstore(sA0, sB0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const bool odd = c & 1;
+    const double *sA = odd ? sA1 : sA0;
+    const double *sB = odd ? sB1 : sB0;
+    if (c + 1 < nch) gload(kb + (c + 1) * kGBK);
 #pragma unroll
     for (int kk = 0; kk < kGBK / 4; ++kk) {
-      const int kr = (4 * kk + tq) * kGLD;
-      const double a0 = sA[kr + wm * 32 + fl];
-      const double a1 = sA[kr + wm * 32 + 16 + fl];
+      const int kr = 4 * kk + tq;
+      double a[WTM];
+#pragma unroll
+      for (int i = 0; i < WTM; ++i) a[i] = sA[kr * PA + wm * 16 * WTM + i * 16 + fl];
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        const double b0 = sB[b][kr + wn * 32 + fl];
-        const double b1 = sB[b][kr + wn * 32 + 16 + fl];
-        acc[b][0][0] = gmfma(a0, b0, acc[b][0][0]);
-        acc[b][0][1] = gmfma(a0, b1, acc[b][0][1]);
-        acc[b][1][0] = gmfma(a1, b0, acc[b][1][0]);
-        acc[b][1][1] = gmfma(a1, b1, acc[b][1][1]);
+#pragma unroll
+        for (int j = 0; j < WTN; ++j) {
+          const double bv = sB[b * kGBK * PB + kr * PB + wn * 16 * WTN + j * 16 + fl];
+#pragma unroll
+          for (int i = 0; i < WTM; ++i) acc[b][i][j] = gmfma(a[i], bv, acc[b][i][j]);
+        }
       }
     }
+    if (c + 1 < nch) sstore(odd ? sA0 : sA1, odd ? sB0 : sB1);
     __syncthreads();
   }
   const size_t zoff = (size_t)blockIdx.z * g.slab;
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WTM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < WTN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 32 + i * 16 + tq + 4 * r;
-          const int col = n0 + wn * 32 + j * 16 + fl;
+          const int row = m0 + wm * 16 * WTM + i * 16 + tq + 4 * r;
+          const int col = n0 + wn * 16 * WTN + j * 16 + fl;
           if (row < g.M && col < g.N) g.C[b][zoff + (size_t)row * g.ldc + col] = acc[b][i][j][r];
         }
 }
@@ -128,7 +185,7 @@ __global__ void k_gemm_reduce(const double *__restrict__ part, int nz, size_t sl
 struct GemmPlan {
   int nz = 1, kchunk = 0;
 };
-GemmPlan gemm_plan(int M, int N, int K);
+GemmPlan gemm_plan(int M, int N, int K, int NB);
 template <bool TA, bool TB, int NB>
 int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ldb, double *const *C,
          int ldc, int M, int N, int K, double *work);

@@ -17,22 +17,86 @@ __global__ void k_gemm_reduce(const double *__restrict__ part, int nz, size_t sl
   }
 }
 
-GemmPlan gemm_plan(int M, int N, int K) {
+// tile shape per operand count: a WG_M x (4 / WG_M) wave grid of WT_M x WT_N
+// MFMA tiles per wave per operand, at most 16 accumulators per wave.  The
+// R = 40 accompaniment GEMMs (M or N <= 48) take a 48-wide single-wave strip
+// so only the 40 -> 48 pad of the MFMA rows is wasted.
+struct TileShape {
+  int wgm, wtm, wtn;
+};
+static TileShape tile_shape(int M, int N, int NB) {
+  if (NB == 1) {
+    if (M <= 48) return {1, 3, 2};
+    if (N <= 48) return {4, 2, 3};
+    return {2, 4, 4};
+  }
+  if (NB == 2) {
+    if (M <= 48) return {1, 3, 2};
+    if (M <= 64) return {2, 2, 4};
+    return {2, 4, 2};
+  }
+  if (M <= 48) return {1, 3, 1};
+  return {2, 2, 2};
+}
+
+static void tile_dims(const TileShape &t, int &BM, int &BN) {
+  BM = 16 * t.wgm * t.wtm;
+  BN = 16 * (4 / t.wgm) * t.wtn;
+}
+
+// split K until the grid holds >= 1024 blocks (4 per CU), chunks >= 64
+GemmPlan gemm_plan(int M, int N, int K, int NB) {
   GemmPlan p;
-  const long tiles = (long)((M + kGBM - 1) / kGBM) * ((N + kGBN - 1) / kGBN);
+  int BM, BN;
+  tile_dims(tile_shape(M, N, NB), BM, BN);
+  const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int nz = 1;
-  while (tiles * nz < 512 && K / (nz * 2) >= 256) nz *= 2;
-  p.nz = nz;
+  while (tiles * nz < 1024 && K / (nz * 2) >= 64) nz *= 2;
   p.kchunk = ((K + nz - 1) / nz + kGBK - 1) / kGBK * kGBK;
   p.nz = (K + p.kchunk - 1) / p.kchunk;
   if (p.nz < 1) p.nz = 1;
   return p;
 }
 
+template <bool TA, bool TB, int NB, int WGM, int WTM, int WTN>
+static int launch_gemm(hipStream_t s, const GemmArgs &g, int nz) {
+  constexpr int BM = 16 * WGM * WTM, BN = 16 * (4 / WGM) * WTN;
+  const size_t smem = 2 * (size_t)kGBK * (gpitch(BM) + NB * gpitch(BN)) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    if (smem > 64 * 1024)
+      FASST_HIP(hipFuncSetAttribute((const void *)k_gemm<TA, TB, NB, WGM, WTM, WTN>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    attr = true;
+  }
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, nz);
+  k_gemm<TA, TB, NB, WGM, WTM, WTN><<<grid, 256, smem, s>>>(g);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+// dispatch to the instantiations tile_shape can return for this NB
+template <bool TA, bool TB, int NB>
+static int launch_shape(hipStream_t s, const GemmArgs &g, int nz) {
+  const TileShape t = tile_shape(g.M, g.N, NB);
+  if constexpr (NB == 1) {
+    if (t.wgm == 1) return launch_gemm<TA, TB, NB, 1, 3, 2>(s, g, nz);
+    if (t.wgm == 4) return launch_gemm<TA, TB, NB, 4, 2, 3>(s, g, nz);
+    return launch_gemm<TA, TB, NB, 2, 4, 4>(s, g, nz);
+  } else if constexpr (NB == 2) {
+    if (t.wgm == 1) return launch_gemm<TA, TB, NB, 1, 3, 2>(s, g, nz);
+    if (t.wtm == 2) return launch_gemm<TA, TB, NB, 2, 2, 4>(s, g, nz);
+    return launch_gemm<TA, TB, NB, 2, 4, 2>(s, g, nz);
+  } else {
+    if (t.wgm == 1) return launch_gemm<TA, TB, NB, 1, 3, 1>(s, g, nz);
+    return launch_gemm<TA, TB, NB, 2, 2, 2>(s, g, nz);
+  }
+}
+
 template <bool TA, bool TB, int NB>
 int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ldb, double *const *C,
          int ldc, int M, int N, int K, double *work) {
-  GemmPlan p = gemm_plan(M, N, K);
+  GemmPlan p = gemm_plan(M, N, K, NB);
   GemmArgs g;
   g.A = A;
   g.lda = lda;
@@ -49,10 +113,7 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
       g.B[b] = B[b];
       g.C[b] = C[b];
     }
-    dim3 grid((N + kGBN - 1) / kGBN, (M + kGBM - 1) / kGBM, 1);
-    k_gemm<TA, TB, NB><<<grid, 256, 0, s>>>(g);
-    FASST_LAUNCH_CHECK();
-    return FASST_OK;
+    return launch_shape<TA, TB, NB>(s, g, 1);
   }
   // split-K into work slabs laid out [NB][nz][M][N] (ldc = N)
   const size_t slab = (size_t)M * N;
@@ -62,9 +123,8 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
     g.B[b] = B[b];
     g.C[b] = work + (size_t)b * p.nz * slab;
   }
-  dim3 grid((N + kGBN - 1) / kGBN, (M + kGBM - 1) / kGBM, p.nz);
-  k_gemm<TA, TB, NB><<<grid, 256, 0, s>>>(g);
-  FASST_LAUNCH_CHECK();
+  int st = launch_shape<TA, TB, NB>(s, g, p.nz);
+  if (st) return st;
   for (int b = 0; b < NB; ++b) {
     if (ldc == N) {
       k_gemm_reduce<<<(int)std::min<size_t>((slab + 255) / 256, 4096), 256, 0, s>>>(
@@ -78,7 +138,7 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
 }
 
 size_t gemm_workspace(int M, int N, int K, int NB) {
-  GemmPlan p = gemm_plan(M, N, K);
+  GemmPlan p = gemm_plan(M, N, K, NB);
   return p.nz > 1 ? (size_t)NB * p.nz * M * N : 0;
 }
 

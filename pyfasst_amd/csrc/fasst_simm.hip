@@ -131,6 +131,182 @@ __global__ void k_simm_xy(const double *__restrict__ h, const double *__restrict
   }
 }
 
+// k_simm_xy's operands for one element (both channels' formulas in one place)
+template <bool ST>
+__device__ __forceinline__ void xy_of(double hv, double sx, double &x, double &y) {
+  y = 1.0 / fmax(hv, kSimmEps);
+  x = ST ? sx / fmax(hv * hv, kSimmEps) : (y * sx) / fmax(hv, kSimmEps);
+}
+
+// Skinny accompaniment products with k_simm_xy fused into the operand loads
+// (R <= 48 rows of WM / HM padded to three 16-row MFMA tiles).  Operand q of
+// the NO = 2 (mono) or 4 (stereo) operands is {X_R, Y_R, X_L, Y_L}[q].
+//
+// k_simm_wmt_xy:  out_q[r][n] = sum_f WM[f][r] T_q[f][n]  (the HM and beta
+//   numerators, SIMM.py:747-756, :911-919).  Wave = 16 frames x all R rows;
+//   lane (fl, tq) streams T at (f = k0 + 4s + tq, n = n0 + fl): every load
+//   instruction reads four 128-byte row segments.  Split-K over f along
+//   gridDim.z into out + z*slab, [q][R][N] per slab.
+template <bool ST>
+__global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(
+    const double *__restrict__ WM, const double *__restrict__ hR, const double *__restrict__ SXR,
+    const double *__restrict__ hL, const double *__restrict__ SXL, double *__restrict__ out,
+    size_t slab, int F, int N, int R, int kchunk) {
+  constexpr int NC = ST ? 2 : 1, NO = 2 * NC;
+  const int lane = threadIdx.x & 63, fl = lane & 15, tq = lane >> 4;
+  const int n = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + fl;
+  const int kb = blockIdx.z * kchunk, ke = min(F, kb + kchunk);
+  const bool nin = n < N;
+  const double *hs[2] = {hR, hL}, *ss[2] = {SXR, SXL};
+  d4 acc[NO][3];
+#pragma unroll
+  for (int q = 0; q < NO; ++q)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
+  double hv[ST ? 1 : 2][NC][4], sv[ST ? 1 : 2][NC][4];
+  auto load = [&](int buf, int k0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int f = k0 + 4 * s + tq;
+      const bool ok = nin && f < ke;
+      const size_t idx = (size_t)f * N + n;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        hv[buf][c][s] = ok ? hs[c][idx] : 0.0;
+        sv[buf][c][s] = ok ? ss[c][idx] : 0.0;
+      }
+    }
+  };
+  auto compute = [&](int buf, int k0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int f = k0 + 4 * s + tq;
+      double a[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = i * 16 + fl;
+        a[i] = (f < ke && r < R) ? WM[(size_t)f * R + r] : 0.0;  // zero rows outside [kb, ke)
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        double x, y;
+        xy_of<ST>(hv[buf][c][s], sv[buf][c][s], x, y);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          acc[2 * c][i] = gmfma(a[i], x, acc[2 * c][i]);
+          acc[2 * c + 1][i] = gmfma(a[i], y, acc[2 * c + 1][i]);
+        }
+      }
+    }
+  };
+  if constexpr (ST) {  // 48 accumulators: no room for a second load buffer
+    for (int k0 = kb; k0 < ke; k0 += 16) {
+      load(0, k0);
+      compute(0, k0);
+    }
+  } else {  // next chunk's loads in flight under the current chunk's MFMAs
+    int k0 = kb;
+    if (k0 < ke) load(0, k0);
+    for (; k0 < ke; k0 += 32) {
+      if (k0 + 16 < ke) load(1, k0 + 16);
+      compute(0, k0);
+      if (k0 + 16 >= ke) break;
+      if (k0 + 32 < ke) load(0, k0 + 32);
+      compute(1, k0 + 16);
+    }
+  }
+  if (!nin) return;
+  double *o = out + blockIdx.z * slab;
+#pragma unroll
+  for (int q = 0; q < NO; ++q)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + tq + 4 * r;
+        if (row < R) o[((size_t)q * R + row) * N + n] = acc[q][i][r];
+      }
+}
+
+// k_simm_xy_hmt:  out_q[f][r] = sum_n T_q[f][n] HM[r][n]  (the WM numerators,
+//   SIMM.py:828-845).  Wave = 16 frequency rows x all R columns.  The frame
+//   sum is permuted within each 32-frame chunk: lane (fl, tq) owns frames
+//   kc + tq + 4 j, j < 8, of row f = fl (every load instruction reads 32
+//   contiguous bytes of 16 rows); HM's chunk [48][32] is shared by the
+//   block's 4 waves through LDS (pitch 34: the half-wave's (fl, tq) pairs hit
+//   32 distinct bank pairs).  Split-K over frames along gridDim.z, [q][F][R] per slab.
+template <bool ST>
+__global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(
+    const double *__restrict__ HM, const double *__restrict__ hR, const double *__restrict__ SXR,
+    const double *__restrict__ hL, const double *__restrict__ SXL, double *__restrict__ out,
+    size_t slab, int F, int N, int R, int kchunk) {
+  constexpr int NC = ST ? 2 : 1, NO = 2 * NC, KC = 32, PH = KC + 2;
+  __shared__ double sH[48 * PH];
+  const int tid = threadIdx.x, lane = tid & 63, fl = lane & 15, tq = lane >> 4;
+  const int f = blockIdx.y * 64 + (tid >> 6) * 16 + fl;
+  const int kb = blockIdx.z * kchunk, ke = min(N, kb + kchunk);
+  const bool fin = f < F;
+  const double *hs[2] = {hR, hL}, *ss[2] = {SXR, SXL};
+  d4 acc[NO][3];
+#pragma unroll
+  for (int q = 0; q < NO; ++q)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int kc = kb; kc < ke; kc += KC) {
+    double hv[NC][8], sv[NC][8];
+    const size_t base = (size_t)f * N + kc + tq;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = fin && kc + tq + 4 * j < ke;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        hv[c][j] = ok ? hs[c][base + 4 * j] : 0.0;
+        sv[c][j] = ok ? ss[c][base + 4 * j] : 0.0;
+      }
+    }
+    double hm[6];  // 48 x 32 chunk of HM, zero outside [0, R) x [kc, ke)
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int e = tid + 256 * t, r = e / KC, k = e % KC;
+      hm[t] = (r < R && kc + k < ke) ? HM[(size_t)r * N + kc + k] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int e = tid + 256 * t;
+      sH[(e / KC) * PH + e % KC] = hm[t];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      double b[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) b[i] = sH[(i * 16 + fl) * PH + tq + 4 * j];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        double x, y;
+        xy_of<ST>(hv[c][j], sv[c][j], x, y);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          acc[2 * c][i] = gmfma(x, b[i], acc[2 * c][i]);
+          acc[2 * c + 1][i] = gmfma(y, b[i], acc[2 * c + 1][i]);
+        }
+      }
+    }
+  }
+  double *o = out + blockIdx.z * slab;
+#pragma unroll
+  for (int q = 0; q < NO; ++q)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = blockIdx.y * 64 + (tid >> 6) * 16 + tq + 4 * r;
+        const int col = i * 16 + fl;
+        if (row < F && col < R) o[((size_t)q * F + row) * R + col] = acc[q][i][r];
+      }
+}
+
 // HPHI numerator/denominator: out[m][n] = sum_f WPHI[f][m] * {num,den}(f, n),
 // num/den built on the fly from Z = SF0 (:688-694).  Block: 256 frames x one
 // f-chunk; partials [chunk][2][K][N].
@@ -506,6 +682,98 @@ int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, dou
   return gemm<false, false, 1>(c->stream, A, lda, Bs, ldb, Cs, ldc, M, N, K, c->gwork.p);
 }
 
+// split of the fused skinny products (k_simm_wmt_xy / k_simm_xy_hmt): a
+// grid of >= 1024 (resp. 512) blocks, K chunks of >= 64 (256) rows
+struct SkinnySplit {
+  int nz, kchunk;
+};
+static SkinnySplit wmt_split(int F, int N) {
+  const long bx = (N + 63) / 64;
+  int nz = 1;
+  while (bx * nz < 1024 && F / (2 * nz) >= 64) nz *= 2;
+  const int kchunk = ((F + nz - 1) / nz + 15) / 16 * 16;
+  return {(F + kchunk - 1) / kchunk, kchunk};
+}
+static SkinnySplit hmt_split(int F, int N) {
+  const long by = (F + 63) / 64;
+  int nz = 1;
+  while (by * nz < 512 && N / (2 * nz) >= 256) nz *= 2;
+  const int kchunk = ((N + nz - 1) / nz + 31) / 32 * 32;
+  return {(N + kchunk - 1) / kchunk, kchunk};
+}
+static size_t skinny_workspace(int F, int N, int R, int stereo) {
+  if (R > 48) return 0;
+  const size_t no = stereo ? 4 : 2;
+  return std::max((size_t)wmt_split(F, N).nz * no * R * N, (size_t)hmt_split(F, N).nz * no * F * R);
+}
+
+void reduce_slabs(simm_ctx *c, int no, int nz, size_t n, double *const *dst) {
+  for (int q = 0; q < no; ++q)
+    k_gemm_reduce<<<(int)std::min<size_t>((n + 255) / 256, 4096), 256, 0, c->stream>>>(
+        c->gwork.p + (size_t)q * n, nz, (size_t)no * n, dst[q], n);
+}
+
+// dst[q] (R x N) = WM^T {X_R, Y_R, X_L, Y_L}[q] from the current model
+int wmt_xy(simm_ctx *c, double *const *dst) {
+  const int F = c->F, N = c->N, R = c->R, no = c->stereo ? 4 : 2;
+  if (R > 48) {  // wide accompaniment dictionaries: materialise X, Y, general GEMM
+    k_simm_xy<<<egrid((size_t)F * N), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p,
+                                                           (size_t)F * N, c->stereo);
+    if (c->stereo)
+      k_simm_xy<<<egrid((size_t)F * N), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p,
+                                                             (size_t)F * N, c->stereo);
+    const double *Bs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
+    return c->stereo ? gemm<true, false, 4>(c->stream, c->WM.p, R, Bs, N, dst, N, R, N, F, c->gwork.p)
+                     : gemm<true, false, 2>(c->stream, c->WM.p, R, Bs, N, dst, N, R, N, F, c->gwork.p);
+  }
+  const SkinnySplit sp = wmt_split(F, N);
+  const size_t slab = (size_t)no * R * N;
+  dim3 grid((N + 63) / 64, 1, sp.nz);
+  if (c->stereo)
+    k_simm_wmt_xy<true><<<grid, 256, 0, c->stream>>>(c->WM.p, c->hR.p, c->SXR.p, c->hL.p, c->SXL.p,
+                                                      c->gwork.p, slab, F, N, R, sp.kchunk);
+  else
+    k_simm_wmt_xy<false><<<grid, 256, 0, c->stream>>>(c->WM.p, c->hR.p, c->SXR.p, nullptr, nullptr,
+                                                       c->gwork.p, slab, F, N, R, sp.kchunk);
+  FASST_LAUNCH_CHECK();
+  reduce_slabs(c, no, sp.nz, (size_t)R * N, dst);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+// dst[q] (F x R) = {X_R, Y_R, X_L, Y_L}[q] HM^T from the current model
+int xy_hmt(simm_ctx *c, double *const *dst) {
+  const int F = c->F, N = c->N, R = c->R, no = c->stereo ? 4 : 2;
+  if (R > 48) {
+    k_simm_xy<<<egrid((size_t)F * N), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p,
+                                                           (size_t)F * N, c->stereo);
+    if (c->stereo)
+      k_simm_xy<<<egrid((size_t)F * N), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p,
+                                                             (size_t)F * N, c->stereo);
+    const double *srcs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
+    for (int q = 0; q < no; ++q) {  // X HM^T : (F x N)(N x R)
+      const double *Bs[1] = {c->HM.p};
+      double *Cs[1] = {dst[q]};
+      int st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p);
+      if (st) return st;
+    }
+    return FASST_OK;
+  }
+  const SkinnySplit sp = hmt_split(F, N);
+  const size_t slab = (size_t)no * F * R;
+  dim3 grid(1, (F + 63) / 64, sp.nz);
+  if (c->stereo)
+    k_simm_xy_hmt<true><<<grid, 256, 0, c->stream>>>(c->HM.p, c->hR.p, c->SXR.p, c->hL.p, c->SXL.p,
+                                                      c->gwork.p, slab, F, N, R, sp.kchunk);
+  else
+    k_simm_xy_hmt<false><<<grid, 256, 0, c->stream>>>(c->HM.p, c->hR.p, c->SXR.p, nullptr, nullptr,
+                                                       c->gwork.p, slab, F, N, R, sp.kchunk);
+  FASST_LAUNCH_CHECK();
+  reduce_slabs(c, no, sp.nz, (size_t)F * R, dst);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
 // SMR = (WM bR^2) HM, SML = (WM bL^2) HM  (stereo); SM = WM HM (mono)
 int refresh_sm(simm_ctx *c) {
   if (c->stereo) {
@@ -579,22 +847,15 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   if (reco) reco_error(c, reco + 1);
   // ---- HM (:740-773 / :318-331)
   if (c->stereo) {
-    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
-    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p, FN, c->stereo);
-    const double *Bs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
     double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
-    if ((st = gemm<true, false, 4>(c->stream, c->WM.p, R, Bs, N, Cs, N, R, N, F, c->gwork.p)))
-      return st;
+    if ((st = wmt_xy(c, Cs))) return st;
     k_hm_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
                                                              c->RN0.p + (size_t)R * N,
                                                              c->RN1.p + (size_t)R * N, c->bR.p,
                                                              c->bL.p, R, N, omega);
   } else {
-    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
-    const double *Bs[2] = {c->T0.p, c->T1.p};
     double *Cs[2] = {c->RN0.p, c->RN1.p};
-    if ((st = gemm<true, false, 2>(c->stream, c->WM.p, R, Bs, N, Cs, N, R, N, F, c->gwork.p)))
-      return st;
+    if ((st = wmt_xy(c, Cs))) return st;
     k_mu_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
                                                             (size_t)R * N, omega, 1);
   }
@@ -612,29 +873,14 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   }
   // ---- WM (:826-869 / :355-387)
   if (c->stereo) {
-    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
-    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p, FN, c->stereo);
-    const double *srcs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
     double *dsts[4] = {c->P0.p, c->P1.p, c->P2.p, c->P3.p};
-    for (int q = 0; q < 4; ++q) {  // X HM^T : (F x N)(N x R)
-      const double *Bs[1] = {c->HM.p};
-      double *Cs[1] = {dsts[q]};
-      if ((st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p)))
-        return st;
-    }
+    if ((st = xy_hmt(c, dsts))) return st;
     k_wm_update<<<R, 256, 0, c->stream>>>(c->WM.p, c->P0.p, c->P1.p, c->P2.p, c->P3.p, c->bR.p,
                                           c->bL.p, c->sw.p, F, R, omega, 1);
     k_rowscale<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->sw.p, R, N);
   } else {
-    k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
-    const double *srcs[2] = {c->T0.p, c->T1.p};
     double *dsts[2] = {c->P0.p, c->P1.p};
-    for (int q = 0; q < 2; ++q) {
-      const double *Bs[1] = {c->HM.p};
-      double *Cs[1] = {dsts[q]};
-      if ((st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p)))
-        return st;
-    }
+    if ((st = xy_hmt(c, dsts))) return st;
     k_wm_update<<<R, 256, 0, c->stream>>>(c->WM.p, c->P0.p, c->P1.p, nullptr, nullptr, nullptr,
                                           nullptr, c->sw.p, F, R, omega, 0);
     // N7 (SIMM.py:388): HM *= sumWM broadcasts over the frame axis
@@ -652,13 +898,9 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   k_alpha_update<<<1, 64, 0, c->stream>>>(c->apart.p, c->nb_alpha, c->alpha.p, omega);
   if ((st = refresh_hat(c, nullptr, 0))) return st;
   // ---- beta (:909-941)
-  k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p, FN, c->stereo);
-  k_simm_xy<<<egrid(FN), 256, 0, c->stream>>>(c->hL.p, c->SXL.p, c->T2.p, c->T3.p, FN, c->stereo);
   {
-    const double *Bs[4] = {c->T0.p, c->T1.p, c->T2.p, c->T3.p};
     double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
-    if ((st = gemm<true, false, 4>(c->stream, c->WM.p, R, Bs, N, Cs, N, R, N, F, c->gwork.p)))
-      return st;
+    if ((st = wmt_xy(c, Cs))) return st;
   }
   k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p, c->HM.p, c->bd.p, N);
   k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p, c->HM.p, c->bd.p + R, N);
@@ -704,6 +946,7 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   gw = std::max(gw, gemm_workspace(F, N, R, 1));
   gw = std::max(gw, gemm_workspace(R, N, F, stereo ? 4 : 2));
   gw = std::max(gw, gemm_workspace(F, R, N, 1));
+  gw = std::max(gw, skinny_workspace(F, N, R, stereo));
 #define SA(buf, n) \
   if (!st) st = c->buf.alloc(n)
   SA(SXR, FN);

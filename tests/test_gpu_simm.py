@@ -81,10 +81,12 @@ def _data(F, N, NF0, P, seed):
             rs.gamma(1.0, 1.0, size=(F, NF0)), rs.gamma(1.0, 1.0, size=(F, P)))
 
 
-# shapes that exercise ragged 64x64 GEMM tiles and the split-K path
-# (F = 1025 splits WF0^T X over f; N = 600 splits X HM^T over frames)
+# shapes that exercise ragged GEMM tiles and the split-K paths (F = 1025
+# splits WF0^T X over f; N = 600 / 1300 split X HM^T over frames); R <= 48
+# takes the fused skinny kernels (R = 40: the pipeline's numCompAccomp),
+# R = 60 the materialised X, Y + general GEMM
 SHAPES = [(257, 301, 97, 10, 4, 7), (1025, 130, 150, 12, 4, 10), (129, 600, 40, 5, 2, 3),
-          (33, 17, 5, 3, 1, 1)]
+          (33, 17, 5, 3, 1, 1), (200, 1300, 30, 6, 2, 40), (97, 150, 20, 4, 2, 60)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
