@@ -385,83 +385,124 @@ __global__ __launch_bounds__(256) void k_hgamma_rows(
     const double *__restrict__ Z, const double *__restrict__ hR, const double *__restrict__ hL,
     const double *__restrict__ SXR, const double *__restrict__ SXL,
     const double *__restrict__ alpha, const double *__restrict__ HPHI, double *__restrict__ out,
-    int N, int K, int stereo) {
-  __shared__ double s_red[256];
-  const int f = blockIdx.x;
-  double sn[8], sd[8];
-  for (int k = 0; k < 8; ++k) sn[k] = sd[k] = 0.0;
+    int F, int N, int K, int stereo) {
+  constexpr int FB = 4;  // frequency rows per block: each HPHI load serves FB rows
+  __shared__ double s_red[FB * 16][4];
+  const int f0 = blockIdx.x * FB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double sn[FB][8], sd[FB][8];
+#pragma unroll
+  for (int r = 0; r < FB; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sn[r][k] = sd[r][k] = 0.0;
   const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
   const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
   for (int n = threadIdx.x; n < N; n += 256) {
-    const size_t i = (size_t)f * N + n;
-    double num, den;
-    if (stereo) {
-      const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
-      const double com = aR2 * Z[i] / mr;
-      const double d = aL2 * Z[i] / ml;
-      num = com * SXR[i];
-      num /= mr;
-      num += d * SXL[i] / ml;
-      den = d + com;
-    } else {
-      const double m = fmax(hR[i], kSimmEps);
-      den = Z[i] / m;
-      num = (den * SXR[i]) / m;
-    }
-    for (int k = 0; k < K; ++k) {
-      const double h = HPHI[(size_t)k * N + n];
-      sn[k] += num * h;
-      sd[k] += den * h;
+    double h[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = k < K ? HPHI[(size_t)k * N + n] : 0.0;
+#pragma unroll
+    for (int r = 0; r < FB; ++r) {
+      if (f0 + r >= F) break;
+      const size_t i = (size_t)(f0 + r) * N + n;
+      double num, den;
+      if (stereo) {
+        const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
+        const double com = aR2 * Z[i] / mr;
+        const double d = aL2 * Z[i] / ml;
+        num = com * SXR[i];
+        num /= mr;
+        num += d * SXL[i] / ml;
+        den = d + com;
+      } else {
+        const double m = fmax(hR[i], kSimmEps);
+        den = Z[i] / m;
+        num = (den * SXR[i]) / m;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // fixed trip count: sn / sd stay in registers
+        sn[r][k] += num * h[k];
+        sd[r][k] += den * h[k];
+      }
     }
   }
-  for (int q = 0; q < 2 * K; ++q) {
-    s_red[threadIdx.x] = q < K ? sn[q] : sd[q - K];
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
-      __syncthreads();
+  // wave butterflies, then the 4 waves' partials in fixed order
+#pragma unroll
+  for (int r = 0; r < FB; ++r)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (q % 8 >= K) continue;
+      double v = q < 8 ? sn[r][q] : sd[r][q - 8];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) s_red[r * 16 + q][wv] = v;
     }
-    if (threadIdx.x == 0) out[(size_t)f * 2 * K + q] = s_red[0];
-    __syncthreads();
+  __syncthreads();
+  for (int t = threadIdx.x; t < FB * 2 * K; t += 256) {
+    const int r = t / (2 * K), q = t % (2 * K);
+    const int slot = r * 16 + (q < K ? q : 8 + q - K);
+    if (f0 + r < F)
+      out[(size_t)(f0 + r) * 2 * K + q] =
+          (s_red[slot][0] + s_red[slot][1]) + (s_red[slot][2] + s_red[slot][3]);
   }
 }
 
-// HGAMMA update + renormalisations (:802-812 / :335-343), one block:
-// HGAMMA *= (WGAMMA^T numH / max(WGAMMA^T denH, eps))^omega, column-normalise,
-// WPHI = WGAMMA HGAMMA; the HPHI row scale by sumHGAMMA is returned in sg.
-__global__ void k_hgamma_update(double *__restrict__ HGAMMA, const double *__restrict__ WGAMMA,
-                                const double *__restrict__ rows, double *__restrict__ WPHI,
-                                double *__restrict__ sg, int F, int P, int K, double omega) {
-  __shared__ double s_h[64 * 8];
-  for (int idx = threadIdx.x; idx < P * K; idx += blockDim.x) {
-    const int p = idx / K, k = idx % K;
-    double num = 0.0, den = 0.0;
-    for (int f = 0; f < F; ++f) {
-      const double w = WGAMMA[f * P + p];
-      num += w * rows[(size_t)f * 2 * K + k];
-      den += w * rows[(size_t)f * 2 * K + K + k];
-    }
-    s_h[idx] = HGAMMA[idx] * powo(num / fmax(den, kSimmEps), omega);
+// HGAMMA update + renormalisations (:802-812 / :335-343) in three steps:
+// k_hgamma_numden (one block per filter-basis row p) reduces
+//   numH[p][k] = sum_f WGAMMA[f][p] rows[f][k], denH likewise over f;
+// k_hgamma_norm: HGAMMA *= (numH / max(denH, eps))^omega, column-normalise
+//   (sumHGAMMA -> sg, the HPHI row scale);
+// k_wphi: WPHI = WGAMMA HGAMMA.
+__global__ __launch_bounds__(256) void k_hgamma_numden(const double *__restrict__ WGAMMA,
+                                                       const double *__restrict__ rows,
+                                                       double *__restrict__ nd, int F, int P,
+                                                       int K) {
+  __shared__ double s_red[16][8];
+  const int p = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    const double w = WGAMMA[(size_t)f * P + p];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q < 2 * K) acc[q] += w * rows[(size_t)f * 2 * K + q];
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    double v = acc[q];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_red[q][wv] = v;
   }
   __syncthreads();
-  if (threadIdx.x < K) {
-    const int k = threadIdx.x;
-    double s = 0.0;
-    for (int p = 0; p < P; ++p) s += s_h[p * K + k];
-    sg[k] = s;
-    for (int p = 0; p < P; ++p) {
-      const double v = s > 0 ? s_h[p * K + k] / s : s_h[p * K + k];
-      s_h[p * K + k] = v;
-      HGAMMA[p * K + k] = v;
-    }
+  if (threadIdx.x < 2 * K) {
+    const int q = threadIdx.x;
+    nd[p * 2 * K + q] = (s_red[q][0] + s_red[q][1]) + (s_red[q][2] + s_red[q][3]);
   }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < F * K; idx += blockDim.x) {
-    const int f = idx / K, k = idx % K;
-    double w = 0.0;
-    for (int p = 0; p < P; ++p) w += WGAMMA[f * P + p] * s_h[p * K + k];
-    WPHI[idx] = w;
+}
+
+__global__ void k_hgamma_norm(double *__restrict__ HGAMMA, const double *__restrict__ nd,
+                              double *__restrict__ sg, int P, int K, double omega) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
+  double s = 0.0;
+  for (int p = 0; p < P; ++p) {
+    const double v =
+        HGAMMA[p * K + k] * powo(nd[p * 2 * K + k] / fmax(nd[p * 2 * K + K + k], kSimmEps), omega);
+    HGAMMA[p * K + k] = v;
+    s += v;
   }
+  sg[k] = s;
+  if (s > 0)
+    for (int p = 0; p < P; ++p) HGAMMA[p * K + k] /= s;
+}
+
+__global__ void k_wphi(const double *__restrict__ WGAMMA, const double *__restrict__ HGAMMA,
+                       double *__restrict__ WPHI, int F, int P, int K) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= F * K) return;
+  const int f = idx / K, k = idx % K;
+  double w = 0.0;
+  for (int p = 0; p < P; ++p) w += WGAMMA[(size_t)f * P + p] * HGAMMA[p * K + k];
+  WPHI[idx] = w;
 }
 
 // HPHI *= outer(sg, ones); s = column sums; HPHI[:, s>0] /= s  (:808-811)
@@ -560,10 +601,14 @@ __global__ __launch_bounds__(256) void k_alpha_partial(
 
 __global__ void k_alpha_update(const double *__restrict__ part, int nb, double *__restrict__ alpha,
                                double omega) {
-  if (threadIdx.x != 0) return;
+  // one wave: lane-strided partial sums, then a fixed butterfly (deterministic)
+  const int lane = threadIdx.x;
   double s[4] = {0, 0, 0, 0};
-  for (int b = 0; b < nb; ++b)
+  for (int b = lane; b < nb; b += 64)
     for (int q = 0; q < 4; ++q) s[q] += part[(size_t)b * 4 + q];
+  for (int q = 0; q < 4; ++q)
+    for (int o = 32; o > 0; o >>= 1) s[q] += __shfl_xor(s[q], o, 64);
+  if (lane != 0) return;
   double aR = fmax(alpha[0] * pow(s[0] / s[1], omega * .1), kSimmEps);
   double aL = fmax(alpha[1] * pow(s[2] / s[3], omega * .1), kSimmEps);
   aR = aR / fmax(aR + aL, .001);
@@ -628,10 +673,11 @@ __global__ __launch_bounds__(256) void k_is_partial(const double *__restrict__ S
 }
 
 __global__ void k_is_final(const double *__restrict__ part, int nb, double *__restrict__ out) {
-  if (threadIdx.x != 0) return;
+  const int lane = threadIdx.x;  // one wave, as k_alpha_update
   double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[b];
-  *out = s;
+  for (int b = lane; b < nb; b += 64) s += part[b];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) *out = s;
 }
 
 // writeSeparatedSignals masks (SeparateLeadStereoTF.py:1785-1846), eps 1e-9:
@@ -863,10 +909,13 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   if ((st = refresh_hat(c, nullptr, 0))) return st;
   // ---- HGAMMA (:776-823 / :335-350)
   if (update_hgamma) {
-    k_hgamma_rows<<<F, 256, 0, c->stream>>>(c->SF0.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p,
-                                             c->alpha.p, c->HPHI.p, c->hrows.p, N, K, c->stereo);
-    k_hgamma_update<<<1, 256, 0, c->stream>>>(c->HGAMMA.p, c->WGAMMA.p, c->hrows.p, c->WPHI.p,
-                                              c->sg.p, F, c->P, K, omega);
+    k_hgamma_rows<<<(F + 3) / 4, 256, 0, c->stream>>>(c->SF0.p, c->hR.p, c->hL.p, c->SXR.p,
+                                                       c->SXL.p, c->alpha.p, c->HPHI.p, c->hrows.p,
+                                                       F, N, K, c->stereo);
+    k_hgamma_numden<<<c->P, 256, 0, c->stream>>>(c->WGAMMA.p, c->hrows.p, c->apart.p, F, c->P, K);
+    k_hgamma_norm<<<1, 64, 0, c->stream>>>(c->HGAMMA.p, c->apart.p, c->sg.p, c->P, K, omega);
+    k_wphi<<<(F * K + 255) / 256, 256, 0, c->stream>>>(c->WGAMMA.p, c->HGAMMA.p, c->WPHI.p, F,
+                                                       c->P, K);
     k_hphi_rescale<<<(N + 255) / 256, 256, 0, c->stream>>>(c->HPHI.p, c->sg.p, c->s_col.p, K, N);
     k_colscale<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->s_col.p, NF0, N);
     if ((st = refresh_hat(c, c->s_col.p, 1))) return st;
