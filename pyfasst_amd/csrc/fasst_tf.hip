@@ -215,15 +215,44 @@ __global__ void k_tf_to_ft(const double2 *__restrict__ src, double2 *__restrict_
   if (f < F && t < T) dst[((size_t)m * F + f) * T + t] = tile[tx][ty];
 }
 
-__global__ void k_mix_psd(const double *__restrict__ cx, int F, int T, int Fp, int Tp,
+// mix_psd (audioModel.py:304-319): mean over t of the Cx diagonals, averaged
+// over the channels.  Pass 1: block (64 bins, frame chunk), 4 frame phases
+// per bin reduced in LDS -> part[chunk][f] (Cx00, Cx11 sums); pass 2 sums
+// the chunks in order (deterministic; a chunked sum like NumPy's pairwise
+// mean rather than one 10^4-term running sum).
+constexpr int kPsdChunks = 64;
+__global__ __launch_bounds__(256) void k_mix_psd_part(const double *__restrict__ cx, int F,
+                                                      int T, int Fp, int Tp,
+                                                      double2 *__restrict__ part) {
+  __shared__ double2 s[4][64];
+  const int fl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + fl;
+  const int tpc = (T + kPsdChunks - 1) / kPsdChunks;
+  const int tb = blockIdx.y * tpc, te = min(T, tb + tpc);
+  const size_t plane = (size_t)Tp * Fp;
+  double s0 = 0.0, s2 = 0.0;
+  if (f < F)
+    for (int t = tb + ph; t < te; t += 4) {
+      s0 += cx[(size_t)t * Fp + f];
+      s2 += cx[plane + (size_t)t * Fp + f];
+    }
+  s[ph][fl] = make_double2(s0, s2);
+  __syncthreads();
+  if (ph == 0 && f < F) {
+    const double2 a = s[0][fl], b = s[1][fl], c = s[2][fl], d = s[3][fl];
+    part[(size_t)blockIdx.y * Fp + f] = make_double2((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y));
+  }
+}
+
+__global__ void k_mix_psd(const double2 *__restrict__ part, int F, int T, int Fp,
                           double *__restrict__ out) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
-  const size_t plane = (size_t)Tp * Fp;
   double s0 = 0.0, s2 = 0.0;
-  for (int t = 0; t < T; ++t) {
-    s0 += cx[(size_t)t * Fp + f];
-    s2 += cx[plane + (size_t)t * Fp + f];
+  for (int c = 0; c < kPsdChunks; ++c) {
+    const double2 v = part[(size_t)c * Fp + f];
+    s0 += v.x;
+    s2 += v.y;
   }
   out[f] = ((0.0 + s0 / T) + s2 / T) / 2.0;
 }
@@ -511,9 +540,13 @@ int fasst_mix_psd(fasst_ctx *c, double *mix_psd) {
   if (!c || !mix_psd) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   DBuf<double> d;
+  DBuf<double2> part;
   int st;
-  if ((st = d.alloc(c->F))) return st;
-  k_mix_psd<<<(c->F + 255) / 256, 256, 0, c->stream>>>(c->cx.p, c->F, c->T, c->Fp, c->Tp, d.p);
+  if ((st = d.alloc(c->F)) || (st = part.alloc((size_t)kPsdChunks * c->Fp))) return st;
+  k_mix_psd_part<<<dim3((c->F + 63) / 64, kPsdChunks), 256, 0, c->stream>>>(c->cx.p, c->F, c->T,
+                                                                           c->Fp, c->Tp, part.p);
+  FASST_LAUNCH_CHECK();
+  k_mix_psd<<<(c->F + 255) / 256, 256, 0, c->stream>>>(part.p, c->F, c->T, c->Fp, d.p);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipMemcpyAsync(mix_psd, d.p, c->F * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));
