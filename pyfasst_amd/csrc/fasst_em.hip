@@ -54,6 +54,18 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// 1/x for finite normal x (the E-step's guarded det and max(V, eps)):
+// v_rcp_f64 + two Newton steps (<= 1 ulp) instead of the ~10-instruction
+// IEEE division sequence.
+__device__ __forceinline__ double rcp_nr(double x) {
+#ifdef FASST_EXACT_DIV  // A/B builds only
+  return 1.0 / x;
+#endif
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+
 // ---------------------------------------------------------------- prep
 // W[j] = FB[j] . FW[j], written [KP][Fp] (f contiguous).
 // one block per (16-bin tile, source): FB tile and FW staged in LDS; the
@@ -131,7 +143,7 @@ struct EArgs {
   const double *Wkf;                      // [J][KP][Fp]
   const double2 *A;                       // [R][2][Fp]
   const double *psd;                      // [Fp]
-  double *hatW;                           // [J][Tp][Fp]
+  double *hatW;                           // [J][Tp][Fp]: rho = hat_W / max(V, eps)
   double *part;                           // [nchunk][Fp][NACC]
   double *llpart;                         // [nchunk][nft]
   int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
       const double dg = det + kEps;
       const double sg = dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0);
       det = sg * fmax(fabs(det), kEps);
-      const double rd = 1.0 / det;
+      const double rd = rcp_nr(det);
       const double i0 = d1 * rd, i1 = d0 * rd, ior = -ore * rd, ioi = -oim * rd;
       const double x00 = c00[i], x11 = c11[i], xr = cre[i], xi = cim[i];
       // P = Cx S
@@ -336,7 +348,11 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
           }
         }
       }
-      // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414)
+      // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414),
+      // stored as rho = (hat_W / vm^2) * vm with vm = max(V, eps): the FB ratio
+      // of update_spectral_components (:1521-1575, N1) formed here, where V is
+      // already in registers, so the FB contraction needs no V recompute; the
+      // TW contraction recovers hat_W as rho * max(V_old, eps)
       if (!(AB & 2)) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
@@ -350,7 +366,10 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
               hw += fabs(v2 * qa + V[j]);
             }
           }
-          a.hatW[((size_t)j * a.Tp + t) * a.Fp + f] = RKU == 1 ? hw : hw * inv_rk[j];
+          const double hwm = RKU == 1 ? hw : hw * inv_rk[j];
+          const double vm = fmax(V[j], kEps);
+          const double rv = rcp_nr(vm);
+          a.hatW[((size_t)j * a.Tp + t) * a.Fp + f] = (hwm * (rv * rv)) * vm;
         }
       } else {
         double sum = 0.0;
@@ -680,42 +699,30 @@ struct BArgs {
 };
 
 // FB numerator over t (:1521-1575), one wave per (FPW bin tiles, source,
-// frame chunk):  num[f][k] = sum_t (hat_W / V^2 * V) (FW.H)^T[t][k].
-// The single-factor quirk N1 makes other_fact_power == spat_comp_power == V,
-// so the denominator sum_t (V * (1/V)) (FW.H)^T[t][k] is the f-independent
-// sum_t (FW.H)^T[t][k] = (FW . rowsum(TW))[k] (to one rounding of V*(1/V));
-// k_fb_update forms it from hsum, and only the numerator is contracted here.
-// The V tiles reuse the A operand (TW) across the FPW bin tiles and the
-// (FW.H)^T B operand across them as well.
+// frame chunk):  num[f][k] = sum_t rho[f][t] (FW.H)^T[t][k] with
+// rho = hat_W / V^2 * V formed by the E-step (N1: other_fact_power ==
+// spat_comp_power == V).  The denominator sum_t (V * (1/V)) (FW.H)^T[t][k] is
+// the f-independent sum_t (FW.H)^T[t][k] = (FW . rowsum(TW))[k] (to one
+// rounding of V*(1/V)); k_fb_update forms it from hsum, and only the
+// numerator is contracted here: a plain (F x T).(T x K) product whose rho
+// tiles arrive bins-on-lanes, i.e. already in the A-operand layout, and whose
+// (FW.H)^T B operand is shared by the FPW bin tiles.
 template <int NKC, int FPW>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
-  constexpr int NKS = 4 * NKC;  // KP / 4
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
   const int ft0 = blockIdx.x * FPW, j = blockIdx.y;
   if (!a.fb_free[j]) return;
-  double wk[FPW][NKS];
-#pragma unroll
-  for (int p = 0; p < FPW; ++p) {
-    const int f = (ft0 + p) * 16 + fl;
-    const bool fin = ft0 + p < a.nft;
-    const double *w = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) wk[p][s] = fin ? w[(size_t)(4 * s) * a.Fp] : 0.0;
-  }
   d4 num[FPW][NKC];
 #pragma unroll
   for (int p = 0; p < FPW; ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) num[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
-  const double *hwj = a.hatW + (size_t)j * a.Tp * a.Fp;
+  const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
   for (int tt = tb; tt < te; ++tt) {
     const int t0 = tt * 16;
-    double tw[NKS], fb[4][NKC];
-    const double *twp = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) tw[s] = twp[(size_t)(4 * s) * a.Tp];
+    double fb[4][NKC];
     const double *fwh = a.FWHt + ((size_t)j * a.Tp + t0 + tq) * a.KP + fl;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -725,24 +732,10 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
     for (int p = 0; p < FPW; ++p) {
       if (ft0 + p >= a.nft) break;  // wave-uniform: no bin tile left
       const int f = (ft0 + p) * 16 + fl;
-      double h[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) h[i] = hwj[(size_t)(t0 + tq + 4 * i) * a.Fp + f];
-      // two independent MFMA chains (even / odd k-steps) for latency hiding
-      d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;
-#pragma unroll
-      for (int s = 0; s < NKS; s += 2) {
-        v = mfma4(tw[s], wk[p][s], v);
-        v2 = mfma4(tw[s + 1], wk[p][s + 1], v2);
-      }
-      v += v2;
       double r1[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double vm = fmax(v[i], kEps);
-        const double rv = 1.0 / vm;
-        r1[i] = t0 + tq + 4 * i < a.T ? (h[i] * (rv * rv)) * vm : 0.0;
-      }
+      for (int i = 0; i < 4; ++i)
+        r1[i] = t0 + tq + 4 * i < a.T ? rhoj[(size_t)(t0 + tq + 4 * i) * a.Fp + f] : 0.0;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -823,9 +816,10 @@ struct TArgs {
 // tiles, source, bin chunk):
 //   num[k][t] = sum_f W_new[f][k] * V_old * hat_W / V_new^2,
 //   den[k][t] = sum_f W_new[f][k] * V_old / V_new
-// V_old = W_old . TW, V_new = W_new . TW recomputed in registers; the W
-// operands (A of the V tiles, B of the contraction) are shared by the TPW
-// frame tiles.  Partial sums per bin chunk go to tnum / tden.
+// V_old = W_old . TW, V_new = W_new . TW recomputed in registers, hat_W =
+// rho * max(V_old, eps) from the E-step's rho; the W operands (A of the V
+// tiles, B of the contraction) are shared by the TPW frame tiles.  Partial
+// sums per bin chunk go to tnum / tden.
 template <int NKC, int TPW>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
@@ -888,7 +882,8 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
         const double vm = fmax(vn[i], kEps);
         const double rv = 1.0 / vm;
         const bool ok = tok && f0 + tq + 4 * i < a.F;
-        r3[i] = ok ? other * (h[i] * (rv * rv)) : 0.0;
+        const double hw = h[i] * other;  // hat_W from the E-step's rho
+        r3[i] = ok ? other * (hw * (rv * rv)) : 0.0;
         r4[i] = ok ? other * rv : 0.0;
       }
 #pragma unroll
