@@ -128,8 +128,8 @@ def job_value(world, steps, dt_max):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--T", type=int, default=T_FRAMES)
     args = ap.parse_args()
@@ -172,7 +172,7 @@ def main():
 
     # per-kernel HIP-event timing on the engine's stream (separate, untimed pass)
     eng.set_profiling(True)
-    eng.run(psd_schedule(m, 3), m.nmfUpdateCoeff)
+    eng.run(psd_schedule(m, 5), m.nmfUpdateCoeff)
     times = eng.kernel_times()
     eng.set_profiling(False)
 

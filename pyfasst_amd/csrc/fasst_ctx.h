@@ -21,6 +21,12 @@
 struct fasst_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // side stream: the small per-iteration prep kernels ((FW.TW)^T, TW row sums)
+  // run there, forked at the iteration start and joined before their first
+  // consumer, so they overlap the E-step instead of serialising before it
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int nofork = 0;  // FASST_NOFORK (A/B measurements only)
   // observation
   int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
   fasst::DBuf<double> cx;        // 4*Tp*Fp

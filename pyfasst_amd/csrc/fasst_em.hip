@@ -1280,6 +1280,8 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
   ALLOC(flags, kNFlags);
   ALLOC(hsum, (size_t)J * KP);
+  // renormalisation chunks (every stage-2 block re-reduces all stage-1
+  // partials, so more chunks measured slower at C3)
   c->nchunk_r = std::max(1, std::min(64, std::min((c->T + 255) / 256, (c->F + 15) / 16)));
   ALLOC(rscal, (size_t)J * (2 + 2 * KP));
   ALLOC(rpmax, (size_t)J * c->nchunk_r * KP);
@@ -1470,12 +1472,25 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
 static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
                          int iter) {
   const int J = c->J;
-  int st = launch_w_old(c);
-  if (st) return st;
+  // (FW.TW)^T and the TW row sums depend only on the previous iteration's
+  // parameters: fork them onto the side stream (kept on the main stream
+  // while per-kernel event timing is on)
+  const bool fork = !c->prof && !c->nofork;
+  hipStream_t side = fork ? c->aux : c->stream;
+  if (fork) {
+    FASST_HIP(hipEventRecord(c->ev_fork, c->stream));
+    FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  }
   prof_begin(c, KFWH);
   k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, (size_t)(c->KP * c->KP + c->KP * 64) * sizeof(double),
-            c->stream>>>(c->FW.p, c->TW.p, c->FWHt.p, J, c->Tp, c->KP, c->halt);
+            side>>>(c->FW.p, c->TW.p, c->FWHt.p, J, c->Tp, c->KP, c->halt);
   prof_end(c, KFWH);
+  FASST_LAUNCH_CHECK();
+  k_tw_rowsum<<<J * c->KP, 256, 0, side>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
+  FASST_LAUNCH_CHECK();
+  if (fork) FASST_HIP(hipEventRecord(c->ev_join, c->aux));
+  int st = launch_w_old(c);
+  if (st) return st;
   st = build_inst_A(c);
   if (st) return st;
   EArgs e;
@@ -1503,8 +1518,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
   launch_estep(c, e);
   FASST_LAUNCH_CHECK();
-  k_tw_rowsum<<<J * c->KP, 256, 0, c->stream>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
-  FASST_LAUNCH_CHECK();
+  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
   prof_begin(c, KLL);
   k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
                                      1.0 / ((double)c->F * (double)c->T), c->halt);
@@ -1693,8 +1707,12 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->ntt = c->Tp / kTile;
   int st = FASST_OK;
   if (const char *ab = getenv("FASST_ABLATE")) c->ablate = atoi(ab);  // profiling only
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    set_error("hipStreamCreate failed");
+  if (const char *nf = getenv("FASST_NOFORK")) c->nofork = atoi(nf);  // A/B only
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    set_error("hipStreamCreate / hipEventCreate failed");
     st = FASST_ERR_DEVICE;
   }
   if (!st) st = c->cx.alloc((size_t)4 * c->Tp * c->Fp);
@@ -1720,6 +1738,7 @@ int fasst_destroy(fasst_ctx *c) {
   {
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
     if (c->h_flags) (void)hipHostFree(c->h_flags);
     if (c->h_ll) (void)hipHostFree(c->h_ll);
     c->cx.release();
@@ -1753,6 +1772,9 @@ int fasst_destroy(fasst_ctx *c) {
       if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
       if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
     }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
   delete c;

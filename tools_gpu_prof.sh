@@ -5,7 +5,8 @@ R="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$R/gpurun_out/${PROF_TAG:-prof}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps ${STEPS:-10} --warmup 2 --no-cpu-baseline"
+# (warmup 20: the first ~15 iterations run while the GPU clock ramps up)
+ARGS="--steps ${STEPS:-50} --warmup 20 --no-cpu-baseline"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 "$R/bench.py" $ARGS > "$OUT/bench_trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; tail -2 "$OUT/bench_trace.log"; [ $rc -eq 0 ] || exit $rc
