@@ -34,7 +34,18 @@ def main(src, dst):
         e["total_ns"] += float(r["TotalDurationNs"])
     for k, e in kernels.items():
         e["avg_us"] = round(e["total_ns"] / e["calls"] / 1e3, 3)
-    pmc = collections.defaultdict(lambda: collections.defaultdict(list))
+    # steady-clock average: the second half of each kernel's launches (the
+    # first iterations of a run execute while the GPU clock ramps up)
+    tpath = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tpath):
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(tpath)):
+            durs[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, d in durs.items():
+            if k in kernels and len(d) >= 2:
+                tail = d[len(d) // 2:]
+                kernels[k]["avg_us_2nd_half"] = round(sum(tail) / len(tail) / 1e3, 3)
+    pmc =collections.defaultdict(lambda: collections.defaultdict(list))
     for sub, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         path = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(path):
@@ -57,11 +68,11 @@ def main(src, dst):
         json.dump(out, fh, indent=1)
     with open(dst + ".txt", "w") as fh:
         fh.write("# rocprofv3 summary of %s\n" % src)
-        fh.write("%-16s %7s %12s %14s %14s %16s\n" % ("kernel", "calls", "avg_us", "FETCH_KiB",
-                                                     "WRITE_KiB", "hbm_B/launch"))
+        fh.write("%-16s %7s %12s %12s %14s %14s %16s\n" % (
+            "kernel", "calls", "avg_us", "avg_us_2h", "FETCH_KiB", "WRITE_KiB", "hbm_B/launch"))
         for k, e in sorted(kernels.items(), key=lambda kv: -kv[1].get("total_ns", 0)):
-            fh.write("%-16s %7s %12s %14s %14s %16s\n" % (
-                k, e.get("calls", ""), e.get("avg_us", ""),
+            fh.write("%-16s %7s %12s %12s %14s %14s %16s\n" % (
+                k, e.get("calls", ""), e.get("avg_us", ""), e.get("avg_us_2nd_half", ""),
                 "%.0f" % e["FETCH_SIZE_KiB"] if e.get("FETCH_SIZE_KiB") is not None else "",
                 "%.0f" % e["WRITE_SIZE_KiB"] if e.get("WRITE_SIZE_KiB") is not None else "",
                 "%.3e" % e["hbm_bytes_per_launch"] if e.get("hbm_bytes_per_launch") else ""))
