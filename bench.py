@@ -37,8 +37,9 @@ def kernel_work(F, T, J, R, K):
                    bytes 32 (Cx) + 8J (hat_W write) per (f,t)
     k_estep_part2: V^T tiles 2JK, P = Cx S and the cross statistics ~ (17J + 10R)
                    per (f,t); bytes 32 (Cx re-read) per (f,t)
-    k_fb_contract: V^T 2K + num 2K per (f,t,j) (the denominator is f-independent,
-                   see fasst_em.hip); bytes 8 (hat_W) per (f,t,j)
+    k_fb_contract: num 2K per (f,t,j): the E-step hands over rho = hat_W/V, and the
+                   denominator is f-independent (see fasst_em.hip); bytes 8 (rho)
+                   per (f,t,j)
     k_tw_contract: V_old, V_new 4K + num/den 4K per (f,t,j); bytes 8 per (f,t,j)
     """
     ft = float(F) * T
@@ -47,7 +48,7 @@ def kernel_work(F, T, J, R, K):
         "k_estep_part1": dict(flops=ft * (2 * J * K + 8 * J + 70 + 9 * np_),
                               bytes=ft * (32 + 8 * J)),
         "k_estep_part2": dict(flops=ft * (2 * J * K + 17 * J + 10 * R), bytes=ft * 32),
-        "k_fb_contract": dict(flops=ft * J * 4 * K, bytes=ft * J * 8),
+        "k_fb_contract": dict(flops=ft * J * 2 * K, bytes=ft * J * 8),
         "k_tw_contract": dict(flops=ft * J * 8 * K, bytes=ft * J * 8),
     }
 
