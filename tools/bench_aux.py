@@ -61,12 +61,36 @@ def bench_simm(steps, warmup, F=2049, N=20000, NF0=1092, P=30, K=4, R=40, seed=0
     # GEMM flops per iteration: WF0^T{num,den} (2), SF0 recompute (1) on F x NF0 x N;
     # the R-sized products (HM: 4, WM: 4, beta: 4, SM refreshes: 2 x 3) on F x R x N
     flops = 2.0 * F * N * (3 * NF0 + 18 * R)
+    achieved = flops / (dt / steps) / 1e12
+    # CPU baseline: the oracle restatement (SIMM.py's operation order) on a
+    # bounded sample, one iteration on N_cpu frames, scaled to N (linear in N)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import simm_ref
+    n_cpu = 1000
+    np.random.seed(1)
+    t1 = time.perf_counter()
+    simm_ref.stereo_simm(SXR[:, :n_cpu], SXL[:, :n_cpu], WF0, WG, K, R, numberOfIterations=1)
+    cpu_s = (time.perf_counter() - t1) * N / n_cpu
     return {"metric": "Stereo_SIMM iterations/sec (config 5)", "value": round(steps / dt, 4),
             "unit": "SIMM it/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
             "warmup": warmup, "dtype": "f64", "data": "synthetic gamma spectrograms, RandomState(0)",
             "config": {"workload": "Stereo_SIMM F=%d N=%d NF0=%d P=%d K=%d R=%d" % (F, N, NF0, P, K, R)},
-            "gemm_tflops_per_s": round(flops / (dt / steps) / 1e12, 2),
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP64_PEAK / 1e12,
+                         "unit": "TFLOP/s", "frac": round(achieved * 1e12 / FP64_PEAK, 4),
+                         "traffic": None, "scope": "whole iteration, GEMM flops 2FN(3 NF0 + 18 R)"},
+            "gemm_tflops_per_s": round(achieved, 2),
+            "cpu_baseline": {"value": round(1.0 / cpu_s, 5), "unit": "SIMM it/s", "cores": _blas_threads(),
+                             "kind": "port", "sample": "oracle/simm_ref.py stereo_simm, 1 iteration "
+                             "on %d of %d frames (%.2f s), scaled" % (n_cpu, N, cpu_s * n_cpu / N)},
             "reference_cpu": "14.27 s/iter = 0.070 it/s (BASELINE/SURVEY §6, measured on CPU)"}
+
+
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return int(max([p.get('num_threads', 1) for p in threadpool_info()] + [1]))
+    except Exception:
+        return 1
 
 
 def bench_nmf(steps, warmup, F=1025, N=2000, K=64, seed=0):
@@ -86,11 +110,24 @@ def bench_nmf(steps, warmup, F=1025, N=2000, K=64, seed=0):
     _lib.check(_lib.lib.nmf_run(ctx.ptr, steps, 1, 1), "run")
     dt = time.perf_counter() - t0
     flops = 2.0 * F * N * K * 6
+    achieved = flops / (dt / steps) / 1e12
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import fasst_ref
+    n_cpu = 20
+    t1 = time.perf_counter()
+    fasst_ref.nmf_decomp_init(SX, nbComps=K, niter=n_cpu, Winit=W.copy(), Hinit=H.copy())
+    cpu_s = (time.perf_counter() - t1) / n_cpu
     return {"metric": "NMF_decomposition iterations/sec (config 2)", "value": round(steps / dt, 3),
             "unit": "NMF it/s", "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
             "warmup": warmup, "dtype": "f64", "data": "synthetic gamma spectrogram, RandomState(0)",
             "config": {"workload": "IS-NMF F=%d T=%d K=%d" % (F, N, K)},
-            "gemm_tflops_per_s": round(flops / (dt / steps) / 1e12, 2),
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP64_PEAK / 1e12,
+                         "unit": "TFLOP/s", "frac": round(achieved * 1e12 / FP64_PEAK, 4),
+                         "traffic": None, "scope": "whole iteration, GEMM flops 12FTK"},
+            "gemm_tflops_per_s": round(achieved, 2),
+            "cpu_baseline": {"value": round(1.0 / cpu_s, 3), "unit": "NMF it/s", "cores": _blas_threads(),
+                             "kind": "port", "sample": "oracle/fasst_ref.py nmf_decomp_init, %d "
+                             "iterations at the full size" % n_cpu},
             "reference_cpu": "0.0318 s/iter = 31.4 it/s (SURVEY §6, measured on CPU)"}
 
 
