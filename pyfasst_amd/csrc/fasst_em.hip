@@ -767,15 +767,20 @@ struct UArgs {
 // k_fb_contract), then W_new = FB . FW in both layouts.
 __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   HALT_GUARD(a.halt);
-  extern __shared__ __attribute__((aligned(16))) double s_fb[];  // [16][KP] + [KP]
+  // LDS: FW [KP][KP] | FB rows [16][KP] | den [KP] | W_new rows [16][KP + 1]
+  extern __shared__ __attribute__((aligned(16))) double s_fw[];
   const int f0 = blockIdx.x * 16, j = blockIdx.y;
   const int KP = a.KP;
+  double *s_fb = s_fw + KP * KP;
   double *s_den = s_fb + 16 * KP;
+  double *s_wn = s_den + KP;
+  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
+    s_fw[idx] = a.FW[(size_t)j * KP * KP + idx];
+  __syncthreads();
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
-    const double *fw = a.FW + ((size_t)j * KP + k) * KP;
     const double *hs = a.hsum + (size_t)j * KP;
     double d = 0.0;
-    for (int q = 0; q < KP; ++q) d += fw[q] * hs[q];
+    for (int q = 0; q < KP; ++q) d += s_fw[k * KP + q] * hs[q];
     s_den[k] = d;
   }
   __syncthreads();
@@ -793,13 +798,19 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
     s_fb[idx] = fb;
   }
   __syncthreads();
+  // W_new = FB . FW: [f][k] rows written coalesced over k here, the [k][f]
+  // layout from the LDS copy below (coalesced over the 16 bins)
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int fl = idx / KP, k = idx % KP, f = f0 + fl;
-    const double *fw = a.FW + (size_t)j * KP * KP + k;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * fw[(size_t)q * KP];
-    a.Wkf_new[((size_t)j * KP + k) * a.Fp + f] = s;
+    for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * s_fw[q * KP + k];
     a.Wfk_new[((size_t)j * a.Fp + f) * KP + k] = s;
+    s_wn[fl * (KP + 1) + k] = s;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+    const int k = idx / 16, fl = idx % 16;
+    a.Wkf_new[((size_t)j * KP + k) * a.Fp + f0 + fl] = s_wn[fl * (KP + 1) + k];
   }
 }
 
@@ -1060,12 +1071,25 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   }
   __syncthreads();
   // FB rows of this chunk (only the K live columns carry data)
+  // (element loops below load a batch of kRnB values before storing any, so
+  // a thread keeps kRnB memory round trips in flight)
+  constexpr int kRnB = 8;
   const int fb = c * a.fpc, fe = min(fb + a.fpc, a.F);
-  for (int idx = threadIdx.x; idx < (fe - fb) * KP; idx += blockDim.x) {
-    const int f = fb + idx / KP, k = idx % KP;
-    if (k < K) {
-      double *p = a.FB + ((size_t)j * a.Fp + f) * KP + k;
-      *p = (*p * e) / s_w[k];
+  {
+    const int n = (fe - fb) * KP;
+    for (int base = threadIdx.x; base < n; base += kRnB * blockDim.x) {
+      double x[kRnB];
+#pragma unroll
+      for (int u = 0; u < kRnB; ++u) {
+        const int idx = base + u * blockDim.x;
+        x[u] = idx < n ? a.FB[((size_t)j * a.Fp + fb + idx / KP) * KP + idx % KP] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kRnB; ++u) {
+        const int idx = base + u * blockDim.x, k = idx % KP;
+        if (idx < n && k < K)
+          a.FB[((size_t)j * a.Fp + fb + idx / KP) * KP + k] = (x[u] * e) / s_w[k];
+      }
     }
   }
   const double se = sqrt(e);
@@ -1090,12 +1114,22 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   const int w = t1 - t0;
   double tsum = 0.0;
   if (w > 0)
-    for (int idx = threadIdx.x; idx < K * w; idx += blockDim.x) {
-      const int k = idx / w, t = t0 + idx % w;
-      double *p = TW + (size_t)k * a.Tp + t;
-      const double x = *p * s_w2[k];
-      *p = x;
-      tsum += x;
+    for (int base = threadIdx.x; base < K * w; base += kRnB * blockDim.x) {
+      double x[kRnB];
+#pragma unroll
+      for (int u = 0; u < kRnB; ++u) {
+        const int idx = base + u * blockDim.x;
+        x[u] = idx < K * w ? TW[(size_t)(idx / w) * a.Tp + t0 + idx % w] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kRnB; ++u) {
+        const int idx = base + u * blockDim.x;
+        if (idx < K * w) {
+          const double y = x[u] * s_w2[idx / w];
+          TW[(size_t)(idx / w) * a.Tp + t0 + idx % w] = y;
+          tsum += y;
+        }
+      }
     }
   tsum = block_sum(tsum, s_red);
   if (threadIdx.x == 0) a.tpart[(size_t)j * a.nchunk + c] = tsum;
@@ -1655,7 +1689,9 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   }
   FASST_LAUNCH_CHECK();
   prof_begin(c, KFBU);
-  k_fb_update<<<dim3(c->nft, J), 256, 17 * c->KP * sizeof(double), c->stream>>>(u);
+  k_fb_update<<<dim3(c->nft, J), 256,
+                (size_t)(c->KP * c->KP + 16 * c->KP + c->KP + 16 * (c->KP + 1)) * sizeof(double),
+                c->stream>>>(u);
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
   switch (nkc) {
