@@ -265,10 +265,12 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
-      c00[i] = a.cx00[off];
-      c11[i] = a.cx11[off];
-      cre[i] = a.cxr[off];
-      cim[i] = a.cxi[off];
+      // streamed planes (Cx, rho: 655 MB each at C3, larger than the 256 MB
+      // Infinity Cache) use non-temporal loads / stores: -1.5% per iteration
+      c00[i] = __builtin_nontemporal_load(a.cx00 + off);
+      c11[i] = __builtin_nontemporal_load(a.cx11 + off);
+      cre[i] = __builtin_nontemporal_load(a.cxr + off);
+      cim[i] = __builtin_nontemporal_load(a.cxi + off);
     }
     d4 v[J];
     tile_v(tt, v, lofs);
@@ -369,7 +371,8 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
           const double hwm = RKU == 1 ? hw : hw * inv_rk[j];
           const double vm = fmax(V[j], kEps);
           const double rv = rcp_nr(vm);
-          a.hatW[((size_t)j * a.Tp + t) * a.Fp + f] = (hwm * (rv * rv)) * vm;
+          __builtin_nontemporal_store((hwm * (rv * rv)) * vm,
+                                      a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
         }
       } else {
         double sum = 0.0;
@@ -874,7 +877,8 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       const int t = (tt0 + p) * 16 + fl;
       double h[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) h[i] = hwj[(size_t)t * a.Fp + f0 + tq + 4 * i];
+      for (int i = 0; i < 4; ++i)  // (last use of rho: non-temporal)
+        h[i] = __builtin_nontemporal_load(hwj + (size_t)t * a.Fp + f0 + tq + 4 * i);
       d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
