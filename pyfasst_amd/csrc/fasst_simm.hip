@@ -20,6 +20,10 @@
 namespace fasst {
 
 constexpr double kSimmEps = 1e-20;  // SIMM.py:150, :506
+// non-temporal access to the streamed F x N planes (see k_simm_refresh)
+#define SLD(p) __builtin_nontemporal_load(&(p))
+#define SST(p, v) __builtin_nontemporal_store((v), &(p))
+#define CLD(p) __builtin_nontemporal_load(&(p))
 
 // ------------------------------------------------------------------ kernels
 #define GRID_STRIDE(i, n)                                                          \
@@ -44,18 +48,18 @@ __global__ void k_simm_numden(const double *__restrict__ Z, const double *__rest
   if (stereo) {
     const double aR2 = alpha[0] * alpha[0], aL2 = alpha[1] * alpha[1];
     GRID_STRIDE(i, n) {
-      const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
-      const double com = aR2 * Z[i] / mr;
-      const double d = aL2 * Z[i] / ml;
-      num[i] = com * SXR[i] / mr + d * SXL[i] / ml;
+      const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
+      const double com = aR2 * CLD(Z[i]) / mr;
+      const double d = aL2 * CLD(Z[i]) / ml;
+      num[i] = com * CLD(SXR[i]) / mr + d * CLD(SXL[i]) / ml;
       den[i] = d + com;
     }
   } else {
     GRID_STRIDE(i, n) {
-      const double m = fmax(hR[i], kSimmEps);
-      const double d = Z[i] / m;
+      const double m = fmax(CLD(hR[i]), kSimmEps);
+      const double d = CLD(Z[i]) / m;
       den[i] = d;
-      num[i] = (d * SXR[i]) / m;
+      num[i] = (d * CLD(SXR[i])) / m;
     }
   }
 }
@@ -85,7 +89,10 @@ __global__ void k_hm_apply(double *__restrict__ HM, const double *__restrict__ P
   }
 }
 
-// hat refresh: optional SF0 column scale, optional SPHI = WPHI HPHI (K small)
+// hat refresh: optional SF0 column scale, optional SPHI = WPHI HPHI (K small).
+// The F x N planes (328 MB each at C5, several per kernel: more than the
+// 256 MB Infinity Cache) are streamed with non-temporal loads / stores (SLD /
+// SST): -2.6% per Stereo_SIMM iteration (same-box A/B).
 __global__ void k_simm_refresh(double *__restrict__ SF0, double *__restrict__ SPHI,
                                const double *__restrict__ WPHI, const double *__restrict__ HPHI,
                                const double *__restrict__ colscale, const double *__restrict__ SMR,
@@ -96,25 +103,25 @@ __global__ void k_simm_refresh(double *__restrict__ SF0, double *__restrict__ SP
   const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
   GRID_STRIDE(i, (size_t)F * N) {
     const int f = i / N, n = i % N;
-    double sf = SF0[i];
+    double sf = SLD(SF0[i]);
     if (colscale) {
       sf *= colscale[n];
-      SF0[i] = sf;
+      SST(SF0[i], sf);
     }
     double sp;
     if (recompute_sphi) {
       sp = 0.0;
       for (int k = 0; k < K; ++k) sp += WPHI[f * K + k] * HPHI[(size_t)k * N + n];
-      SPHI[i] = sp;
+      SST(SPHI[i], sp);
     } else {
-      sp = SPHI[i];
+      sp = SLD(SPHI[i]);
     }
     const double l = sf * sp;
     if (stereo) {
-      hR[i] = fmax(SMR[i] + aR2 * l, kSimmEps);
-      hL[i] = fmax(l * aL2 + SML[i], kSimmEps);
+      SST(hR[i], fmax(SLD(SMR[i]) + aR2 * l, kSimmEps));
+      SST(hL[i], fmax(l * aL2 + SLD(SML[i]), kSimmEps));
     } else {
-      hR[i] = fmax(l + SMR[i], kSimmEps);
+      SST(hR[i], fmax(l + SLD(SMR[i]), kSimmEps));
     }
   }
 }
@@ -327,17 +334,17 @@ __global__ __launch_bounds__(256) void k_hphi_partial(
       const size_t i = (size_t)f * N + n;
       double num, den;
       if (stereo) {
-        const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
-        const double com = aR2 * Z[i] / mr;
-        const double d = aL2 * Z[i] / ml;
-        num = com * SXR[i];
+        const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
+        const double com = aR2 * CLD(Z[i]) / mr;
+        const double d = aL2 * CLD(Z[i]) / ml;
+        num = com * CLD(SXR[i]);
         num /= mr;
-        num += d * SXL[i] / ml;
+        num += d * CLD(SXL[i]) / ml;
         den = d + com;
       } else {
-        const double m = fmax(hR[i], kSimmEps);
-        den = Z[i] / m;
-        num = (den * SXR[i]) / m;
+        const double m = fmax(CLD(hR[i]), kSimmEps);
+        den = CLD(Z[i]) / m;
+        num = (den * CLD(SXR[i])) / m;
       }
       for (int k = 0; k < K; ++k) {
         const double w = WPHI[f * K + k];
@@ -406,17 +413,17 @@ __global__ __launch_bounds__(256) void k_hgamma_rows(
       const size_t i = (size_t)(f0 + r) * N + n;
       double num, den;
       if (stereo) {
-        const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
-        const double com = aR2 * Z[i] / mr;
-        const double d = aL2 * Z[i] / ml;
-        num = com * SXR[i];
+        const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
+        const double com = aR2 * CLD(Z[i]) / mr;
+        const double d = aL2 * CLD(Z[i]) / ml;
+        num = com * CLD(SXR[i]);
         num /= mr;
-        num += d * SXL[i] / ml;
+        num += d * CLD(SXL[i]) / ml;
         den = d + com;
       } else {
-        const double m = fmax(hR[i], kSimmEps);
-        den = Z[i] / m;
-        num = (den * SXR[i]) / m;
+        const double m = fmax(CLD(hR[i]), kSimmEps);
+        den = CLD(Z[i]) / m;
+        num = (den * CLD(SXR[i])) / m;
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {  // fixed trip count: sn / sd stay in registers
@@ -581,12 +588,12 @@ __global__ __launch_bounds__(256) void k_alpha_partial(
   __shared__ double s_red[4][256];
   double a[4] = {0, 0, 0, 0};
   GRID_STRIDE(i, n) {
-    const double l = SF0[i] * SPHI[i];
-    const double mr = fmax(hR[i], kSimmEps), ml = fmax(hL[i], kSimmEps);
+    const double l = CLD(SF0[i]) * CLD(SPHI[i]);
+    const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
     const double dR = l / mr, dL = l / ml;
-    a[0] += dR * SXR[i] / mr;
+    a[0] += dR * CLD(SXR[i]) / mr;
     a[1] += dR;
-    a[2] += dL * SXL[i] / ml;
+    a[2] += dL * CLD(SXL[i]) / ml;
     a[3] += dL;
   }
   for (int q = 0; q < 4; ++q) s_red[q][threadIdx.x] = a[q];
