@@ -15,6 +15,8 @@
 // Split-K along gridDim.z writes partial C slabs (C + z*slab) that
 // k_gemm_reduce sums in fixed order (deterministic).
 #pragma once
+#include <rocblas/rocblas.h>
+
 #include "fasst_common.h"
 
 namespace fasst {
@@ -191,5 +193,13 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
          int ldc, int M, int N, int K, double *work);
 // doubles of `work` gemm() needs for these sizes (0: no split)
 size_t gemm_workspace(int M, int N, int K, int NB);
+
+// Plain (unfused) large products go to rocBLAS dgemm: row-major
+// C (M x N) = op(A) op(B) with op = transpose when ta / tb, issued on the
+// stream the handle is bound to.  rocBLAS's Tensile kernels (the same
+// v_mfma_f64_16x16x4 instruction) sustain ~1.8x the FP64 rate of k_gemm at
+// the Stereo_SIMM sizes (tools/ubench_dgemm.hip).
+int blas_gemm(rocblas_handle h, bool ta, bool tb, int M, int N, int K, const double *A, int lda,
+              const double *B, int ldb, double *C, int ldc);
 
 }  // namespace fasst

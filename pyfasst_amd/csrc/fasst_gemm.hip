@@ -44,6 +44,22 @@ static void tile_dims(const TileShape &t, int &BM, int &BN) {
   BN = 16 * (4 / t.wgm) * t.wtn;
 }
 
+// Row-major C = op(A) op(B) as the column-major product C^T = op(B)^T op(A)^T:
+// a row-major X (r x c, ld) is the column-major X^T (c x r, ld).
+int blas_gemm(rocblas_handle h, bool ta, bool tb, int M, int N, int K, const double *A, int lda,
+              const double *B, int ldb, double *C, int ldc) {
+  const double one = 1.0, zero = 0.0;
+  const rocblas_status s =
+      rocblas_dgemm(h, tb ? rocblas_operation_transpose : rocblas_operation_none,
+                    ta ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &one, B,
+                    ldb, A, lda, &zero, C, ldc);
+  if (s != rocblas_status_success) {
+    set_error("rocblas_dgemm: %s", rocblas_status_to_string(s));
+    return FASST_ERR_DEVICE;
+  }
+  return FASST_OK;
+}
+
 // split K until the grid holds >= 1024 blocks (4 per CU), chunks >= 64
 GemmPlan gemm_plan(int M, int N, int K, int NB) {
   GemmPlan p;

@@ -719,6 +719,8 @@ using namespace fasst;
 struct simm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  rocblas_handle blas = nullptr;  // bound to `stream`: the NF0-sized plain GEMMs
+  int use_blas = 1;               // FASST_SIMM_BLAS=0: k_gemm instead (A/B only)
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
   DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
@@ -733,6 +735,14 @@ int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, dou
   const double *Bs[1] = {B};
   double *Cs[1] = {C};
   return gemm<false, false, 1>(c->stream, A, lda, Bs, ldb, Cs, ldc, M, N, K, c->gwork.p);
+}
+
+// SF0 = WF0 HF0 (F x NF0)(NF0 x N)
+int sf0_gemm(simm_ctx *c) {
+  if (c->use_blas)
+    return blas_gemm(c->blas, false, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
+                     c->SF0.p, c->N);
+  return gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, c->N, c->SF0.p, c->N, c->F, c->N, c->NF0);
 }
 
 // split of the fused skinny products (k_simm_wmt_xy / k_simm_xy_hmt): a
@@ -853,7 +863,7 @@ int rebuild_model(simm_ctx *c) {
   int st;
   const int F = c->F, N = c->N, K = c->K;
   if ((st = gemm_nn(c, c->WGAMMA.p, c->P, c->HGAMMA.p, K, c->WPHI.p, K, F, K, c->P))) return st;
-  if ((st = gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, N, c->SF0.p, N, F, N, c->NF0))) return st;
+  if ((st = sf0_gemm(c))) return st;
   if ((st = refresh_sm(c))) return st;
   // the reference's initial hat is not floored by eps (:579-585); every use
   // floors it again with max(., eps), so the floored copy is equivalent
@@ -878,7 +888,11 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   // ---- HF0 (:623-674 / :281-291)
   k_simm_numden<<<egrid(FN), 256, 0, c->stream>>>(c->SPHI.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p,
                                                    c->alpha.p, c->T0.p, c->T1.p, FN, c->stereo);
-  {
+  if (c->use_blas) {  // WF0^T {num, den}: (NF0 x F)(F x N)
+    if ((st = blas_gemm(c->blas, true, false, NF0, N, F, c->WF0.p, NF0, c->T0.p, N, c->NP0.p, N)) ||
+        (st = blas_gemm(c->blas, true, false, NF0, N, F, c->WF0.p, NF0, c->T1.p, N, c->NP1.p, N)))
+      return st;
+  } else {
     const double *Bs[2] = {c->T0.p, c->T1.p};
     double *Cs[2] = {c->NP0.p, c->NP1.p};
     if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, N, Cs, N, NF0, N, F, c->gwork.p)))
@@ -886,7 +900,7 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   }
   k_mu_apply<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->NP0.p, c->NP1.p,
                                                              (size_t)NF0 * N, omega, 0);
-  if ((st = gemm_nn(c, c->WF0.p, NF0, c->HF0.p, N, c->SF0.p, N, F, N, NF0))) return st;
+  if ((st = sf0_gemm(c))) return st;
   if ((st = refresh_hat(c, nullptr, 0))) return st;
   if (reco) reco_error(c, reco);
   // ---- HPHI (:686-729 / :296-313)
@@ -996,6 +1010,12 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   const size_t FN = (size_t)F * N;
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
+  if (!st && (rocblas_create_handle(&c->blas) != rocblas_status_success ||
+              rocblas_set_stream(c->blas, c->stream) != rocblas_status_success)) {
+    set_error("rocblas_create_handle / rocblas_set_stream failed");
+    st = FASST_ERR_DEVICE;
+  }
+  if (const char *v = getenv("FASST_SIMM_BLAS")) c->use_blas = atoi(v);
   size_t gw = 0;
   gw = std::max(gw, gemm_workspace(NF0, N, F, 2));
   gw = std::max(gw, gemm_workspace(F, N, NF0, 1));
@@ -1058,10 +1078,9 @@ int simm_destroy(simm_ctx *c) {
   if (!c) return FASST_OK;
   {
     DeviceGuard g(c->device);
-    if (c->stream) {
-      (void)hipStreamSynchronize(c->stream);
-      (void)hipStreamDestroy(c->stream);
-    }
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->blas) (void)rocblas_destroy_handle(c->blas);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
   }
   delete c;  // DBuf destructors free device memory
   return FASST_OK;
