@@ -895,7 +895,7 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       for (int i = 0; i < 4; ++i) {
         const double other = fmax(vo[i], kEps);
         const double vm = fmax(vn[i], kEps);
-        const double rv = 1.0 / vm;
+        const double rv = rcp_nr(vm);
         const bool ok = tok && f0 + tq + 4 * i < a.F;
         const double hw = h[i] * other;  // hat_W from the E-step's rho
         r3[i] = ok ? other * (hw * (rv * rv)) : 0.0;
