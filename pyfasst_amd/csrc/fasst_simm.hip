@@ -126,6 +126,55 @@ __global__ void k_simm_refresh(double *__restrict__ SF0, double *__restrict__ SP
   }
 }
 
+// Accompaniment refresh fused with the hat refresh (the step after every HM,
+// WM and beta update, SIMM.py:747-773, :826-869, :909-941): stereo
+// SMR = (WM bR^2) HM, SML = (WM bL^2) HM, mono SM = WM HM (R <= RMAX), then
+// hR / hL exactly as k_simm_refresh.  One thread per frame n keeps the HM
+// column in registers for FB bins; the FB rows of WM (times beta^2) sit in
+// LDS.  Replaces two K = R products (which wrote SMR / SML only for the
+// refresh to read them back) and the refresh pass: 6 streamed planes
+// instead of 8, one launch instead of five.
+template <int RMAX>
+__global__ __launch_bounds__(256) void k_simm_sm_refresh(
+    const double *__restrict__ WbR, const double *__restrict__ WbL, const double *__restrict__ HM,
+    const double *__restrict__ SF0, const double *__restrict__ SPHI,
+    const double *__restrict__ alpha, double *__restrict__ SMR, double *__restrict__ SML,
+    double *__restrict__ hR, double *__restrict__ hL, int F, int N, int R, int stereo) {
+  constexpr int FB = 16;
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int f0 = blockIdx.y * FB;
+  if (n >= N) return;
+  double hm[RMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) hm[r] = r < R ? HM[(size_t)r * N + n] : 0.0;
+  const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
+  const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
+  for (int fl = 0; fl < FB; ++fl) {
+    const int f = f0 + fl;
+    if (f >= F) break;
+    // the WM (x beta^2) rows, zero-padded to RMAX, are wave-uniform: scalar
+    // loads and SGPR operands (the padded terms add exact zeros)
+    const double *wr = WbR + (size_t)f * RMAX, *wl = WbL + (size_t)f * RMAX;
+    double sr = 0.0, sl = 0.0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) sr += wr[r] * hm[r];
+    if (stereo) {
+#pragma unroll
+      for (int r = 0; r < RMAX; ++r) sl += wl[r] * hm[r];
+    }
+    const size_t i = (size_t)f * N + n;
+    const double l = SLD(SF0[i]) * SLD(SPHI[i]);
+    SST(SMR[i], sr);
+    if (stereo) {
+      SST(SML[i], sl);
+      SST(hR[i], fmax(sr + aR2 * l, kSimmEps));
+      SST(hL[i], fmax(l * aL2 + sl, kSimmEps));
+    } else {
+      SST(hR[i], fmax(l + sr, kSimmEps));
+    }
+  }
+}
+
 // stereo: X = SX/max(h^2, eps), Y = 1/max(h, eps)             (:747-753)
 // mono:   Y = 1/max(h, eps), X = (Y*SX)/max(h, eps)               (:318-321)
 __global__ void k_simm_xy(const double *__restrict__ h, const double *__restrict__ SX,
@@ -572,6 +621,23 @@ __global__ void k_rowscale(double *__restrict__ X, const double *__restrict__ s,
 }
 
 // WMb = WM * beta^2 (column scale), F x R
+// W[f][r] (r < R) = WM[f][r] (* b[r]^2 when b), zero for R <= r < RP
+__global__ void k_wm_beta_pad(const double *__restrict__ WM, const double *__restrict__ b,
+                              double *__restrict__ W, int F, int R, int RP) {
+  GRID_STRIDE(i, (size_t)F * RP) {
+    const int f = i / RP, r = i % RP;
+    double w = 0.0;
+    if (r < R) {
+      w = WM[(size_t)f * R + r];
+      if (b) {
+        const double bb = b[r];
+        w = w * (bb * bb);
+      }
+    }
+    W[i] = w;
+  }
+}
+
 __global__ void k_wm_beta(const double *__restrict__ WM, const double *__restrict__ b,
                           double *__restrict__ WMb, int F, int R) {
   GRID_STRIDE(i, (size_t)F * R) {
@@ -721,10 +787,11 @@ struct simm_ctx {
   hipStream_t stream = nullptr;
   rocblas_handle blas = nullptr;  // bound to `stream`: the NF0-sized plain GEMMs
   int use_blas = 1;               // FASST_SIMM_BLAS=0: k_gemm instead (A/B only)
+  int fuse_sm = 1;                // FASST_SIMM_FUSE_SM=0: unfused SM refresh (A/B only)
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
   DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
-  DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, NP0, NP1, WMb, s_col, sg, sw;
+  DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, NP0, NP1, WMb, WMb2, s_col, sg, sw;
   DBuf<double> hpart, hrows, apart, bd, gwork, P0, P1, P2, P3, RN0, RN1, reco;
 };
 
@@ -849,6 +916,29 @@ int refresh_sm(simm_ctx *c) {
   return gemm_nn(c, c->WM.p, c->R, c->HM.p, c->N, c->SMR.p, c->N, c->F, c->N, c->R);
 }
 
+int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi);
+
+// refresh_sm + refresh_hat(c, nullptr, 0) as one fused pass when R is small
+constexpr int kSmRmax = 48;
+int refresh_sm_hat(simm_ctx *c) {
+  if (c->R <= kSmRmax && c->fuse_sm) {
+    const size_t FRP = (size_t)c->F * kSmRmax;
+    k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->stereo ? c->bR.p : nullptr,
+                                                     c->WMb.p, c->F, c->R, kSmRmax);
+    if (c->stereo)
+      k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->bL.p, c->WMb2.p, c->F, c->R,
+                                                       kSmRmax);
+    const dim3 grid((c->N + 255) / 256, (c->F + 15) / 16);
+    k_simm_sm_refresh<kSmRmax><<<grid, 256, 0, c->stream>>>(
+        c->WMb.p, c->WMb2.p, c->HM.p, c->SF0.p, c->SPHI.p, c->alpha.p, c->SMR.p, c->SML.p,
+        c->hR.p, c->hL.p, c->F, c->N, c->R, c->stereo);
+    FASST_LAUNCH_CHECK();
+    return FASST_OK;
+  }
+  int st = refresh_sm(c);
+  return st ? st : refresh_hat(c, nullptr, 0);
+}
+
 int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi) {
   k_simm_refresh<<<egrid((size_t)c->F * c->N), 256, 0, c->stream>>>(
       c->SF0.p, c->SPHI.p, c->WPHI.p, c->HPHI.p, colscale, c->SMR.p, c->SML.p, c->alpha.p,
@@ -926,8 +1016,7 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     k_mu_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
                                                             (size_t)R * N, omega, 1);
   }
-  if ((st = refresh_sm(c))) return st;
-  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  if ((st = refresh_sm_hat(c))) return st;
   // ---- HGAMMA (:776-823 / :335-350)
   if (update_hgamma) {
     k_hgamma_rows<<<(F + 3) / 4, 256, 0, c->stream>>>(c->SF0.p, c->hR.p, c->hL.p, c->SXR.p,
@@ -959,8 +1048,7 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     else
       k_colscale<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->sw.p, R, N);  // R == N
   }
-  if ((st = refresh_sm(c))) return st;
-  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  if ((st = refresh_sm_hat(c))) return st;
   if (!c->stereo) return FASST_OK;
   // ---- alpha (:872-906)
   k_alpha_partial<<<c->nb_alpha, 256, 0, c->stream>>>(c->SF0.p, c->SPHI.p, c->hR.p, c->hL.p,
@@ -977,8 +1065,7 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p + (size_t)R * N, c->HM.p, c->bd.p + 2 * R, N);
   k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p + (size_t)R * N, c->HM.p, c->bd.p + 3 * R, N);
   k_beta_update<<<1, 64, 0, c->stream>>>(c->bd.p, c->bR.p, c->bL.p, R, omega);
-  if ((st = refresh_sm(c))) return st;
-  return refresh_hat(c, nullptr, 0);
+  return refresh_sm_hat(c);
 }
 
 }  // namespace
@@ -1016,6 +1103,7 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
     st = FASST_ERR_DEVICE;
   }
   if (const char *v = getenv("FASST_SIMM_BLAS")) c->use_blas = atoi(v);
+  if (const char *v = getenv("FASST_SIMM_FUSE_SM")) c->fuse_sm = atoi(v);
   size_t gw = 0;
   gw = std::max(gw, gemm_workspace(NF0, N, F, 2));
   gw = std::max(gw, gemm_workspace(F, N, NF0, 1));
@@ -1050,7 +1138,8 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   SA(T3, stereo ? FN : 1);
   SA(NP0, (size_t)NF0 * N);
   SA(NP1, (size_t)NF0 * N);
-  SA(WMb, (size_t)F * R);
+  SA(WMb, (size_t)F * std::max(R, 48));  // (48 = kSmRmax: padded rows of the fused refresh)
+  SA(WMb2, (size_t)F * std::max(R, 48));
   SA(s_col, N);
   SA(sg, K);
   SA(sw, R);
