@@ -4,12 +4,13 @@
 // Frame n needs every state's cum[., n-1], so frames are sequential; the
 // parallelism is over target states s (and over the source states s' of
 // each reduction):
-//   k_vt_frame     one launch per frame (kernel boundaries are the frame
-//                  barrier -- no in-launch grid synchronisation): one wave per
-//                  target s, lanes stride over s' with coalesced reads of the
-//                  target-major transition row TT[s][.] (L2-resident across
-//                  frames: S^2 doubles = 9.5 MB at S = 1092, 1.2 MB per XCD),
-//                  then a 64-lane (value, index) butterfly.
+//   k_vt_frame4    one launch per frame (kernel boundaries are the frame
+//                  barrier -- no in-launch grid synchronisation): 4 waves per
+//                  target s, each over a quarter of s' with coalesced reads of
+//                  the target-major transition row TT[s][.] (L2-resident
+//                  across frames: S^2 doubles = 9.5 MB at S = 1092, 1.2 MB per
+//                  XCD), 64-lane (value, index) butterflies, then the 4 wave
+//                  results folded in source order.
 //   k_vt_block     small S (the matrix fits in LDS): ONE workgroup runs every
 //                  frame with TT and the two cum vectors in LDS, 16 waves over
 //                  the targets, a workgroup barrier per frame.
@@ -84,20 +85,60 @@ __global__ void k_vt_init(const double *__restrict__ prior, const double *__rest
   if (s < S) cum[s] = prior[s] + logd0[s];   // pyx :60-63
 }
 
-__global__ __launch_bounds__(256) void k_vt_frame(const double *__restrict__ TT, long ldt,
-                                                  const double *__restrict__ cum_prev,
-                                                  double *__restrict__ cum_next,
-                                                  const double *__restrict__ logd_n,
-                                                  int *__restrict__ ante_n, int S) {
-  const int lane = threadIdx.x & 63;
-  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s >= S) return;
-  double bv;
-  int bi;
-  vt_argmax(cum_prev, TT + (size_t)s * ldt, S, lane, bv, bi);
+// One frame step (large S): a block of NW waves per target s; wave q reduces
+// the source range [q*Q, (q+1)*Q) over coalesced reads of the target-major
+// row TT[s][.] (L2-resident across frames), thread 0 folds the NW (value,
+// index) results in source order, so ties still resolve to the first maximal
+// source and a NaN at s' = 0 (wave 0's range) still sticks.  NW = 4 measured
+// best at S = 1092 (125 ms per 20000 frames vs 188 ms with one wave per
+// target; 2 / 8 / 16 waves: 140 / 171 / 303 ms).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_vt_frame4(const double *__restrict__ TT, long ldt,
+                                                   const double *__restrict__ cum_prev,
+                                                   double *__restrict__ cum_next,
+                                                   const double *__restrict__ logd_n,
+                                                   int *__restrict__ ante_n, int S) {
+  __shared__ double s_v[NW];
+  __shared__ int s_i[NW];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int s = blockIdx.x;
+  const int Q = (S + NW - 1) / NW;
+  const int lo = q * Q, hi = min(S, lo + Q);
+  const double *row = TT + (size_t)s * ldt;
+  double bv = -INFINITY;
+  int bi = INT_MAX;
+  for (int base = lo; base < hi; base += 64 * kVtBatch) {
+    double v[kVtBatch];
+#pragma unroll
+    for (int u = 0; u < kVtBatch; ++u) {
+      const int sp = base + u * 64 + lane;
+      v[u] = sp < hi ? cum_prev[sp] + row[sp] : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < kVtBatch; ++u) {
+      const int sp = base + u * 64 + lane;
+      if (sp < hi) vt_better(bv, bi, v[u], sp);
+    }
+  }
+  vt_wave_reduce(bv, bi);
+  if (q == 0) {
+    const double v0 = cum_prev[0] + row[0];
+    if (v0 != v0) {  // NaN at s' = 0: nothing compares greater (pyx :77)
+      bv = v0;
+      bi = 0;
+    }
+  }
   if (lane == 0) {
-    cum_next[s] = bv + logd_n[s];   // pyx :83-85
-    ante_n[s] = bi;
+    s_v[q] = bv;
+    s_i[q] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v = s_v[0];
+    int i = s_i[0];
+    for (int w = 1; w < NW; ++w) vt_better(v, i, s_v[w], s_i[w]);
+    cum_next[s] = v + logd_n[s];   // pyx :83-85
+    ante_n[s] = i;
   }
 }
 
@@ -268,12 +309,11 @@ int viterbi_tracking(int device, int n_states, int n_frames, const double *log_d
     g_vt_kind = 1;
     k_vt_init<<<(S + 255) / 256, 256>>>(dprior.p, dDT.p, cum.p, S);
     FASST_LAUNCH_CHECK();
-    const int grid = (S + 3) / 4;
     for (int n = 1; n < N; ++n) {
       const double *cp = cum.p + ((n - 1) & 1) * Sp;
       double *cn = cum.p + (n & 1) * Sp;
-      k_vt_frame<<<grid, 256>>>(dTT.p, Sp, cp, cn, dDT.p + (size_t)n * Sp, ante.p + (size_t)n * Sp,
-                                S);
+      k_vt_frame4<4><<<S, 256>>>(dTT.p, Sp, cp, cn, dDT.p + (size_t)n * Sp,
+                                 ante.p + (size_t)n * Sp, S);
     }
     FASST_LAUNCH_CHECK();
     FASST_HIP(hipMemcpyAsync(clast.p, cum.p + ((N - 1) & 1) * Sp, S * sizeof(double),
