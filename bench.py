@@ -137,11 +137,16 @@ def main():
 
     world, rank, local, seed, device = rank_setup()
     dist = None
+    # RCCL ("nccl") is the product; FASST_BENCH_BACKEND=gloo rehearses the
+    # multi-rank path with more ranks than GPUs (ranks share cards round-robin)
+    backend = os.environ.get("FASST_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if backend != "nccl":
+            device = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend)
 
     m = build_model(seed=seed, device=device, T=args.T)
     eng = m._engine
@@ -169,7 +174,8 @@ def main():
             m._restart_tw(mask, order)
             order, Ks, conv = m._upload()
     barrier_sync()
-    dt = max_over_ranks(time.perf_counter() - t0, dist, "cuda:%d" % local)
+    dt = max_over_ranks(time.perf_counter() - t0, dist,
+                        "cuda:%d" % device if backend == "nccl" else "cpu")
 
     # per-kernel HIP-event timing on the engine's stream (separate, untimed pass)
     eng.set_profiling(True)
