@@ -98,6 +98,17 @@ int fasst_run(fasst_ctx *ctx, int n_iter, const double *psd, double omega,
  * STFT; S out complex128 [J][2][F][T].                                       */
 int fasst_wiener_images(fasst_ctx *ctx, const double *psd, const double *X, double *S);
 
+/* separate_comps up to the waveforms it writes (audioModel.py:1088-1233):
+ * the Wiener images above, then the per-source, per-channel iSTFT
+ * (tftransforms/stft.py:71-131, window / analysis_window as STFT's
+ * synthWindow / window) of each image without leaving device memory.  Needs
+ * the resident STFT (fasst_set_audio / fasst_set_stft) and nfft/2+1 == F.
+ * y out float64 [J][2][len], len = hop*(T-1) + wlen - wlen/2 (istft's length
+ * before the caller's [:datalen] trim).                                      */
+int fasst_separate_waveforms(fasst_ctx *ctx, const double *psd, const double *window,
+                             const double *analysis_window, int wlen, int nfft, int hop,
+                             double *y);
+
 /* Per-kernel timing with HIP events recorded on the context's stream
  * (used by bench.py for the roofline of the dominant kernel).
  * fasst_kernel_times returns the number of kernel slots and fills the mean

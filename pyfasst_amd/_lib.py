@@ -56,6 +56,8 @@ SIGNATURES = {
     "fasst_renormalize": (ctypes.c_int, [_vp, _ip]),
     "fasst_run": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_double, _dp, _ip, _ip]),
     "fasst_wiener_images": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
+    "fasst_separate_waveforms": (ctypes.c_int, [_vp, _dp, _dp, _dp, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, _dp]),
     "fasst_stft": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_int, _dp, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_int, _dp, _ip]),
     "fasst_istft": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, ctypes.c_int,

@@ -394,6 +394,25 @@ class FASST(object):
     def separated_images(self, spec_comp_ind=None):
         """STFT-domain Wiener images S[n, c] = sum_c2 WG_n[c, c2] X[c2], as the
         reference computes before its iSTFT (audioModel.py:1136-1214)."""
+        src_spat, psd = self._separation_plan(spec_comp_ind)
+        S = self._engine.wiener_images(psd)
+        return S[src_spat]
+
+    def separated_waveforms(self, spec_comp_ind=None):
+        """The per-source, per-channel iSTFT of separated_images() without the
+        images leaving the GPU (STFT transform only): [n, channel, sample],
+        trimmed to the input length as tft.invertTransform() does
+        (audioModel.py:1187-1217, tftransforms/stft.py:71-131)."""
+        t = self.tft
+        if getattr(t, 'transformname', None) != 'stft':
+            raise NotImplementedError("device-resident separation needs the STFT transform "
+                                      "(use separated_images() + tft.invertTransform())")
+        src_spat, psd = self._separation_plan(spec_comp_ind)
+        Y = self._engine.separate_waveforms(psd, t.synthWindow, t.window, t.ftlen, t.fthop)
+        return Y[src_spat][:, :, :t.datalen_init]
+
+    def _separation_plan(self, spec_comp_ind):
+        """(spatial component of each output source, last annealed PSD)."""
         if spec_comp_ind is None:
             spec_comp_ind = {}
             for spec_ind in range(len(self.spec_comps)):
@@ -409,8 +428,7 @@ class FASST(object):
         if len(set(src_spat)) != len(src_spat) or len(src_spat) != len(order):
             raise NotImplementedError("sources must map one-to-one to spatial components")
         psd = np.asarray(self.noise['PSD'], dtype=np.float64) * np.ones(self.nbFreqsSigRepr)
-        S = self._engine.wiener_images(psd)
-        return S[src_spat]
+        return src_spat, psd
 
     def separate_comps(self, dir_results=None, spec_comp_ind=None, suffix=None):
         """Wiener-filter and write one WAV per source (audioModel.py:1088-1236)."""
@@ -419,19 +437,27 @@ class FASST(object):
         nc = self.audioObject.channels
         if nc != 2:
             raise NotImplementedError()
-        S = self.separated_images(spec_comp_ind)
-        nbSources = S.shape[0]
+        if getattr(self.tft, 'transformname', None) == 'stft':
+            Y = self.separated_waveforms(spec_comp_ind)   # iSTFT on the device
+            S = None
+            nbSources = Y.shape[0]
+        else:
+            S = self.separated_images(spec_comp_ind)
+            nbSources = S.shape[0]
         if not hasattr(self, "files"):
             self.files = {}
         self.files['spat_comp'] = []
         fileroot = self.audioObject.filename.split('/')[-1][:-4]
         for n in range(nbSources):
-            ndata = []
-            for chan1 in range(nc):
-                self.tft.transfo = S[n, chan1]
-                ndata.append(self.tft.invertTransform())
-                del self.tft.transfo
-            ndata = np.array(ndata).T
+            if S is None:
+                ndata = Y[n].T
+            else:
+                ndata = []
+                for chan1 in range(nc):
+                    self.tft.transfo = S[n, chan1]
+                    ndata.append(self.tft.invertTransform())
+                    del self.tft.transfo
+                ndata = np.array(ndata).T
             _suffix = ''
             if suffix is not None and n in suffix:
                 _suffix = '_' + suffix[n]

@@ -951,7 +951,7 @@ int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi) {
 // (:578-585 / :229-233)
 int rebuild_model(simm_ctx *c) {
   int st;
-  const int F = c->F, N = c->N, K = c->K;
+  const int F = c->F, K = c->K;
   if ((st = gemm_nn(c, c->WGAMMA.p, c->P, c->HGAMMA.p, K, c->WPHI.p, K, F, K, c->P))) return st;
   if ((st = sf0_gemm(c))) return st;
   if ((st = refresh_sm(c))) return st;

@@ -664,6 +664,85 @@ int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double
   return FASST_OK;
 }
 
+int fasst_separate_waveforms(fasst_ctx *c, const double *psd, const double *window,
+                             const double *analysis_window, int wlen, int nfft, int hop,
+                             double *y) {
+  if (!c || !c->configured || !psd || !window || !y) {
+    set_error("fasst_separate_waveforms: context not configured");
+    return FASST_ERR_SHAPE;
+  }
+  int st = check_fft(nfft, wlen, hop);
+  if (st) return st;
+  if (nfft / 2 + 1 != c->F) {
+    set_error("fasst_separate_waveforms: nfft=%d gives %d bins, the model has F=%d", nfft,
+              nfft / 2 + 1, c->F);
+    return FASST_ERR_SHAPE;
+  }
+  if (!c->have_X) {
+    set_error("fasst_separate_waveforms: no STFT available (set_audio / set_stft)");
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(c->device);
+  if ((st = fft_smem(nfft))) return st;
+  const int J = c->J, T = c->T;
+  const size_t plane = (size_t)c->Tp * c->Fp;
+  const int len_out = hop * (T - 1) + wlen - wlen / 2;  // istft (stft.py:108-129)
+  DBuf<double> dpsd, coef, dw, daw, dframes, dy;
+  DBuf<int> droff;
+  DBuf<double2> dS, dtw;
+  if ((st = dpsd.alloc(c->Fp)) || (st = coef.alloc((size_t)J * 4 * c->Fp)) ||
+      (st = droff.alloc(kMaxJ + 1)) || (st = dS.alloc((size_t)J * 2 * plane)) ||
+      (st = dw.alloc(wlen)) || (st = daw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)) ||
+      (st = dframes.alloc((size_t)T * wlen)) || (st = dy.alloc((size_t)J * 2 * len_out)))
+    return st;
+  auto tw = twiddles(nfft, +1);
+  FASST_HIP(hipMemcpyAsync(dpsd.p, psd, c->F * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(droff.p, c->roff, (J + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(dw.p, window, (size_t)wlen * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+  FASST_HIP(hipMemcpyAsync(daw.p, analysis_window ? analysis_window : window,
+                           (size_t)wlen * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpyAsync(dtw.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice,
+                           c->stream));
+  if ((st = build_inst_A(c))) return st;
+  if ((st = launch_w_old(c))) return st;
+  k_mixcoef<<<(c->Fp + 255) / 256, 256, 0, c->stream>>>(c->A.p, coef.p, J, droff.p, c->F, c->Fp);
+  FASST_LAUNCH_CHECK();
+  WArgs w;
+  w.TW = c->TW.p;
+  w.Wkf = c->Wkf.p;
+  w.coef = coef.p;
+  w.psd = dpsd.p;
+  w.X = c->X.p;
+  w.S = dS.p;
+  w.F = c->F;
+  w.T = c->T;
+  w.Fp = c->Fp;
+  w.Tp = c->Tp;
+  w.KP = c->KP;
+  const dim3 grid(c->ntt, c->nft);
+  switch (J) {
+    case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
+    case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
+    case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
+    default: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+  }
+  FASST_LAUNCH_CHECK();
+  // each image's frames are rows of its [Tp][Fp] plane: iSTFT straight from
+  // HBM (k_istft_frames takes the row stride), only waveforms leave the card
+  for (int q = 0; q < 2 * J; ++q) {
+    k_istft_frames<<<T, 256, nfft * sizeof(double2), c->stream>>>(
+        dS.p + (size_t)q * plane, c->Fp, dw.p, wlen, dtw.p, nfft, ilog2(nfft), dframes.p);
+    FASST_LAUNCH_CHECK();
+    k_ola<<<(len_out + 255) / 256, 256, 0, c->stream>>>(dframes.p, T, wlen, hop, dw.p, daw.p,
+                                                        dy.p + (size_t)q * len_out, len_out);
+    FASST_LAUNCH_CHECK();
+  }
+  FASST_HIP(hipMemcpyAsync(y, dy.p, dy.n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
 int fasst_inv_herm_mat_2d(int device, int n, const double *diag, const double *off,
                           double *inv_diag, double *inv_off, double *det) {
   if (n < 0 || (n > 0 && (!diag || !off || !inv_diag || !inv_off || !det))) return FASST_ERR_SHAPE;

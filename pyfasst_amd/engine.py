@@ -131,6 +131,19 @@ class Engine(object):
         n = lib.fasst_kernel_times(self._h, dptr(ms), cnt, nk)
         return {lib.fasst_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(n) if cnt[i]}
 
+    def separate_waveforms(self, psd, window, analysis_window, nfft, hop):
+        """Wiener images + per-image iSTFT on the device: [J, 2, len] float64."""
+        psd = np.ascontiguousarray(psd, dtype=np.float64)
+        w = np.ascontiguousarray(window, dtype=np.float64)
+        aw = np.ascontiguousarray(analysis_window, dtype=np.float64)
+        J = len(self.structure[0])
+        n = int(hop) * (self.T - 1) + w.size - w.size // 2
+        out = np.empty((J, 2, n))
+        check(lib.fasst_separate_waveforms(self._h, dptr(psd), dptr(w), dptr(aw), w.size,
+                                           int(nfft), int(hop), dptr(out)),
+              "fasst_separate_waveforms")
+        return out
+
     def wiener_images(self, psd, X=None):
         psd = np.ascontiguousarray(psd, dtype=np.float64)
         J = len(self.structure[0])

@@ -128,6 +128,14 @@ def test_em_end_to_end_vs_reference(case, tmp_path):
     S = m.separated_images()
     assert rel(np.abs(S), np.abs(g['images'])) < TIGHT
     assert rel(np.abs(S), np.abs(g['images'])) < BAR
+    # the device-resident separation (images never leave HBM) is the per-image
+    # iSTFT of those images, bit for bit (same kernels, same order)
+    Y = m.separated_waveforms() if m.tft.transformname == 'stft' else None
+    for n in range(S.shape[0] if Y is not None else 0):
+        for c in range(2):
+            m.tft.transfo = S[n, c]
+            np.testing.assert_array_equal(Y[n, c], m.tft.invertTransform())
+            del m.tft.transfo
     # separated WAV files: int16 after iSTFT, identical up to 1 LSB
     m.separate_spat_comps(dir_results=str(tmp_path))
     for n, fn in enumerate(m.files['spat_comp']):
