@@ -93,6 +93,41 @@ def _blas_threads():
         return 1
 
 
+def bench_separate(steps, warmup):
+    """Wiener separation + iSTFT at C3 (audioModel.py:1088-1233): the device-
+    resident path (fasst_separate_waveforms, only the 8 waveforms cross PCIe)
+    vs the images path (fasst_wiener_images: J x 2 x F x T complex images to
+    the host, the per-image iSTFT after).  Host-inclusive wall times."""
+    sys.path.insert(0, ROOT)
+    import bench as B
+    m = B.build_model(seed=0, device=0)
+    eng = m._engine
+    m._upload()
+    nfft, hop = 4096, 512
+    w = np.hanning(nfft)
+    psd = np.full(m.nbFreqsSigRepr, 1e-6)
+    for _ in range(max(warmup, 1)):
+        eng.separate_waveforms(psd, w, w, nfft, hop)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        Y = eng.separate_waveforms(psd, w, w, nfft, hop)
+    dt = (time.perf_counter() - t0) / steps
+    eng.wiener_images(psd)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        S = eng.wiener_images(psd)
+    di = (time.perf_counter() - t1) / steps
+    J = Y.shape[0]
+    return {"metric": "FASST separation (Wiener images + iSTFT) per clip, host-inclusive",
+            "value": round(dt * 1e3, 3), "unit": "ms", "higher_is_better": False,
+            "steps": steps, "warmup": warmup, "dtype": "f64",
+            "data": "synthetic C3 model (bench.py build_model, seed 0)",
+            "config": {"workload": "J=%d sources x 2 channels, F=%d, T=%d, nfft %d hop %d"
+                                   % (J, m.nbFreqsSigRepr, m.nbFramesSigRepr, nfft, hop)},
+            "waveform_bytes_to_host": int(Y.nbytes),
+            "images_path_ms": round(di * 1e3, 3), "image_bytes_to_host": int(S.nbytes)}
+
+
 def bench_nmf(steps, warmup, F=1025, N=2000, K=64, seed=0):
     from pyfasst_amd import _lib
     from pyfasst_amd.tools.nmf import _NmfContext
@@ -236,11 +271,13 @@ def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi", "wf0"), required=True)
+    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi", "wf0", "separate"),
+                    required=True)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
-    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt, "viterbi": bench_viterbi, "wf0": bench_wf0}[a.workload]
+    fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt, "viterbi": bench_viterbi,
+          "wf0": bench_wf0, "separate": bench_separate}[a.workload]
     print(json.dumps(fn(a.steps, a.warmup)), flush=True)
 
 
