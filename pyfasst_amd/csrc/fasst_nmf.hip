@@ -68,6 +68,259 @@ __global__ void k_nmf_h(double *__restrict__ H, const double *__restrict__ num,
     H[i] *= num[i] / fmax(den[i], kNmfEps);
 }
 
+__device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Fused IS-NMF contractions (K a multiple of 16, <= 64): the model hat = W H
+// is recomputed tile by tile on the MFMA pipe and never stored, the ratios
+// X = SX / max(hat^2, eps), Y = 1 / max(hat, eps) stay in registers, and the
+// accumulator-as-operand layout of 16x16x4 feeds them straight into the
+// contraction (as the FASST FB / TW contractions, fasst_em.hip).  Each
+// 4-wave workgroup splits its reduction range over its waves, folds the four
+// partials in LDS in wave order, and writes one partial per workgroup row to
+// `part` ([group][num / den][K][F or N]); the consumer (k_nmf_w_part /
+// k_nmf_h_part) sums the groups in index order: deterministic.
+template <int NT, int NKC>
+__device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT][NKC],
+                                               double *__restrict__ pn, double *__restrict__ pd,
+                                               int r0, int R, int wv, int lane) {
+  constexpr int NE = NT * NKC * 4;
+  __shared__ double red[2][NE][64];
+  const int fl = lane & 15, tq = lane >> 4;
+  for (int w = 0; w < 4; ++w) {
+    if (wv == w) {
+#pragma unroll
+      for (int p = 0; p < NT; ++p)
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int e = (p * NKC + kc) * 4 + m;
+            double a = num[p][kc][m], b = den[p][kc][m];
+            if (w) {
+              a = red[0][e][lane] + a;
+              b = red[1][e][lane] + b;
+            }
+            if (w < 3) {
+              red[0][e][lane] = a;
+              red[1][e][lane] = b;
+            } else {
+              const int r = r0 + p * 16 + tq + 4 * m, k = kc * 16 + fl;
+              if (r < R) {
+                pn[(size_t)k * R + r] = a;
+                pd[(size_t)k * R + r] = b;
+              }
+            }
+          }
+    }
+    __syncthreads();
+  }
+}
+
+// W update (nmf.py:39-44): numT[k][f] = sum_t H[k][t] X[f][t], denT with Y.
+// A workgroup owns FPW 16-bin tiles and 4 frame chunks (one per wave); the
+// W rows are loop-invariant B operands of the hat tiles.
+template <int NKC, int FPW>
+__global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
+                                                  const double *__restrict__ H,
+                                                  const double *__restrict__ SXt,
+                                                  double *__restrict__ part, int F, int N, int tpc) {
+  constexpr int NKS = 4 * NKC, K = 16 * NKC;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
+  const int ft0 = blockIdx.x * FPW, nft = (F + 15) / 16, ntt = (N + 15) / 16;
+  double wk[FPW][NKS];
+#pragma unroll
+  for (int p = 0; p < FPW; ++p) {
+    const int f = (ft0 + p) * 16 + fl;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) wk[p][s] = f < F ? W[(size_t)f * K + 4 * s + tq] : 0.0;
+  }
+  d4 num[FPW][NKC], den[FPW][NKC];
+#pragma unroll
+  for (int p = 0; p < FPW; ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+  const int tb = (blockIdx.y * 4 + wv) * tpc, te = min(tb + tpc, ntt);
+  for (int tt = tb; tt < te; ++tt) {
+    const int t0 = tt * 16;
+    double th[NKS], hb[4][NKC];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) th[s] = t0 + fl < N ? H[(size_t)(4 * s + tq) * N + t0 + fl] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 4 * i;
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) hb[i][kc] = t < N ? H[(size_t)(kc * 16 + fl) * N + t] : 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      if (ft0 + p >= nft) break;  // wave-uniform
+      const int f = (ft0 + p) * 16 + fl;
+      d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;  // hat at (frame t0+tq+4i, bin f)
+#pragma unroll
+      for (int s = 0; s < NKS; s += 2) {
+        v = nmfma(th[s], wk[p][s], v);
+        v2 = nmfma(th[s + 1], wk[p][s + 1], v2);
+      }
+      v += v2;
+      double x[4], y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = t0 + tq + 4 * i;
+        const bool ok = f < F && t < N;
+        const double h = v[i];
+        const double sx = ok ? SXt[(size_t)t * F + f] : 0.0;
+        x[i] = ok ? sx / fmax(h * h, kNmfEps) : 0.0;
+        y[i] = ok ? 1.0 / fmax(h, kNmfEps) : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+          num[p][kc] = nmfma(x[i], hb[i][kc], num[p][kc]);
+          den[p][kc] = nmfma(y[i], hb[i][kc], den[p][kc]);
+        }
+    }
+  }
+  const size_t slab = (size_t)K * F;
+  double *pn = part + (size_t)blockIdx.y * 2 * slab;
+  nmf_fold_store<FPW, NKC>(num, den, pn, pn + slab, ft0 * 16, F, wv, lane);
+}
+
+// H update (nmf.py:53-59): num[k][t] = sum_f W[f][k] X[f][t], den with Y,
+// hat from the updated W and the rescaled H (hs = W column sums from the W
+// update, applied on load as k_nmf_hscale would; null when W is frozen).  A
+// workgroup owns TPW 16-frame tiles and 4 bin chunks (one per wave).
+template <int NKC, int TPW>
+__global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
+                                                  const double *__restrict__ H,
+                                                  const double *__restrict__ hs,
+                                                  const double *__restrict__ SX,
+                                                  double *__restrict__ part, int F, int N, int fpc) {
+  constexpr int NKS = 4 * NKC, K = 16 * NKC;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
+  const int tt0 = blockIdx.x * TPW, nft = (F + 15) / 16, ntt = (N + 15) / 16;
+  double bt[TPW][NKS];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    const int t = (tt0 + p) * 16 + fl;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const double h = t < N ? H[(size_t)(4 * s + tq) * N + t] : 0.0;
+      bt[p][s] = hs ? h * hs[4 * s + tq] : h;
+    }
+  }
+  d4 num[TPW][NKC], den[TPW][NKC];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+  const int fb = (blockIdx.y * 4 + wv) * fpc, fe = min(fb + fpc, nft);
+  for (int ft = fb; ft < fe; ++ft) {
+    const int f0 = ft * 16;
+    double ao[NKS], bw[4][NKC];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) ao[s] = f0 + fl < F ? W[(size_t)(f0 + fl) * K + 4 * s + tq] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + 4 * i + tq;
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) bw[i][kc] = f < F ? W[(size_t)f * K + kc * 16 + fl] : 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < TPW; ++p) {
+      if (tt0 + p >= ntt) break;  // wave-uniform
+      const int t = (tt0 + p) * 16 + fl;
+      d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;  // hat at (bin f0+tq+4i, frame t)
+#pragma unroll
+      for (int s = 0; s < NKS; s += 2) {
+        v = nmfma(ao[s], bt[p][s], v);
+        v2 = nmfma(ao[s + 1], bt[p][s + 1], v2);
+      }
+      v += v2;
+      double x[4], y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = f0 + tq + 4 * i;
+        const bool ok = f < F && t < N;
+        const double h = v[i];
+        const double sx = ok ? SX[(size_t)f * N + t] : 0.0;
+        x[i] = ok ? sx / fmax(h * h, kNmfEps) : 0.0;
+        y[i] = ok ? 1.0 / fmax(h, kNmfEps) : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+          num[p][kc] = nmfma(x[i], bw[i][kc], num[p][kc]);
+          den[p][kc] = nmfma(y[i], bw[i][kc], den[p][kc]);
+        }
+    }
+  }
+  const size_t slab = (size_t)K * N;
+  double *pn = part + (size_t)blockIdx.y * 2 * slab;
+  nmf_fold_store<TPW, NKC>(num, den, pn, pn + slab, tt0 * 16, N, wv, lane);
+}
+
+// k_nmf_w over the fused path's group partials ([g][num / den][K][F])
+__global__ __launch_bounds__(256) void k_nmf_w_part(double *__restrict__ W,
+                                                    const double *__restrict__ part, int ng,
+                                                    double *__restrict__ s_out, int F, int K) {
+  __shared__ double s_red[256];
+  const int k = blockIdx.x;
+  const size_t slab = (size_t)K * F;
+  double acc = 0.0;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    const double *q = part + (size_t)k * F + f;
+    double n = q[0], d = q[slab];
+    for (int g = 1; g < ng; ++g) {
+      n += q[(size_t)g * 2 * slab];
+      d += q[(size_t)g * 2 * slab + slab];
+    }
+    const double w = W[(size_t)f * K + k] * (n / fmax(d, kNmfEps));
+    W[(size_t)f * K + k] = w;
+    acc += w;
+  }
+  s_red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
+    __syncthreads();
+  }
+  double s = s_red[0];
+  if (s == 0) s = 1.0;  // sumW[sumW==0] = 1. (nmf.py:46)
+  for (int f = threadIdx.x; f < F; f += 256) W[(size_t)f * K + k] /= s;
+  if (threadIdx.x == 0) s_out[k] = s;
+}
+
+// k_nmf_hscale + k_nmf_h over the group partials ([g][num / den][K][N])
+__global__ void k_nmf_h_part(double *__restrict__ H, const double *__restrict__ part, int ng,
+                             const double *__restrict__ hs, int K, int N) {
+  const size_t slab = (size_t)K * N;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slab;
+       i += (size_t)gridDim.x * blockDim.x) {
+    double n = part[i], d = part[slab + i];
+    for (int g = 1; g < ng; ++g) {
+      n += part[(size_t)g * 2 * slab + i];
+      d += part[(size_t)g * 2 * slab + slab + i];
+    }
+    const double h = hs ? H[i] * hs[i / N] : H[i];
+    H[i] = h * (n / fmax(d, kNmfEps));
+  }
+}
+
+// out[c][r] = in[r][c] for an R x C matrix (row-major), 16 x 16 LDS tiles
+__global__ void k_nmf_transpose(const double *__restrict__ in, double *__restrict__ out, int R,
+                                int C) {
+  __shared__ double tile[16][17];
+  const int c0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  if (r0 + ty < R && c0 + tx < C) tile[ty][tx] = in[(size_t)(r0 + ty) * C + c0 + tx];
+  __syncthreads();
+  if (c0 + ty < C && r0 + tx < R) out[(size_t)(c0 + ty) * R + r0 + tx] = tile[tx][ty];
+}
+
 }  // namespace fasst
 
 using namespace fasst;
@@ -77,6 +330,9 @@ struct nmf_ctx {
   hipStream_t stream = nullptr;
   int F = 0, N = 0, K = 0;
   DBuf<double> SX, W, H, hat, X, Y, numT, denT, num, den, s, work;
+  // fused path (K % 16 == 0, K <= 64): transposed copies and chunk partials
+  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1;
+  DBuf<double> SXt, part;
 };
 
 namespace {
@@ -95,9 +351,41 @@ int model_xy(nmf_ctx *c) {
   return FASST_OK;
 }
 
+constexpr int kNmfFPW = 2, kNmfTPW = 2, kNmfCUs = 256;
+
+template <int NKC>
+static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
+  const int F = c->F, N = c->N, K = c->K;
+  const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
+  if (update_w) {
+    k_nmf_wnum<NKC, kNmfFPW><<<dim3((nft + kNmfFPW - 1) / kNmfFPW, c->ng_w), 256, 0, c->stream>>>(
+        c->W.p, c->H.p, c->SXt.p, c->part.p, F, N, c->tpc_w);
+    k_nmf_w_part<<<K, 256, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
+  }
+  const double *hs = update_w ? c->s.p : nullptr;
+  if (update_h) {
+    k_nmf_hnum<NKC, kNmfTPW><<<dim3((ntt + kNmfTPW - 1) / kNmfTPW, c->ng_h), 256, 0, c->stream>>>(
+        c->W.p, c->H.p, hs, c->SX.p, c->part.p, F, N, c->fpc_h);
+    k_nmf_h_part<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->part.p, c->ng_h, hs, K,
+                                                                N);
+  } else if (update_w) {
+    k_nmf_hscale<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->s.p, K, N);
+  }
+}
+
 int nmf_iteration(nmf_ctx *c, int update_w, int update_h) {
   int st;
   const int F = c->F, N = c->N, K = c->K;
+  if (c->fused) {
+    switch (K / 16) {
+      case 1: nmf_fused<1>(c, update_w, update_h); break;
+      case 2: nmf_fused<2>(c, update_w, update_h); break;
+      case 3: nmf_fused<3>(c, update_w, update_h); break;
+      default: nmf_fused<4>(c, update_w, update_h); break;
+    }
+    FASST_LAUNCH_CHECK();
+    return FASST_OK;
+  }
   if (update_w) {
     if ((st = model_xy(c))) return st;
     const double *Bs[2] = {c->X.p, c->Y.p};
@@ -153,6 +441,23 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
   if (!st) st = c->den.alloc((size_t)K * N);
   if (!st) st = c->s.alloc(K);
   if (!st) st = c->work.alloc(gw);
+  // fused path: 4-wave groups (one per CU at the kernels' occupancy of one
+  // wave per SIMD), as many groups as fit in one pass over the 256 CUs
+  c->fused = K % 16 == 0 && K <= 64;
+  if (const char *v = getenv("FASST_NMF_FUSED")) c->fused = c->fused && atoi(v) != 0;
+  if (c->fused) {
+    const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
+    const int uw = (nft + kNmfFPW - 1) / kNmfFPW, uh = (ntt + kNmfTPW - 1) / kNmfTPW;
+    int ng = std::max(1, std::min((ntt + 3) / 4, kNmfCUs / uw));
+    c->tpc_w = (ntt + 4 * ng - 1) / (4 * ng);
+    c->ng_w = ((ntt + c->tpc_w - 1) / c->tpc_w + 3) / 4;
+    ng = std::max(1, std::min((nft + 3) / 4, kNmfCUs / uh));
+    c->fpc_h = (nft + 4 * ng - 1) / (4 * ng);
+    c->ng_h = ((nft + c->fpc_h - 1) / c->fpc_h + 3) / 4;
+    const size_t np = std::max((size_t)c->ng_w * 2 * K * F, (size_t)c->ng_h * 2 * K * N);
+    if (!st) st = c->SXt.alloc(FN);
+    if (!st) st = c->part.alloc(np);
+  }
   if (st) {
     nmf_destroy(c);
     return st;
@@ -178,6 +483,9 @@ int nmf_set_data(nmf_ctx *c, const double *SX) {
   if (!c || !SX) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   FASST_HIP(hipMemcpyAsync(c->SX.p, SX, (size_t)c->F * c->N * 8, hipMemcpyHostToDevice, c->stream));
+  if (c->fused)  // frame-major copy: the W-update contraction reads 16 bins per row segment
+    k_nmf_transpose<<<dim3((c->N + 15) / 16, (c->F + 15) / 16), 256, 0, c->stream>>>(
+        c->SX.p, c->SXt.p, c->F, c->N);
   FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
 }

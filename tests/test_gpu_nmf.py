@@ -43,9 +43,11 @@ def test_nmf_decomp_init_golden():
         nmf.NMF_decomp_init(g['SX'], nbComps=4, niter=1, Hinit=np.ones((3, 3)))
 
 
-# config 2 (F=1025, T=2000, K=64: split-K on both contractions), ragged
-# tiles, a single component
-@pytest.mark.parametrize("F,N,K,niter", [(1025, 2000, 64, 3), (257, 301, 13, 6), (33, 17, 1, 4)])
+# config 2 (F=1025, T=2000, K=64: fused contractions), ragged tiles on the
+# fused path (K=16, 32, 48), the GEMM path (K=13, 80) and a single component
+@pytest.mark.parametrize("F,N,K,niter", [(1025, 2000, 64, 3), (257, 301, 13, 6), (33, 17, 1, 4),
+                                         (65, 40, 32, 4), (130, 77, 16, 3), (47, 211, 48, 3),
+                                         (100, 90, 80, 2)])
 def test_nmf_vs_oracle(F, N, K, niter):
     rs = np.random.RandomState(F + N)
     SX = rs.gamma(0.7, 1.0, size=(F, N)) * np.outer(rs.gamma(2, 1, F), np.ones(N))
