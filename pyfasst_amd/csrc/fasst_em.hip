@@ -167,6 +167,12 @@ struct EArgs {
 #ifndef ESTEP_MINB2
 #define ESTEP_MINB2 2
 #endif
+#ifndef ESTEP_IB1
+#define ESTEP_IB1 2
+#endif
+#ifndef ESTEP_IB2
+#define ESTEP_IB2 4
+#endif
 template <int J, int NKS, int RKU, int PART, int AB>
 __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_estep(const EArgs a) {
   HALT_GUARD(a.halt);
@@ -176,6 +182,7 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
   constexpr int NTOT = 4 * NP + 8 * J;
   constexpr int KP = 4 * NKS;
   constexpr int RK = RKU ? RKU : kMaxR;
+  constexpr int IB = PART == 1 ? ESTEP_IB1 : ESTEP_IB2;  // frames per LDS coefficient read
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *s_cr = smem;                     // [kMaxR][4][16]
   double *s_cj = s_cr + kMaxR * 4 * 16;    // [J][4][16]
@@ -275,20 +282,36 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
     d4 v[J];
     tile_v(tt, v, lofs);
     const double *cj = s_cj + lofs + fl;
+    // frames are taken IB at a time so that every per-bin LDS coefficient is
+    // read once per IB frames (LDS bandwidth, not VALU, bounded part 1 with
+    // one read per frame); the per-frame arithmetic and its order are unchanged
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int ib = 0; ib < 4; ib += IB) {
+    double sx[IB][4];
+#pragma unroll
+    for (int ii = 0; ii < IB; ++ii) {
+      sx[ii][0] = psd;
+      sx[ii][1] = psd;
+      sx[ii][2] = 0.0;
+      sx[ii][3] = 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double q = cj[(j * 4 + c) * 16];
+#pragma unroll
+        for (int ii = 0; ii < IB; ++ii) sx[ii][c] += q * v[j][ib + ii];
+      }
+    double nn[IB][4];
+#pragma unroll
+    for (int ii = 0; ii < IB; ++ii) {
+      const int i = ib + ii;
       const int t = t0 + tq + 4 * i;
       double V[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) V[j] = v[j][i];
-      double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        d0 += cj[(j * 4 + 0) * 16] * V[j];
-        d1 += cj[(j * 4 + 1) * 16] * V[j];
-        ore += cj[(j * 4 + 2) * 16] * V[j];
-        oim += cj[(j * 4 + 3) * 16] * V[j];
-      }
+      const double d0 = sx[ii][0], d1 = sx[ii][1], ore = sx[ii][2], oim = sx[ii][3];
       // inv_herm_mat_2d (signalTools.py:177-194)
       double det = d0 * d1 - (ore * ore + oim * oim);
       const double dg = det + kEps;
@@ -350,36 +373,52 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
           }
         }
       }
-      // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414),
-      // stored as rho = (hat_W / vm^2) * vm with vm = max(V, eps): the FB ratio
-      // of update_spectral_components (:1521-1575, N1) formed here, where V is
-      // already in registers, so the FB contraction needs no V recompute; the
-      // TW contraction recovers hat_W as rho * max(V_old, eps)
-      if (!(AB & 2)) {
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          double hw = 0.0;
-          const double v2 = V[j] * V[j];
-#pragma unroll
-          for (int qq = 0; qq < RK; ++qq) {
-            if (RKU || qq < rk[j]) {
-              const double *cr = s_cr + lofs + (r0[j] + qq) * 64 + fl;
-              const double qa = cr[0] * n00 + cr[16] * n11 + (cr[32] * n01r + cr[48] * n01i);
-              hw += fabs(v2 * qa + V[j]);
-            }
-          }
-          const double hwm = RKU == 1 ? hw : hw * inv_rk[j];
-          const double vm = fmax(V[j], kEps);
-          const double rv = rcp_nr(vm);
-          __builtin_nontemporal_store((hwm * (rv * rv)) * vm,
-                                      a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
-        }
-      } else {
+      nn[ii][0] = n00;
+      nn[ii][1] = n11;
+      nn[ii][2] = n01r;
+      nn[ii][3] = n01i;
+      if (AB & 2) {
         double sum = 0.0;
 #pragma unroll
         for (int j = 0; j < J; ++j) sum += V[j] * n00;
         a.hatW[(size_t)t * a.Fp + f] = sum;
       }
+    }
+    // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414),
+    // stored as rho = (hat_W / vm^2) * vm with vm = max(V, eps): the FB ratio
+    // of update_spectral_components (:1521-1575, N1) formed here, where V is
+    // already in registers, so the FB contraction needs no V recompute; the
+    // TW contraction recovers hat_W as rho * max(V_old, eps)
+    if (PART == 1 && !(AB & 2)) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        double hw[IB];
+#pragma unroll
+        for (int ii = 0; ii < IB; ++ii) hw[ii] = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < RK; ++qq) {
+          if (RKU || qq < rk[j]) {
+            const double *cr = s_cr + lofs + (r0[j] + qq) * 64 + fl;
+            const double c0 = cr[0], c1 = cr[16], c2 = cr[32], c3 = cr[48];
+#pragma unroll
+            for (int ii = 0; ii < IB; ++ii) {
+              const double Vj = v[j][ib + ii];
+              const double qa = c0 * nn[ii][0] + c1 * nn[ii][1] + (c2 * nn[ii][2] + c3 * nn[ii][3]);
+              hw[ii] += fabs((Vj * Vj) * qa + Vj);
+            }
+          }
+        }
+#pragma unroll
+        for (int ii = 0; ii < IB; ++ii) {
+          const double Vj = v[j][ib + ii];
+          const double hwm = RKU == 1 ? hw[ii] : hw[ii] * inv_rk[j];
+          const double vm = fmax(Vj, kEps);
+          const double rv = rcp_nr(vm);
+          __builtin_nontemporal_store((hwm * (rv * rv)) * vm,
+                                      a.hatW + ((size_t)j * a.Tp + t0 + tq + 4 * (ib + ii)) * a.Fp + f);
+        }
+      }
+    }
     }
     if (PART == 1) {  // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
       const unsigned long long b = __double_as_longlong(lm);
