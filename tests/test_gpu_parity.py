@@ -150,7 +150,8 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     from pyfasst_amd import synthetic
     from pyfasst_amd.audioObject import SpectralAudio
     am = _am()
-    X = synthetic.stereo_mixture(F, T, J=J, K_true=4, rank=rank, seed=seed)
+    X = synthetic.stereo_mixture(F, T, J=J, K_true=4, rank=rank if np.isscalar(rank) else 2,
+                                 seed=seed)
     np.random.seed(1)
     m = am.MultiChanNMFConv(SpectralAudio(X=X), nbComps=J, nbNMFComps=K, spatial_rank=rank,
                             iter_num=iters, wlen=2 * (F - 1), hopsize=(F - 1) // 2)
@@ -167,6 +168,8 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (129, 301, 4, 32, 2, 3),     # config-3 structure (R = 8, K = 32), ragged T
     (65, 77, 2, 20, 1, 4),       # K not a multiple of 16, R = 2
     (33, 17, 3, 5, 2, 2),        # tiny F and T (one tile), odd K
+    (97, 203, 3, 40, [1, 2, 1], 3),  # mixed ranks (general-rank E-step), K padded to 64
+    (161, 250, 4, 16, 1, 3),     # rank 1 everywhere, K = 16 (one MFMA k block)
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
