@@ -30,27 +30,53 @@ HBM_PEAK = 8.0e12          # B/s (spec)
 
 
 def kernel_work(F, T, J, R, K):
-    """Algorithmic FLOPs / bytes per launch of each GEM-iteration kernel.
+    """ALGORITHMIC FLOPs / bytes per launch of the GEM-iteration kernels
+    (SURVEY.md §8(d) accounting: every quantity counted once per iteration,
+    however often a kernel chooses to recompute it; `exec_flops` is what the
+    kernel actually issues, for reference only).
 
-    k_estep_part1: V^T tiles 2JK, Sigma_x, 2x2 inverse, loglik, N = S Cx S - S and
-                   the J(J+1)/2 pair statistics ~ (8J + 70 + 9 J(J+1)/2) per (f,t);
-                   bytes 32 (Cx) + 8J (hat_W write) per (f,t)
-    k_estep_part2: V^T tiles 2JK, P = Cx S and the cross statistics ~ (17J + 10R)
-                   per (f,t); bytes 32 (Cx re-read) per (f,t)
-    k_fb_contract: num 2K per (f,t,j): the E-step hands over rho = hat_W/V, and the
-                   denominator is f-independent (see fasst_em.hip); bytes 8 (rho)
-                   per (f,t,j)
-    k_tw_contract: V_old, V_new 4K + num/den 4K per (f,t,j); bytes 8 per (f,t,j)
+    k_estep_part1: V tiles 2JK (the only algorithmic V before the E-step),
+                   Sigma_x, 2x2 inverse, loglik, N = S Cx S - S, the
+                   J(J+1)/2 pair statistics and hat_W ~ (8J + 70 + 9 J(J+1)/2)
+                   per (f,t); bytes 32 (Cx read) + 8J (rho write) per (f,t)
+    k_estep_part2: P = Cx S and the cross statistics ~ (17J + 10R) per (f,t)
+                   (its V tiles are a recompute); no algorithmic bytes (its Cx
+                   read is a re-read)
+    k_fb_contract: FB numerator 2K per (f,t,j); bytes 8 (rho) per (f,t,j)
+    k_tw_contract: V after the FB update 2K + TW numerator 2K + denominator
+                   2K per (f,t,j) (its V_old tiles are a recompute); bytes 8
+                   (rho re-read, counted in B_alg as hat_W's re-read) per (f,t,j)
     """
     ft = float(F) * T
     np_ = J * (J + 1) / 2
     return {
         "k_estep_part1": dict(flops=ft * (2 * J * K + 8 * J + 70 + 9 * np_),
+                              exec_flops=ft * (2 * J * K + 8 * J + 70 + 9 * np_),
                               bytes=ft * (32 + 8 * J)),
-        "k_estep_part2": dict(flops=ft * (2 * J * K + 17 * J + 10 * R), bytes=ft * 32),
-        "k_fb_contract": dict(flops=ft * J * 2 * K, bytes=ft * J * 8),
-        "k_tw_contract": dict(flops=ft * J * 8 * K, bytes=ft * J * 8),
+        "k_estep_part2": dict(flops=ft * (17 * J + 10 * R),
+                              exec_flops=ft * (2 * J * K + 17 * J + 10 * R), bytes=0.0),
+        "k_fb_contract": dict(flops=ft * J * 2 * K, exec_flops=ft * J * 2 * K, bytes=ft * J * 8),
+        "k_tw_contract": dict(flops=ft * J * 6 * K, exec_flops=ft * J * 8 * K, bytes=ft * J * 8),
     }
+
+
+def iteration_work(F, T, J, R, K):
+    """per GEM iteration, B_alg = 8 F T (4 + 2J) bytes,
+    F_mfma = 10 J F K T, F_valu = F T (8 R^2 + 40 R); t_ideal = max(B_alg / BW,
+    F_mfma / P_mfma + F_valu / P_valu)."""
+    ft = float(F) * T
+    b_alg = 8.0 * ft * (4 + 2 * J)
+    f_mfma = 10.0 * J * K * ft
+    f_valu = ft * (8 * R * R + 40 * R)
+    t_ideal = max(b_alg / HBM_PEAK, f_mfma / FP64_MFMA_PEAK + f_valu / FP64_VALU_PEAK)
+    return dict(B_alg=b_alg, F_mfma=f_mfma, F_valu=f_valu, t_ideal_s=t_ideal)
+
+
+# the kernels one GEM iteration launches (each once), for the PMC traffic sum
+ITERATION_KERNELS = ("k_w_from_fb", "k_fwh_t", "k_tw_rowsum", "k_inst_A", "k_estep_part1",
+                     "k_estep_part2", "k_estep", "k_loglik", "k_mix", "k_mix_inst",
+                     "k_fb_contract", "k_fb_update", "k_tw_contract", "k_tw_update",
+                     "k_renorm_stats", "k_renorm_apply", "k_renorm_final")
 
 
 def build_model(seed, device, T=T_FRAMES):
@@ -71,16 +97,20 @@ def psd_schedule(m, n):
     return np.array([m._annealed_psd(i % N) for i in range(n)])
 
 
-def cpu_baseline(T_sample=1000):
-    """The oracle (NumPy restatement with the reference's operation structure)
-    on a bounded sample: same F, J, rank, K but T_sample frames, one GEM
-    iteration; scaled to the full T (the iteration is linear in T)."""
+def cpu_baseline(T_sample=T_FRAMES):
+    """The oracle (NumPy restatement keeping the reference's operation
+    structure: the R x R pair loop over full F x T arrays, per-bin Python
+    loops) timed for ONE GEM iteration of the same C3 workload, at the full
+    T = 10000 by default (the reference's 5.2 GB temporaries do not scale
+    linearly from a smaller sample).  Also reports the restatement / reference
+    time ratio measured in the build container (profiles/r2_cpu_ratio.json)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fasst_ref as R
     from pyfasst_amd import synthetic
     X = synthetic.stereo_mixture(F_BINS, T_sample, J=J_SRC, K_true=8, rank=RANK, seed=0)
     o = R.RefFASST(iter_num=1)
     o.set_transform([X[0], X[1]])
+    del X
     np.random.seed(1)
     R.init_nmf_inst(o, J_SRC, K_NMF, RANK)
     R.make_convolutive(o)
@@ -90,15 +120,25 @@ def cpu_baseline(T_sample=1000):
     dt = time.perf_counter() - t0
     try:
         from threadpoolctl import threadpool_info
-        cores = max([p.get('num_threads', 1) for p in threadpool_info()] + [1])
+        info = threadpool_info()
+        cores = max([p.get('num_threads', 1) for p in info] + [1])
+        blas = ",".join(sorted(set("%s %s" % (p.get('internal_api'), p.get('version'))
+                                   for p in info)))
     except Exception:
-        cores = 1
+        cores, blas = 1, "unknown"
     scale = T_FRAMES / float(T_sample)
-    return {"value": 1.0 / (dt * scale), "unit": "EM it/s", "cores": int(cores), "kind": "port",
-            "sample": "oracle/fasst_ref.py, 1 GEM iteration at F=%d T=%d J=%d r=%d K=%d "
-                      "(%.2f s), scaled x%.0f to T=%d; BLAS threads=%d, elementwise NumPy "
-                      "single-threaded" % (F_BINS, T_sample, J_SRC, RANK, K_NMF, dt, scale,
-                                           T_FRAMES, cores)}
+    out = {"value": 1.0 / (dt * scale), "unit": "EM it/s", "cores": int(cores), "kind": "port",
+           "sample": "oracle/fasst_ref.py, 1 GEM iteration at F=%d T=%d J=%d r=%d K=%d: %.2f s%s; "
+                     "BLAS %s with %d threads, elementwise NumPy single-threaded"
+                     % (F_BINS, T_sample, J_SRC, RANK, K_NMF, dt,
+                        "" if scale == 1 else " (scaled x%.1f to T=%d)" % (scale, T_FRAMES),
+                        blas, cores)}
+    rp = os.path.join(ROOT, "profiles", "r2_cpu_ratio.json")
+    if os.path.exists(rp):
+        r = json.load(open(rp))
+        out["oracle_over_reference_time"] = r.get("ratio")
+        out["ratio_source"] = os.path.relpath(rp, ROOT)
+    return out
 
 
 def rank_setup(env=None):
@@ -133,6 +173,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--T", type=int, default=T_FRAMES)
+    ap.add_argument("--cpu-T", type=int, default=T_FRAMES,
+                    help="frames of the CPU-baseline sample (default: the full T)")
     args = ap.parse_args()
 
     world, rank, local, seed, device = rank_setup()
@@ -185,16 +227,24 @@ def main():
 
     if rank == 0:
         R = sum(m.rank)
-        work = kernel_work(m.nbFreqsSigRepr, m.nbFramesSigRepr, J_SRC, R, K_NMF)
+        F, T = m.nbFreqsSigRepr, m.nbFramesSigRepr
+        work = kernel_work(F, T, J_SRC, R, K_NMF)
+        itw = iteration_work(F, T, J_SRC, R, K_NMF)
         dom = max(times, key=lambda k: times[k][0])
         rl = None
         pmc = None
-        pmc_path = os.environ.get("FASST_PMC_JSON", os.path.join(ROOT, "profiles", "r1_bench.json"))
+        pmc_path = os.environ.get("FASST_PMC_JSON", os.path.join(ROOT, "profiles", "r2_bench.json"))
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))["kernels"]
             except Exception:
                 pmc = None
+        step_s = dt / args.steps
+        iter_traffic = None
+        if pmc:
+            tot = [pmc[k]["hbm_bytes_per_launch"] for k in ITERATION_KERNELS
+                   if k in pmc and pmc[k].get("hbm_bytes_per_launch")]
+            iter_traffic = float(sum(tot)) if tot else None
         if dom in work:
             sec = times[dom][0] * 1e-3
             achieved = work[dom]["flops"] / sec / 1e12
@@ -204,8 +254,20 @@ def main():
             rl = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_MFMA_PEAK / 1e12,
                   "unit": "TFLOP/s", "frac": round(achieved * 1e12 / FP64_MFMA_PEAK, 4),
                   "traffic": traffic, "kernel": dom, "kernel_ms": round(times[dom][0], 4),
-                  "dtype": "f64", "algorithmic_bytes": work[dom]["bytes"],
-                  "traffic_source": os.path.relpath(pmc_path, ROOT) if traffic else None}
+                  "dtype": "f64", "algorithmic_flops": work[dom]["flops"],
+                  "executed_flops": work[dom]["exec_flops"],
+                  "executed_tflops": round(work[dom]["exec_flops"] / sec / 1e12, 3),
+                  "algorithmic_bytes": work[dom]["bytes"],
+                  "traffic_source": os.path.relpath(pmc_path, ROOT) if traffic else None,
+                  # whole GEM iteration against SURVEY.md §8(d)'s ideal time
+                  "iteration": {
+                      "t_ideal_ms": round(itw["t_ideal_s"] * 1e3, 4),
+                      "t_measured_ms": round(step_s * 1e3, 4),
+                      "frac": round(itw["t_ideal_s"] / step_s, 4),
+                      "B_alg": itw["B_alg"], "F_mfma": itw["F_mfma"], "F_valu": itw["F_valu"],
+                      "traffic": iter_traffic,
+                      "traffic_ratio": round(iter_traffic / itw["B_alg"], 3) if iter_traffic
+                      else None}}
         out = {
             "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",
             "value": round(job_value(world, args.steps, dt), 4),
@@ -227,7 +289,7 @@ def main():
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(times.items())},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline()
+            out["cpu_baseline"] = cpu_baseline(args.cpu_T)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

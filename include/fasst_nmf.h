@@ -33,6 +33,27 @@ int nmf_set_params(nmf_ctx *ctx, const double *W, const double *H);
 int nmf_run(nmf_ctx *ctx, int n_iter, int update_w, int update_h);
 int nmf_get_params(nmf_ctx *ctx, double *W, double *H);
 
+/* Per-source mono Wiener separation of the IS-NMF model (BASELINE configs[1],
+ * SURVEY.md §8 N8): the one-channel degenerate of the reference's FASST
+ * separation -- compute_sigma_comp_2d / compute_inv_sigma_mix_2d /
+ * compute_Wiener_gain_2d (audioModel.py:1327-1467) and the image
+ * sum_c2 WG X (audioModel.py:1205-1214) -- with Sigma_n = V_n =
+ * W[:, k in n] H[k in n, :] (tools/nmf.py:24-61's model), Sigma_x =
+ * sum_n V_n + psd (psd may be NULL = 0) and the inv_herm_mat_2d determinant
+ * guard (tools/signalTools.py:177-188) on the 1 x 1 Sigma_x.
+ *   W [F][K], H [K][N], comp_source[K] in [0, J) (other values: unused
+ *   component), X complex [F][N] (interleaved doubles), K <= 256.
+ * nmf_wiener_images   -> S complex [J][F][N]
+ * nmf_wiener_waveforms -> y [J][hop (N-1) + wlen - wlen/2]: the iSTFT of each
+ *   image (tftransforms/stft.py:71-131; nfft / 2 + 1 must equal F) without the
+ *   images leaving the device.                                              */
+int nmf_wiener_images(int device, int F, int N, int K, const double *W, const double *H, int J,
+                      const int *comp_source, const double *psd, const double *X, double *S);
+int nmf_wiener_waveforms(int device, int F, int N, int K, const double *W, const double *H, int J,
+                         const int *comp_source, const double *psd, const double *X,
+                         const double *window, const double *analysis_window, int wlen, int nfft,
+                         int hop, double *y);
+
 #ifdef __cplusplus
 }
 #endif

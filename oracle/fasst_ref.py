@@ -613,3 +613,31 @@ def init_nmf_same(model, niter=10, rng=np.random):
         sc['factor'][0]['FB'][:] = W[:, :n]
         sc['factor'][0]['TW'][:] = H[:n]
     model.renormalize_parameters(rng=rng)
+
+
+# ----------------------------------------------------------------------------
+# BASELINE configs[1] (C2): per-source mono Wiener images of the IS-NMF model.
+# The one-channel degenerate of compute_sigma_comp_2d (audioModel.py:1327-1372,
+# mixing = 1), compute_inv_sigma_mix_2d (:1374-1394, the inv_herm_mat_2d guard
+# of signalTools.py:177-188 on a 1 x 1 Sigma_x) and compute_Wiener_gain_2d
+# (:1396-1467), image WG X as separate_comps (:1205-1214), with V_n the
+# IS-NMF model of tools/nmf.py:24-61 restricted to source n's components.
+# PARITY UNPINNED by reference code: the reference's FASST raises for mono
+# signals (audioModel.py:394, :418-420, :605-607), so no
+# reference output exists for this stage.
+def mono_wiener_images(X, W, H, comp_ind, psd=None):
+    F, T = X.shape
+    nsrc = len(comp_ind)
+    sd = np.zeros([nsrc, F, T])
+    for n in range(nsrc):
+        c = list(comp_ind[n])
+        sd[n] = np.dot(W[:, c], H[c])
+    d = sd.sum(axis=0)
+    if psd is not None:
+        d += np.asarray(psd)[:, None]
+    det = np.sign(d + EPS) * np.maximum(np.abs(d), EPS)
+    isd = 1. / det
+    S = np.zeros([nsrc, F, T], dtype=complex)
+    for n in range(nsrc):
+        S[n] = (sd[n] * isd) * X
+    return S

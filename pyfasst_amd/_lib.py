@@ -85,6 +85,11 @@ SIGNATURES = {
     "nmf_set_params": (ctypes.c_int, [_vp, _dp, _dp]),
     "nmf_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "nmf_get_params": (ctypes.c_int, [_vp, _dp, _dp]),
+    "nmf_wiener_images": (ctypes.c_int, [ctypes.c_int] * 4 + [_dp, _dp, ctypes.c_int, _ip, _dp,
+                                                              _dp, _dp]),
+    "nmf_wiener_waveforms": (ctypes.c_int, [ctypes.c_int] * 4 + [_dp, _dp, ctypes.c_int, _ip, _dp,
+                                                                 _dp, _dp, _dp, ctypes.c_int,
+                                                                 ctypes.c_int, ctypes.c_int, _dp]),
     # include/fasst_cqt.h
     "cqt_create": (ctypes.c_int, [ctypes.c_int] * 8 + [_dp, _dp, _dp, _dp] +
                    [ctypes.c_int] * 3 + [_dp, ctypes.POINTER(_vp)]),

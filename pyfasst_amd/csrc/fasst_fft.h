@@ -45,4 +45,18 @@ static inline int ilog2(int n) {
   return (1 << l) == n ? l : -1;
 }
 
+// Host-side launchers of the fasst_tf.hip kernels for the other translation
+// units (HIP kernels do not link across TUs without -fgpu-rdc).
+// [nm][F][T] (host order) <-> [nm][Tp][Fp] (frame-major, bins contiguous)
+int tf_launch_ft_to_tf(hipStream_t s, const double2 *src, double2 *dst, int F, int T, int Fp,
+                       int Tp, int nm);
+int tf_launch_tf_to_ft(hipStream_t s, const double2 *src, double2 *dst, int F, int T, int Fp,
+                       int Tp, int nm);
+// iSTFT of one frame-major image (rows of `ld` bins, T frames) into y[len_out]
+// (tftransforms/stft.py:71-131); frames is [T][wlen] scratch, tw the +1
+// twiddles of nfft.
+int tf_launch_istft(hipStream_t s, const double2 *S, int ld, int T, const double *win,
+                    const double *awin, const double2 *tw, int wlen, int nfft, int hop,
+                    double *frames, double *y, int len_out);
+
 }  // namespace fasst

@@ -10,6 +10,7 @@
 //   num = W^T X, den = W^T Y       (one GEMM launch, shared W operand)
 //   H *= num/max(den, eps)
 #include "fasst_gemm.h"
+#include "fasst_fft.h"
 
 #include <algorithm>
 
@@ -321,9 +322,148 @@ __global__ void k_nmf_transpose(const double *__restrict__ in, double *__restric
   if (c0 + ty < C && r0 + tx < R) out[(size_t)(c0 + ty) * R + r0 + tx] = tile[tx][ty];
 }
 
+// ---------------------------------------------------------------- C2 Wiener
+// Per-source mono Wiener images of the IS-NMF model (BASELINE configs[1]):
+// the one-channel degenerate of the FASST separation (audioModel.py:1327-1467:
+// Sigma_n = V_n, Sigma_x = sum_n Sigma_n + noise PSD, its inverse with the
+// inv_herm_mat_2d determinant guard of signalTools.py:177-188 reduced to
+// 1 x 1, WG_n = Sigma_n Sigma_x^-1, image = WG_n X, :1205-1214).  V_n =
+// W[:, comps of n] H[comps of n, :] with the components grouped by source
+// on the host (koff = source boundaries in the permuted order).
+//
+// Block: 16 bins x 64 frames, 256 threads; the W rows and H columns of the
+// tile sit in LDS; each thread owns one bin and 4 frames.  Sigma_x is summed
+// over the sources in a first pass, each V_n is recomputed (K FMAs per
+// point) in the second pass right before its image is written: the kernel is
+// HBM-bound (X read once, J images written once), V is never stored.
+constexpr int kWienerMaxK = 256;
+__global__ __launch_bounds__(256) void k_nmf_wiener(const double *__restrict__ W,
+                                                    const double *__restrict__ H,
+                                                    const int *__restrict__ koff, int J,
+                                                    const double *__restrict__ psd,
+                                                    const double2 *__restrict__ X,
+                                                    double2 *__restrict__ S, int F, int N, int K,
+                                                    int Fp, int Np) {
+  extern __shared__ __attribute__((aligned(16))) double s_wh[];
+  double *s_w = s_wh;             // [16][K + 1]
+  double *s_h = s_wh + 16 * (K + 1);  // [K][64]
+  const int f0 = blockIdx.y * 16, t0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, fl = tid & 15, tq = tid >> 4;
+  for (int idx = tid; idx < 16 * K; idx += 256) {
+    const int r = idx / K, k = idx % K;
+    s_w[r * (K + 1) + k] = f0 + r < F ? W[(size_t)(f0 + r) * K + k] : 0.0;
+  }
+  for (int idx = tid; idx < K * 64; idx += 256) {
+    const int k = idx >> 6, tl = idx & 63;
+    s_h[idx] = t0 + tl < N ? H[(size_t)k * N + t0 + tl] : 0.0;
+  }
+  __syncthreads();
+  const int f = f0 + fl;
+  const double *wr = s_w + fl * (K + 1);
+  auto vsrc = [&](int n, int i) {
+    double v = 0.0;
+    for (int k = koff[n]; k < koff[n + 1]; ++k) v = fma(wr[k], s_h[k * 64 + tq + 16 * i], v);
+    return v;
+  };
+  const double nz = (psd && f < F) ? psd[f] : 0.0;
+  double inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double sx = 0.0;
+    for (int n = 0; n < J; ++n) sx += vsrc(n, i);
+    sx += nz;
+    const double sg = (sx + kNmfEps) > 0.0 ? 1.0 : ((sx + kNmfEps) < 0.0 ? -1.0 : 0.0);
+    inv[i] = 1.0 / (sg * fmax(fabs(sx), kNmfEps));
+  }
+  if (f >= Fp) return;
+  double2 x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + tq + 16 * i;
+    x[i] = (f < F && t < N) ? X[(size_t)t * Fp + f] : make_double2(0.0, 0.0);
+  }
+  for (int n = 0; n < J; ++n) {
+    double2 *Sn = S + (size_t)n * Np * Fp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 16 * i;
+      if (t >= Np) continue;
+      const double g = vsrc(n, i) * inv[i];
+      Sn[(size_t)t * Fp + f] = make_double2(g * x[i].x, g * x[i].y);
+    }
+  }
+}
+
 }  // namespace fasst
 
 using namespace fasst;
+
+namespace {
+
+// grouped (source-contiguous) copies of W's columns / H's rows
+int wiener_setup(int F, int N, int K, const double *W, const double *H, int J, const int *comp_src,
+                 std::vector<double> &Wg, std::vector<double> &Hg, std::vector<int> &koff) {
+  if (F < 1 || N < 1 || K < 1 || K > kWienerMaxK || J < 1 || !W || !H || !comp_src) {
+    set_error("nmf wiener: bad sizes F=%d N=%d K=%d (max %d) J=%d", F, N, K, kWienerMaxK, J);
+    return FASST_ERR_SHAPE;
+  }
+  std::vector<int> order;
+  koff.assign(J + 1, 0);
+  for (int n = 0; n < J; ++n) {
+    for (int k = 0; k < K; ++k)
+      if (comp_src[k] == n) order.push_back(k);
+    koff[n + 1] = (int)order.size();
+  }
+  Wg.resize((size_t)F * K, 0.0);
+  Hg.resize((size_t)K * N, 0.0);
+  const int Ku = (int)order.size();  // components assigned to no source are dropped
+  for (int f = 0; f < F; ++f)
+    for (int q = 0; q < Ku; ++q) Wg[(size_t)f * K + q] = W[(size_t)f * K + order[q]];
+  for (int q = 0; q < Ku; ++q)
+    std::copy(H + (size_t)order[q] * N, H + (size_t)(order[q] + 1) * N, Hg.begin() + (size_t)q * N);
+  return FASST_OK;
+}
+
+// device images S [J][Np][Fp] (frame-major) from host W, H, X [F][N], psd [F]
+struct WienerDev {
+  DBuf<double> W, H, psd;
+  DBuf<int> koff;
+  DBuf<double2> Xh, X, S;
+  int Fp = 0, Np = 0;
+};
+
+int wiener_images_dev(hipStream_t s, int F, int N, int K, const double *W, const double *H,
+                      int J, const int *comp_src, const double *psd, const double *X,
+                      WienerDev &d) {
+  std::vector<double> Wg, Hg;
+  std::vector<int> koff;
+  int st = wiener_setup(F, N, K, W, H, J, comp_src, Wg, Hg, koff);
+  if (st) return st;
+  if (!X) return FASST_ERR_SHAPE;
+  d.Fp = round_up(F, 16);
+  d.Np = round_up(N, 64);
+  if ((st = d.W.alloc((size_t)F * K)) || (st = d.H.alloc((size_t)K * N)) ||
+      (st = d.psd.alloc(F)) || (st = d.koff.alloc(J + 1)) || (st = d.Xh.alloc((size_t)F * N)) ||
+      (st = d.X.alloc((size_t)d.Np * d.Fp)) || (st = d.S.alloc((size_t)J * d.Np * d.Fp)))
+    return st;
+  FASST_HIP(hipMemcpyAsync(d.W.p, Wg.data(), Wg.size() * 8, hipMemcpyHostToDevice, s));
+  FASST_HIP(hipMemcpyAsync(d.H.p, Hg.data(), Hg.size() * 8, hipMemcpyHostToDevice, s));
+  FASST_HIP(hipMemcpyAsync(d.koff.p, koff.data(), koff.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  if (psd) FASST_HIP(hipMemcpyAsync(d.psd.p, psd, (size_t)F * 8, hipMemcpyHostToDevice, s));
+  FASST_HIP(hipMemcpyAsync(d.Xh.p, X, (size_t)F * N * sizeof(double2), hipMemcpyHostToDevice, s));
+  if ((st = tf_launch_ft_to_tf(s, d.Xh.p, d.X.p, F, N, d.Fp, d.Np, 1))) return st;
+  const size_t smem = (size_t)(16 * (K + 1) + K * 64) * sizeof(double);
+  if (smem > 64 * 1024)
+    FASST_HIP(hipFuncSetAttribute((const void *)k_nmf_wiener,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  k_nmf_wiener<<<dim3(d.Np / 64, d.Fp / 16), 256, smem, s>>>(d.W.p, d.H.p, d.koff.p, J,
+                                                             psd ? d.psd.p : nullptr, d.X.p,
+                                                             d.S.p, F, N, K, d.Fp, d.Np);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+}  // namespace
 
 struct nmf_ctx {
   int device = 0;
@@ -508,6 +648,59 @@ int nmf_run(nmf_ctx *c, int n_iter, int update_w, int update_h) {
   }
   FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
+}
+
+int nmf_wiener_images(int device, int F, int N, int K, const double *W, const double *H, int J,
+                      const int *comp_source, const double *psd, const double *X, double *S) {
+  if (!S) return FASST_ERR_SHAPE;
+  DeviceGuard g(device);
+  hipStream_t s = nullptr;
+  FASST_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  WienerDev d;
+  int st = wiener_images_dev(s, F, N, K, W, H, J, comp_source, psd, X, d);
+  DBuf<double2> hS;
+  if (!st) st = hS.alloc((size_t)J * F * N);
+  if (!st) st = tf_launch_tf_to_ft(s, d.S.p, hS.p, F, N, d.Fp, d.Np, J);
+  if (!st && hipMemcpyAsync(S, hS.p, hS.n * sizeof(double2), hipMemcpyDeviceToHost, s) != hipSuccess)
+    st = FASST_ERR_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess && !st) st = FASST_ERR_DEVICE;
+  (void)hipStreamDestroy(s);
+  return st;
+}
+
+int nmf_wiener_waveforms(int device, int F, int N, int K, const double *W, const double *H, int J,
+                         const int *comp_source, const double *psd, const double *X,
+                         const double *window, const double *analysis_window, int wlen, int nfft,
+                         int hop, double *y) {
+  if (!y || !window || nfft / 2 + 1 != F) {
+    set_error("nmf_wiener_waveforms: nfft=%d does not give F=%d bins", nfft, F);
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(device);
+  hipStream_t s = nullptr;
+  FASST_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  WienerDev d;
+  int st = wiener_images_dev(s, F, N, K, W, H, J, comp_source, psd, X, d);
+  const int len_out = hop * (N - 1) + wlen - wlen / 2;  // istft (stft.py:108-129)
+  DBuf<double> dw, daw, frames, dy;
+  DBuf<double2> dtw;
+  if (!st && ((st = dw.alloc(wlen)) || (st = daw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)) ||
+              (st = frames.alloc((size_t)N * wlen)) || (st = dy.alloc((size_t)J * len_out)))) {
+  }
+  auto tw = twiddles(nfft, +1);
+  if (!st && (hipMemcpyAsync(dw.p, window, (size_t)wlen * 8, hipMemcpyHostToDevice, s) ||
+              hipMemcpyAsync(daw.p, analysis_window ? analysis_window : window, (size_t)wlen * 8,
+                             hipMemcpyHostToDevice, s) ||
+              hipMemcpyAsync(dtw.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice, s)))
+    st = FASST_ERR_DEVICE;
+  for (int n = 0; n < J && !st; ++n)
+    st = tf_launch_istft(s, d.S.p + (size_t)n * d.Np * d.Fp, d.Fp, N, dw.p, daw.p, dtw.p, wlen,
+                         nfft, hop, frames.p, dy.p + (size_t)n * len_out, len_out);
+  if (!st && hipMemcpyAsync(y, dy.p, dy.n * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+    st = FASST_ERR_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess && !st) st = FASST_ERR_DEVICE;
+  (void)hipStreamDestroy(s);
+  return st;
 }
 
 int nmf_get_params(nmf_ctx *c, double *W, double *H) {

@@ -387,6 +387,34 @@ static int fft_smem(int N) {
   return FASST_OK;
 }
 
+int tf_launch_ft_to_tf(hipStream_t s, const double2 *src, double2 *dst, int F, int T, int Fp,
+                       int Tp, int nm) {
+  k_ft_to_tf<<<dim3((Tp + 15) / 16, (Fp + 15) / 16, nm), 256, 0, s>>>(src, dst, F, T, Fp, Tp);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+int tf_launch_tf_to_ft(hipStream_t s, const double2 *src, double2 *dst, int F, int T, int Fp,
+                       int Tp, int nm) {
+  k_tf_to_ft<<<dim3((Tp + 15) / 16, (Fp + 15) / 16, nm), 256, 0, s>>>(src, dst, F, T, Fp, Tp);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+int tf_launch_istft(hipStream_t s, const double2 *S, int ld, int T, const double *win,
+                    const double *awin, const double2 *tw, int wlen, int nfft, int hop,
+                    double *frames, double *y, int len_out) {
+  int st = check_fft(nfft, wlen, hop);
+  if (st) return st;
+  if ((st = fft_smem(nfft))) return st;
+  k_istft_frames<<<T, 256, nfft * sizeof(double2), s>>>(S, ld, win, wlen, tw, nfft, ilog2(nfft),
+                                                        frames);
+  FASST_LAUNCH_CHECK();
+  k_ola<<<(len_out + 255) / 256, 256, 0, s>>>(frames, T, wlen, hop, win, awin, y, len_out);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
 }  // namespace fasst
 
 using namespace fasst;
@@ -615,12 +643,12 @@ int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double
     return FASST_ERR_SHAPE;
   }
   int st;
+  DeviceGuard g(c->device);  // before upload_stft: X and its staging live on c->device
   if (X && (st = upload_stft(c, X))) return st;
   if (!c->have_X) {
     set_error("fasst_wiener_images: no STFT available (set_audio / set_stft / X argument)");
     return FASST_ERR_SHAPE;
   }
-  DeviceGuard g(c->device);
   const int J = c->J;
   DBuf<double> dpsd, coef;
   DBuf<int> droff;

@@ -34,11 +34,16 @@ def stereo_mixture(F, T, J=4, K_true=8, rank=2, seed=0, dtype=np.complex128):
     return X
 
 
-def mono_mixture(F, T, J=2, K_true=32, seed=0):
-    """Power spectrogram SX [F, T] of a mono NMF mixture (config C2)."""
+def mono_stft(F, T, J=2, K_true=32, seed=0):
+    """Complex STFT X [F, T] of a mono NMF mixture (config C2):
+    X ~ CN(0, sum_j W_j H_j), W ~ Gamma(2, 1), H ~ Gamma(0.5, 1)."""
     rs = np.random.RandomState(seed)
     V = np.zeros((F, T))
     for _ in range(J):
         V += rs.gamma(2.0, 1.0, size=(F, K_true)) @ rs.gamma(0.5, 1.0, size=(K_true, T))
-    x = _cn(rs, (F, T), V)
-    return np.abs(x) ** 2
+    return _cn(rs, (F, T), V)
+
+
+def mono_mixture(F, T, J=2, K_true=32, seed=0):
+    """Power spectrogram SX = |X|^2 [F, T] of mono_stft (config C2)."""
+    return np.abs(mono_stft(F, T, J, K_true, seed)) ** 2

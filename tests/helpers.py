@@ -31,6 +31,29 @@ CQT_CASES = (
 )
 
 
+# BASELINE-size cases of tests/golden/make_fullsize.py (oracle-generated fixtures)
+FULL_CASES = {
+    "c3_full": dict(F=2049, T=10000, J=4, K=32, rank=2, conv=True, iters=2, K_true=8,
+                    data_rank=2, data_seed=0, init_seed=1),
+    "c3_t1000": dict(F=2049, T=1000, J=4, K=32, rank=2, conv=True, iters=3, K_true=8,
+                     data_rank=2, data_seed=3, init_seed=1),
+    "c1_50": dict(F=1025, T=1122, J=2, K=32, rank=1, conv=False, iters=50, K_true=8,
+                  data_rank=1, data_seed=0, init_seed=0),
+    "c5_full": dict(F=2049, N=20000, NF0=1092, P=30, K=4, R=40, iters=1, data_seed=0,
+                    init_seed=1),
+}
+
+
+def sub_f(F):
+    """Bins kept in the full-size fixtures (every 7th, and the last)."""
+    return np.unique(np.r_[np.arange(0, F, 7), F - 1])
+
+
+def sub_t(T):
+    """Frames kept in the full-size fixtures (about 40, and the last)."""
+    return np.unique(np.r_[np.arange(0, T, max(1, T // 40)), T - 1])
+
+
 def load(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 

@@ -1,0 +1,187 @@
+"""BASELINE-size parity on the MI355X: the HIP path at the configurations the
+bench is quoted on, against the oracle's outputs on identical seeded inputs.
+
+The fixtures (tests/golden/{c3_full,c3_t1000,c1_50,c5_full}.npz) are written
+by tests/golden/make_fullsize.py, which runs oracle/fasst_ref.py and
+oracle/simm_ref.py at these sizes in the build container (the oracle is
+pinned bit-exactly to the reference on the small golden cases); the box
+regenerates the seeded inputs (pyfasst_amd/synthetic.py).  Outputs are
+compared on the fixture's subsample (every 7th bin, ~40 frames) and through
+full-array sums.
+
+Tolerances: 1e-8 relative (max-normalised) after 1-3 iterations; the C1-shaped
+50-iteration run holds the north-star bar, 1e-4 relative on the separated
+magnitude spectrograms, and reports the drift it actually shows (SURVEY.md §7
+measured 7.4e-5 for a 1e-7 input perturbation after 50 iterations).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import FULL_CASES, load, rel, sub_f, sub_t
+
+pytestmark = pytest.mark.gpu
+
+BAR = 1e-4
+
+
+def _fasst_model(name, **over):
+    import pyfasst_amd.audioModel as am
+    from pyfasst_amd import synthetic
+    from pyfasst_amd.audioObject import SpectralAudio
+    c = dict(FULL_CASES[name], **over)
+    X = synthetic.stereo_mixture(c["F"], c["T"], J=c["J"], K_true=c["K_true"],
+                                 rank=c["data_rank"], seed=c["data_seed"])
+    np.random.seed(c["init_seed"])
+    cls = am.MultiChanNMFConv if c["conv"] else am.MultiChanNMFInst_FASST
+    m = cls(SpectralAudio(X=X), nbComps=c["J"], nbNMFComps=c["K"], spatial_rank=c["rank"],
+            iter_num=c["iters"], wlen=2 * (c["F"] - 1), hopsize=(c["F"] - 1) // 4)
+    if c["conv"]:
+        m.makeItConvolutive()
+    return m
+
+
+def _drift(m, g, name):
+    """max relative deviation from the oracle fixture per output group"""
+    c = FULL_CASES[name]
+    fs, ts = sub_f(c["F"]), sub_t(c["T"])
+    d = {"params": 0.0, "FB": 0.0, "TW": 0.0, "sums": 0.0}
+    for j in range(c["J"]):
+        p = m.spat_comps[j]['params']
+        d["params"] = max(d["params"], rel(p[..., fs] if c["conv"] else p, g["params_%d" % j]))
+        fac = m.spec_comps[j]['factor'][0]
+        d["FB"] = max(d["FB"], rel(fac['FB'][fs], g["FB_%d" % j]))
+        d["TW"] = max(d["TW"], rel(fac['TW'][:, ts], g["TW_%d" % j]))
+        d["sums"] = max(d["sums"], abs(fac['FB'].sum() / g["FB_sum_%d" % j] - 1),
+                        abs(fac['TW'].sum() / g["TW_sum_%d" % j] - 1))
+    S = np.abs(m.separated_images())
+    d["absS"] = rel(S[:, :, fs][:, :, :, ts], g["absS"])
+    d["absS_sum"] = rel(S.sum(axis=(2, 3)), g["absS_sum"])
+    return d
+
+
+@pytest.mark.parametrize("name", ["c3_full", "c3_t1000"])
+def test_config3_full_size_vs_oracle(name):
+    """BASELINE configs[2] (F=2049, T=10000, J=4, r=2, K=32) at its real size:
+    the production launch shapes (several E-step / FB chunks, TW bin splits,
+    ragged last chunks) against the oracle's GEM iterations."""
+    g = load(name)
+    m = _fasst_model(name)
+    ll = m.estim_param_a_post_model()
+    assert rel(ll, g["logliks"]) < 1e-10, (ll, g["logliks"])
+    assert rel(m.noise['PSD'], g["final_psd"]) < 1e-14
+    d = _drift(m, g, name)
+    print(name, "drift", d)
+    for k, v in d.items():
+        assert v < 1e-8, (k, v)
+
+
+def test_chunk_overrides_vs_oracle(monkeypatch):
+    """Forced multi-chunk reductions (E-step chunks 3, FB chunks 3, TW bin
+    splits 2, ragged last chunks) on a small case against the live oracle."""
+    import fasst_ref as R
+    from test_gpu_parity import _c3_like
+    monkeypatch.setenv("FASST_NCHUNK_E", "3")
+    monkeypatch.setenv("FASST_NCHUNK_B", "3")
+    monkeypatch.setenv("FASST_NSPLIT_T", "2")
+    m, o, X = _c3_like(129, 301, 4, 32, 2, 3)
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for j in range(4):
+        assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+        assert rel(m.spec_comps[j]['factor'][0]['FB'], o.spec_comps[j]['factor'][0]['FB']) < 1e-8
+        assert rel(m.spec_comps[j]['factor'][0]['TW'], o.spec_comps[j]['factor'][0]['TW']) < 1e-8
+    assert rel(np.abs(m.separated_images()), np.abs(o.separated_images(X))) < 1e-8
+    del R
+
+
+def test_config1_shape_50_iterations_drift():
+    """C1-shaped run (MultiChanNMFInst_FASST J=2, rank 1, K=32, F=1025,
+    T=1122, 50 GEM iterations) against the oracle: the north-star 1e-4 bar on
+    the separated magnitude spectrograms after the full iteration count."""
+    name = "c1_50"
+    g = load(name)
+    m = _fasst_model(name)
+    ll = m.estim_param_a_post_model()
+    d = _drift(m, g, name)
+    d["logliks"] = rel(ll, g["logliks"])
+    print("c1_50 drift after 50 iterations:", d)
+    assert d["absS"] < BAR and d["absS_sum"] < BAR
+    # the FP64 path holds far tighter than the bar (recorded, asserted loosely)
+    assert d["logliks"] < 1e-8
+    assert max(d["params"], d["FB"], d["TW"]) < 1e-5
+
+
+def test_config5_full_size_vs_oracle():
+    """BASELINE configs[4]: one Stereo_SIMM iteration at F=2049, N=20000,
+    NF0=1092, P=30, K=4, R=40 against oracle/simm_ref.py (SIMM.py:613-941)."""
+    from pyfasst_amd.SeparateLeadStereo.SIMM import SIMM as S
+    c = FULL_CASES["c5_full"]
+    g = load("c5_full")
+    F, N, NF0, P, K, Rr = (c[k] for k in ("F", "N", "NF0", "P", "K", "R"))
+    rs = np.random.RandomState(c["data_seed"])
+    SXR = rs.gamma(0.8, 1.0, size=(F, N))
+    SXL = rs.gamma(0.8, 1.0, size=(F, N))
+    WF0 = rs.gamma(1.0, 1.0, size=(F, NF0))
+    WG = rs.gamma(1.0, 1.0, size=(F, P))
+    np.random.seed(c["init_seed"])
+    res = S.Stereo_SIMM(SXR, SXL, WF0, WG, numberOfFilters=K,
+                        numberOfAccompanimentSpectralShapes=Rr, numberOfIterations=c["iters"],
+                        computeError=True, verbose=False)
+    names = ['alphaR', 'alphaL', 'HGAMMA', 'HPHI', 'HF0', 'betaR', 'betaL', 'HM', 'WM',
+             'recoError']
+    fs, ts = sub_f(F), sub_t(N)
+    worst = {}
+    for n, v in zip(names, res):
+        v = np.asarray(v)
+        s = v.sum()
+        worst[n + "_sum"] = abs(s - g[n + "_sum"]) / max(abs(g[n + "_sum"]), 1e-300)
+        if n in ('HPHI', 'HM'):
+            v = v[:, ts]
+        elif n == 'HF0':
+            v = v[::8][:, ts]
+        elif n == 'WM':
+            v = v[fs]
+        worst[n] = rel(v, g[n])
+    print("c5_full drift:", worst)
+    for k, v in worst.items():
+        assert v < 1e-8, (k, v)
+
+
+def test_config4_independent_contexts_concurrent():
+    """Config 4 semantics in one process: two contexts on distinct seeded
+    clips, run concurrently from two host threads on one GPU, each bit-equal
+    to its solo run (fresh state per clip)."""
+    over = dict(F=513, T=1200, iters=4)
+    solo = []
+    for seed in (0, 1):
+        m = _fasst_model("c3_full", data_seed=seed, **over)
+        ll = m.estim_param_a_post_model()
+        solo.append((ll, [m.spec_comps[j]['factor'][0]['TW'].copy() for j in range(4)],
+                     [m.spat_comps[j]['params'].copy() for j in range(4)]))
+        del m
+    models = [_fasst_model("c3_full", data_seed=s, **over) for s in (0, 1)]
+    out = [None, None]
+    err = []
+
+    def work(i):
+        try:
+            out[i] = models[i].estim_param_a_post_model()
+        except Exception as e:   # surfaced below
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in (0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not err, err
+    for i in (0, 1):
+        np.testing.assert_array_equal(out[i], solo[i][0])
+        for j in range(4):
+            np.testing.assert_array_equal(models[i].spec_comps[j]['factor'][0]['TW'], solo[i][1][j])
+            np.testing.assert_array_equal(models[i].spat_comps[j]['params'], solo[i][2][j])
+    # and the two clips really differ
+    assert rel(out[0], out[1]) > 1e-6

@@ -62,3 +62,18 @@ def test_nmf_vs_oracle(F, N, K, niter):
     np.random.seed(6)
     Wr, Hr = R.nmf_decomp_init(SX, nbComps=K, niter=2, updateH=False)
     assert rel(W, Wr) < 1e-9 and rel(H, Hr) < 1e-9   # (H still takes the W column scale)
+
+
+# frozen W on the fused path (K % 16 == 0, K <= 64: no W rescale, the H
+# numerator kernel runs without the column-scale operand), ragged F and N
+@pytest.mark.parametrize("F,N,K", [(131, 77, 16), (257, 203, 32), (90, 301, 64)])
+def test_nmf_frozen_w_fused_vs_oracle(F, N, K):
+    rs = np.random.RandomState(F * N)
+    SX = rs.gamma(0.7, 1.0, size=(F, N))
+    Winit = rs.gamma(1.0, 1.0, size=(F, K))
+    np.random.seed(9)
+    W, H = _nmf().NMF_decomp_init(SX, nbComps=K, niter=4, Winit=Winit, updateW=False)
+    np.random.seed(9)
+    Wr, Hr = R.nmf_decomp_init(SX, nbComps=K, niter=4, Winit=Winit, updateW=False)
+    assert np.array_equal(W, Winit)
+    assert rel(H, Hr) < 1e-9, rel(H, Hr)

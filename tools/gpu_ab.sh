@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of environment switches on the bench (kernel times from HIP events).
-# Usage: ./tools_gpu_ab.sh "FASST_MFMA16=1" "FASST_MFMA16=0"
+# Usage: tools/gpu_ab.sh "FASST_MFMA16=1" "FASST_MFMA16=0"
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for v in "$@"; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of environment settings on the Stereo_SIMM secondary bench (config 5).
-# Usage: ./tools_gpu_ab_simm.sh "FASST_X=0" "FASST_HIP_LIB=/path/variant.so" ...
+# Usage: tools/gpu_ab_simm.sh "FASST_X=0" "FASST_HIP_LIB=/path/variant.so" ...
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for v in "$@"; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run) over a short bench run.
-# Usage: ./tools_gpu_pmc.sh "SQ_WAVE_CYCLES,SQ_WAIT_ANY:SQ_INSTS_VALU,SQ_INSTS_MFMA"
+# Usage: tools/gpu_pmc.sh "SQ_WAVE_CYCLES,SQ_WAIT_ANY:SQ_INSTS_VALU,SQ_INSTS_MFMA"
 #        (":" separates passes, "," separates the counters of one pass)
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$R/gpurun_out/${PROF_TAG:-pmc}"

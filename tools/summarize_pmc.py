@@ -1,4 +1,4 @@
-"""Average PMC counters per kernel from tools_gpu_pmc.sh output dirs."""
+"""Average PMC counters per kernel from tools/gpu_pmc.sh output dirs."""
 import csv
 import glob
 import os

@@ -1,4 +1,4 @@
-"""Summarise a rocprofv3 run of bench.py (tools_gpu_prof.sh) into profiles/.
+"""Summarise a rocprofv3 run of bench.py (tools/gpu_prof.sh) into profiles/.
 
 Reads <dir>/trace/run_kernel_stats.csv and the FETCH_SIZE / WRITE_SIZE PMC
 passes and writes a JSON + text summary.  HBM bytes per launch follow
