@@ -27,6 +27,7 @@ struct fasst_ctx {
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int nofork = 0;  // FASST_NOFORK (A/B measurements only)
+  int estep_split = 0;  // FASST_ESTEP_SPLIT: round-1 two-pass E-step (A/B measurements only)
   // observation
   int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
   fasst::DBuf<double> cx;        // 4*Tp*Fp

@@ -454,6 +454,308 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
     a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
 }
 
+// Single-pass E-step with the per-bin t-reductions on the matrix cores.
+//
+// Every statistic of the E-step is a per-bin dot product over frames:
+//   cross  Q_j[c]      = sum_t V_j P_c        (P = Cx S, 8 real components)
+//   pairs  M_p[c]      = sum_t V_j1 V_j2 N_c  (N = S Cx S - S, 4 components)
+// For one bin these are tiny GEMMs, (J x T).(T x 8) and (NP x T).(T x 4).
+// v_mfma_f64_4x4x4_4b runs four independent 4x4x4 products per instruction,
+// one per block of 16 lanes (lane = 16 X + 4 b + Y: A[m=Y][k=X],
+// B[k=X][n=Y], D[m=X][n=Y] of block b; tools/probe_mfma4.hip), so with
+// block = bin and k = frame, ONE instruction contracts 4 frames of 4 bins
+// for a 4 x 4 block of statistics.  After each frame group, every lane drops
+// its point's operands (V, P, N and the pair products V_j1 V_j2) into a
+// per-wave LDS slab in the MFMA operand layout, and the wave issues
+// 4 bin groups x (2 + ceil(NP/4)) MFMAs.  The accumulators shrink from
+// 4 J(J+1)/2 + 8J doubles per lane (72 at J = 4, what forced the round-1
+// E-step into two launches) to 4 (2 + ceil(NP/4)) (20 at J = 4), so ONE pass
+// streams Cx once, forms V, Sigma_x and its inverse once per point, and keeps
+// two waves per SIMD; the 72 FMAs per point leave the VALU for the matrix
+// pipe (4x4x4_4b runs at 74.7 TF on this chip, profiles/r1_ubench_fp64.txt).
+__device__ __forceinline__ double mfma44(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int J>
+struct MXShape {
+  static constexpr int NP = J * (J + 1) / 2;
+  static constexpr int NPG = (NP + 3) / 4;      // pair groups of 4
+  static constexpr int NSET = 4 + NPG;          // V | P lo | P hi | N | VV groups
+  static constexpr int GS = NSET * 64 + 1;      // doubles per bin group (+1: bank skew)
+  static constexpr int SLAB = 4 * GS;           // doubles per wave
+};
+
+template <int J, int NKS>
+static constexpr size_t estep_mx_smem() {
+  return (size_t)(kMaxR * 4 * 16 + J * 4 * 16 + 4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) *
+         sizeof(double);
+}
+
+// (the LDS slabs allow two blocks per CU, so the register budget is that of
+// two waves per SIMD: amdgpu_waves_per_eu tells the scheduler, which would
+// otherwise serialise the operand loads to fit three)
+template <int J, int NKS, int RKU>
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_estep_mx(
+    const EArgs a) {
+  HALT_GUARD(a.halt);
+  using S = MXShape<J>;
+  constexpr int NP = S::NP, NPG = S::NPG;
+  constexpr int NACC = 4 * NP + 8 * J;
+  constexpr int KP = 4 * NKS;
+  constexpr int RK = RKU ? RKU : kMaxR;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double *s_cr = smem;                     // [kMaxR][4][16] per-rank coefficients
+  double *s_cj = s_cr + kMaxR * 4 * 16;    // [J][4][16] per-source Sigma_x coefficients
+  double *s_ll = s_cj + J * 4 * 16;        // [4]
+  double *s_w = s_ll + 4;                  // [J][KP][16] W tile
+  double *s_slab = s_w + J * KP * 16;      // [4 waves][SLAB] operand slabs
+  double *s_red = s_w;                     // [4][NACC][16] (epilogue, aliases W + slabs)
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fl = lane & 15, tq = lane >> 4;
+  const int f0 = blockIdx.x * 16;
+  const int f = f0 + fl;
+  double *slab = s_slab + wv * S::SLAB;
+
+  for (int idx = tid; idx < J * KP * 16; idx += 256) {
+    const int ff = idx & 15, jk = idx >> 4;
+    s_w[idx] = a.Wkf[(size_t)jk * a.Fp + f0 + ff];
+  }
+  // operand slots no point writes (sources >= J, pairs >= NP) stay zero
+  for (int idx = tid; idx < 4 * S::SLAB; idx += 256) s_slab[idx] = 0.0;
+  if (tid < 16) {
+    const int ff = f0 + tid;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      double al = 0, be = 0, gr = 0, gi = 0;
+      for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
+        const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + ff];
+        const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + ff];
+        const double aa = a0.x * a0.x + a0.y * a0.y;
+        const double bb = a1.x * a1.x + a1.y * a1.y;
+        const double cr = a0.x * a1.x + a0.y * a1.y;  // Re a0 conj(a1)
+        const double ci = a0.y * a1.x - a0.x * a1.y;  // Im a0 conj(a1)
+        s_cr[(r * 4 + 0) * 16 + tid] = aa;
+        s_cr[(r * 4 + 1) * 16 + tid] = bb;
+        s_cr[(r * 4 + 2) * 16 + tid] = 2.0 * cr;
+        s_cr[(r * 4 + 3) * 16 + tid] = 2.0 * ci;
+        al += aa;
+        be += bb;
+        gr += cr;
+        gi += ci;
+      }
+      s_cj[(j * 4 + 0) * 16 + tid] = al;
+      s_cj[(j * 4 + 1) * 16 + tid] = be;
+      s_cj[(j * 4 + 2) * 16 + tid] = gr;
+      s_cj[(j * 4 + 3) * 16 + tid] = gi;
+    }
+  }
+  __syncthreads();
+
+  int r0[J], rk[J];
+  double inv_rk[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    r0[j] = RKU ? RKU * j : a.roff[j];
+    rk[j] = RKU ? RKU : a.roff[j + 1] - a.roff[j];
+    inv_rk[j] = 1.0 / (double)rk[j];
+  }
+  const double psd = a.psd[f];
+  const bool fvalid = f < a.F;
+  // writer side: this lane's point goes to bin group g = fl / 4, block b = fl % 4, X = tq
+  double *wr = slab + (fl >> 2) * S::GS + 16 * tq + 4 * (fl & 3);
+  // reader side: operands of lane (X, b, Y) sit at [group][set][lane]
+  const double *rd = slab + lane;
+
+  double xacc[4][2], pacc[4][NPG];  // D operands (4x4 blocks per bin group)
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    xacc[g][0] = xacc[g][1] = 0.0;
+#pragma unroll
+    for (int h = 0; h < NPG; ++h) pacc[g][h] = 0.0;
+  }
+  double ll = 0.0, lm = 1.0, lev = 0.0, lspec = 0.0;
+
+  const int tb = blockIdx.y * a.tpc;
+  const int te = min(tb + a.tpc, a.ntt);
+  for (int tt = tb + wv; tt < te; tt += 4) {
+    const int t0 = tt * 16;
+    int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
+    asm volatile("" : "+v"(lofs));
+    // all TW operands in flight before the first MFMA (the scheduler would
+    // otherwise pair each load with its MFMA and wait on every one)
+    double twv[J][NKS];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) twv[j][s] = tw[(size_t)(4 * s) * a.Tp];
+    }
+    double cxv[4][4];  // this tile's Cx, in flight with the TW operands
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
+      cxv[0][i] = __builtin_nontemporal_load(a.cx00 + off);
+      cxv[1][i] = __builtin_nontemporal_load(a.cx11 + off);
+      cxv[2][i] = __builtin_nontemporal_load(a.cxr + off);
+      cxv[3][i] = __builtin_nontemporal_load(a.cxi + off);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    d4 v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      v[j] = d4{0.0, 0.0, 0.0, 0.0};
+      const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) v[j] = mfma4(twv[j][s], sw[4 * s * 16], v[j]);
+    }
+    const double *cr = s_cr + lofs + fl;
+    const double *cj = s_cj + lofs + fl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 4 * i;
+      const double x00 = cxv[0][i], x11 = cxv[1][i], xr = cxv[2][i], xi = cxv[3][i];
+      double V[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) V[j] = v[j][i];
+      // Sigma_x = sum_r V_r a_r a_r^H + PSD I   (compute_suff_stat :613-652)
+      double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        d0 += cj[(j * 4 + 0) * 16] * V[j];
+        d1 += cj[(j * 4 + 1) * 16] * V[j];
+        ore += cj[(j * 4 + 2) * 16] * V[j];
+        oim += cj[(j * 4 + 3) * 16] * V[j];
+      }
+      // inv_herm_mat_2d (signalTools.py:177-194)
+      double det = d0 * d1 - (ore * ore + oim * oim);
+      const double dg = det + kEps;
+      const double sg = dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0);
+      det = sg * fmax(fabs(det), kEps);
+      const double rdet = rcp_nr(det);
+      const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
+      if (fvalid && t < a.T) {
+        const double x = det * M_PI;
+        if (x > 0.0 && x < INFINITY) {
+          const unsigned long long b = __double_as_longlong(x);
+          lev += (double)((int)((b >> 52) & 0x7ff) - 1022);
+          lm *= __longlong_as_double((b & 0x800fffffffffffffULL) | 0x3fe0000000000000ULL);
+        } else {
+          lspec += x == 0.0 ? -INFINITY : (x == INFINITY ? INFINITY : NAN);
+        }
+        ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
+      }
+      // P = Cx S, N = S Cx S - S = P^H S - S
+      const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
+      const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
+      const double p10r = xr * i0 + x11 * ior, p10i = -xi * i0 - x11 * ioi;
+      const double p11r = xr * ior + xi * ioi + x11 * i1, p11i = xr * ioi - xi * ior;
+      const double n00 = p00r * i0 + (p10r * ior - p10i * ioi) - i0;
+      const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
+      const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
+      const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
+      // this point's MFMA operands -> the wave's slab (reader layout)
+#pragma unroll
+      for (int j = 0; j < J; ++j) wr[0 * 64 + j] = V[j];
+      wr[1 * 64 + 0] = p00r;
+      wr[1 * 64 + 1] = p00i;
+      wr[1 * 64 + 2] = p01r;
+      wr[1 * 64 + 3] = p01i;
+      wr[2 * 64 + 0] = p10r;
+      wr[2 * 64 + 1] = p10i;
+      wr[2 * 64 + 2] = p11r;
+      wr[2 * 64 + 3] = p11i;
+      wr[3 * 64 + 0] = n00;
+      wr[3 * 64 + 1] = n11;
+      wr[3 * 64 + 2] = n01r;
+      wr[3 * 64 + 3] = n01i;
+      {
+        int p = 0;
+#pragma unroll
+        for (int j1 = 0; j1 < J; ++j1)
+#pragma unroll
+          for (int j2 = j1; j2 < J; ++j2, ++p) wr[(4 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
+      }
+      // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414),
+      // stored as rho = (hat_W / vm^2) vm, vm = max(V, eps): the FB ratio of
+      // update_spectral_components (:1521-1575, N1), formed where V is at hand
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const double Vj = V[j];
+        double hw = 0.0;
+#pragma unroll
+        for (int q = 0; q < RK; ++q)
+          if (RKU || q < rk[j]) {
+            const double *c = cr + (r0[j] + q) * 64;
+            const double qa = c[0] * n00 + c[16] * n11 + (c[32] * n01r + c[48] * n01i);
+            hw += fabs((Vj * Vj) * qa + Vj);
+          }
+        const double hwm = RKU == 1 ? hw : hw * inv_rk[j];
+        const double vm = fmax(Vj, kEps);
+        const double rv = rcp_nr(vm);
+        __builtin_nontemporal_store((hwm * (rv * rv)) * vm,
+                                    a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
+      }
+      // the slab writes above must land before the cross-lane reads below
+      // (LDS is in order within a wave; this keeps the compiler in order too)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const double *o = rd + g * S::GS;
+        const double av = o[0 * 64];
+        xacc[g][0] = mfma44(av, o[1 * 64], xacc[g][0]);
+        xacc[g][1] = mfma44(av, o[2 * 64], xacc[g][1]);
+        const double bn = o[3 * 64];
+#pragma unroll
+        for (int h = 0; h < NPG; ++h) pacc[g][h] = mfma44(o[(4 + h) * 64], bn, pacc[g][h]);
+      }
+      // the next point's slab writes must not overtake these reads
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
+    const unsigned long long b = __double_as_longlong(lm);
+    lev += (double)((int)((b >> 52) & 0x7ff) - 1022);
+    lm = __longlong_as_double((b & 0x800fffffffffffffULL) | 0x3fe0000000000000ULL);
+  }
+  ll += (log(lm) + lev * M_LN2) + lspec;
+
+  // epilogue: lane (X = m, b, Y = n) holds, per bin group g, the 4x4 blocks
+  // D[m][n] of bin f0 + 4g + b: cross (j = m, c = 4h + n), pairs (p = 4h + m, c = n)
+  __syncthreads();  // s_red aliases the W tile and the slabs
+  double *red = s_red + wv * NACC * 16;
+  {
+    const int m = lane >> 4, bb = (lane >> 2) & 3, n = lane & 3;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int bin = 4 * g + bb;
+      if (m < J) {
+        red[(4 * NP + 8 * m + n) * 16 + bin] = xacc[g][0];
+        red[(4 * NP + 8 * m + 4 + n) * 16 + bin] = xacc[g][1];
+      }
+#pragma unroll
+      for (int h = 0; h < NPG; ++h)
+        if (4 * h + m < NP) red[(4 * (4 * h + m) + n) * 16 + bin] = pacc[g][h];
+    }
+  }
+#pragma unroll
+  for (int mm = 1; mm < 64; mm <<= 1) ll += __shfl_xor(ll, mm, 64);
+  if (lane == 0) s_ll[wv] = ll;
+  __syncthreads();
+  for (int idx = tid; idx < NACC * 16; idx += 256) {
+    const int u = idx >> 4, ff = idx & 15;
+    const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
+                     s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
+    a.part[((size_t)blockIdx.y * a.Fp + f0 + ff) * NACC + u] = x;
+  }
+  if (tid == 0)
+    a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+}
+
 // sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
 __global__ void k_tw_rowsum(const double *__restrict__ TW, double *__restrict__ hsum, int T,
                             int Tp, const int *halt) {
@@ -1485,6 +1787,13 @@ static void launch_estep(fasst_ctx *c, const EArgs &e) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
     dim3 grid(c->nft, c->nchunk_e);
+    if (!c->estep_split && !T::AB) {
+      prof_begin(c, KESTEP);
+      k_estep_mx<T::J, T::NKS, T::RKU>
+          <<<grid, 256, estep_mx_smem<T::J, T::NKS>(), c->stream>>>(e);
+      prof_end(c, KESTEP);
+      return;
+    }
     prof_begin(c, KESTEP);
     k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
     prof_end(c, KESTEP);
@@ -1500,6 +1809,16 @@ static int estep_occupancy(const fasst_ctx *c) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
     int n1 = 0, n2 = 0;
+    if (!c->estep_split && !T::AB) {
+      constexpr size_t smem = estep_mx_smem<T::J, T::NKS>();
+      (void)hipFuncSetAttribute((const void *)k_estep_mx<T::J, T::NKS, T::RKU>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n1, k_estep_mx<T::J, T::NKS, T::RKU>, 256,
+                                                       smem) != hipSuccess)
+        n1 = 1;
+      occ = std::max(1, n1);
+      return;
+    }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &n1, k_estep<T::J, T::NKS, T::RKU, 1, T::AB>, 256, estep_smem<T>(1)) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -1787,6 +2106,7 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   int st = FASST_OK;
   if (const char *ab = getenv("FASST_ABLATE")) c->ablate = atoi(ab);  // profiling only
   if (const char *nf = getenv("FASST_NOFORK")) c->nofork = atoi(nf);  // A/B only
+  if (const char *es = getenv("FASST_ESTEP_SPLIT")) c->estep_split = atoi(es);  // A/B only
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
