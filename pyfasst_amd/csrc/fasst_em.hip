@@ -488,8 +488,7 @@ struct MXShape {
 
 template <int J, int NKS>
 static constexpr size_t estep_mx_smem() {
-  return (size_t)(kMaxR * 4 * 16 + J * 4 * 16 + 4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) *
-         sizeof(double);
+  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) * sizeof(double);
 }
 
 // (the LDS slabs allow two blocks per CU, so the register budget is that of
@@ -503,11 +502,11 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
   constexpr int NP = S::NP, NPG = S::NPG;
   constexpr int NACC = 4 * NP + 8 * J;
   constexpr int KP = 4 * NKS;
-  constexpr int RK = RKU ? RKU : kMaxR;
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double *s_cr = smem;                     // [kMaxR][4][16] per-rank coefficients
-  double *s_cj = s_cr + kMaxR * 4 * 16;    // [J][4][16] per-source Sigma_x coefficients
-  double *s_ll = s_cj + J * 4 * 16;        // [4]
+  // per-source Sigma_x coefficients in a static array: the compiler can see
+  // that the slab stores never touch them and reuse each read within a tile
+  __shared__ double s_cj[J * 4 * 16];      // [J][4][16]
+  double *s_ll = smem;                     // [4]
   double *s_w = s_ll + 4;                  // [J][KP][16] W tile
   double *s_slab = s_w + J * KP * 16;      // [4 waves][SLAB] operand slabs
   double *s_red = s_w;                     // [4][NACC][16] (epilogue, aliases W + slabs)
@@ -532,18 +531,10 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
       for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
         const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + ff];
         const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + ff];
-        const double aa = a0.x * a0.x + a0.y * a0.y;
-        const double bb = a1.x * a1.x + a1.y * a1.y;
-        const double cr = a0.x * a1.x + a0.y * a1.y;  // Re a0 conj(a1)
-        const double ci = a0.y * a1.x - a0.x * a1.y;  // Im a0 conj(a1)
-        s_cr[(r * 4 + 0) * 16 + tid] = aa;
-        s_cr[(r * 4 + 1) * 16 + tid] = bb;
-        s_cr[(r * 4 + 2) * 16 + tid] = 2.0 * cr;
-        s_cr[(r * 4 + 3) * 16 + tid] = 2.0 * ci;
-        al += aa;
-        be += bb;
-        gr += cr;
-        gi += ci;
+        al += a0.x * a0.x + a0.y * a0.y;
+        be += a1.x * a1.x + a1.y * a1.y;
+        gr += a0.x * a1.x + a0.y * a1.y;  // Re a0 conj(a1)
+        gi += a0.y * a1.x - a0.x * a1.y;  // Im a0 conj(a1)
       }
       s_cj[(j * 4 + 0) * 16 + tid] = al;
       s_cj[(j * 4 + 1) * 16 + tid] = be;
@@ -553,14 +544,10 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
   }
   __syncthreads();
 
-  int r0[J], rk[J];
   double inv_rk[J];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    r0[j] = RKU ? RKU * j : a.roff[j];
-    rk[j] = RKU ? RKU : a.roff[j + 1] - a.roff[j];
-    inv_rk[j] = 1.0 / (double)rk[j];
-  }
+  for (int j = 0; j < J; ++j)
+    inv_rk[j] = RKU ? 1.0 / (double)RKU : 1.0 / (double)(a.roff[j + 1] - a.roff[j]);
   const double psd = a.psd[f];
   const bool fvalid = f < a.F;
   // writer side: this lane's point goes to bin group g = fl / 4, block b = fl % 4, X = tq
@@ -610,7 +597,6 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 #pragma unroll
       for (int s = 0; s < NKS; ++s) v[j] = mfma4(twv[j][s], sw[4 * s * 16], v[j]);
     }
-    const double *cr = s_cr + lofs + fl;
     const double *cj = s_cj + lofs + fl;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -677,24 +663,22 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 #pragma unroll
           for (int j2 = j1; j2 < J; ++j2, ++p) wr[(4 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
       }
-      // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414),
-      // stored as rho = (hat_W / vm^2) vm, vm = max(V, eps): the FB ratio of
-      // update_spectral_components (:1521-1575, N1), formed where V is at hand
+      // hat_W[j] = mean over the ranks of j of |V^2 a_r^H N a_r + V| (:727-729,
+      // :413-414) in the rank-merged form |V^2 (sum_r a_r^H N a_r) / rk + V|
+      // (each rank's term is a posterior second moment, >= 0: the two forms
+      // differ by rounding), with sum_r a_r^H N a_r = tr(N sum_r a_r a_r^H) from
+      // the Sigma_x coefficients; stored as rho = (hat_W / vm^2) vm,
+      // vm = max(V, eps): the FB ratio of update_spectral_components
+      // (:1521-1575, N1), formed where V is at hand
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const double Vj = V[j];
-        double hw = 0.0;
-#pragma unroll
-        for (int q = 0; q < RK; ++q)
-          if (RKU || q < rk[j]) {
-            const double *c = cr + (r0[j] + q) * 64;
-            const double qa = c[0] * n00 + c[16] * n11 + (c[32] * n01r + c[48] * n01i);
-            hw += fabs((Vj * Vj) * qa + Vj);
-          }
-        const double hwm = RKU == 1 ? hw : hw * inv_rk[j];
+        const double qa = (cj[(j * 4 + 0) * 16] * n00 + cj[(j * 4 + 1) * 16] * n11) +
+                          2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i);
+        const double hw = fabs((Vj * Vj) * (RKU == 1 ? qa : qa * inv_rk[j]) + Vj);
         const double vm = fmax(Vj, kEps);
         const double rv = rcp_nr(vm);
-        __builtin_nontemporal_store((hwm * (rv * rv)) * vm,
+        __builtin_nontemporal_store((hw * (rv * rv)) * vm,
                                     a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
       }
       // the slab writes above must land before the cross-lane reads below
@@ -702,15 +686,20 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // all operands of the 4 bin groups in flight at once, then the MFMAs
+      // (read -> wait -> MFMA one at a time left the LDS latency exposed)
+      double opd[4][4 + NPG];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int q = 0; q < 4 + NPG; ++q) opd[g][q] = rd[g * S::GS + q * 64];
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const double *o = rd + g * S::GS;
-        const double av = o[0 * 64];
-        xacc[g][0] = mfma44(av, o[1 * 64], xacc[g][0]);
-        xacc[g][1] = mfma44(av, o[2 * 64], xacc[g][1]);
-        const double bn = o[3 * 64];
+        xacc[g][0] = mfma44(opd[g][0], opd[g][1], xacc[g][0]);
+        xacc[g][1] = mfma44(opd[g][0], opd[g][2], xacc[g][1]);
 #pragma unroll
-        for (int h = 0; h < NPG; ++h) pacc[g][h] = mfma44(o[(4 + h) * 64], bn, pacc[g][h]);
+        for (int h = 0; h < NPG; ++h) pacc[g][h] = mfma44(opd[g][4 + h], opd[g][3], pacc[g][h]);
       }
       // the next point's slab writes must not overtake these reads
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
