@@ -35,13 +35,13 @@ def kernel_work(F, T, J, R, K):
     however often a kernel chooses to recompute it; `exec_flops` is what the
     kernel actually issues, for reference only).
 
-    k_estep_part1: V tiles 2JK (the only algorithmic V before the E-step),
-                   Sigma_x, 2x2 inverse, loglik, N = S Cx S - S, the
-                   J(J+1)/2 pair statistics and hat_W ~ (8J + 70 + 9 J(J+1)/2)
-                   per (f,t); bytes 32 (Cx read) + 8J (rho write) per (f,t)
-    k_estep_part2: P = Cx S and the cross statistics ~ (17J + 10R) per (f,t)
-                   (its V tiles are a recompute); no algorithmic bytes (its Cx
-                   read is a re-read)
+    k_estep:       the single-pass E-step: V tiles 2JK (the only algorithmic V
+                   before the E-step), Sigma_x 8J, the guarded 2x2 inverse,
+                   loglik, P and N ~70, the cross and pair statistics
+                   2 (8J + 4 J(J+1)/2), hat_W ~8J per (f,t); bytes 32 (Cx
+                   read) + 8J (rho write) per (f,t)
+    k_estep_part1 / k_estep_part2: the round-1 two-pass E-step (A/B only,
+                   FASST_ESTEP_SPLIT=1); part 2's V tiles are a recompute
     k_fb_contract: FB numerator 2K per (f,t,j); bytes 8 (rho) per (f,t,j)
     k_tw_contract: V after the FB update 2K + TW numerator 2K + denominator
                    2K per (f,t,j) (its V_old tiles are a recompute); bytes 8
@@ -49,7 +49,9 @@ def kernel_work(F, T, J, R, K):
     """
     ft = float(F) * T
     np_ = J * (J + 1) / 2
+    estep = ft * (2 * J * K + 8 * J + 70 + 2 * (8 * J + 4 * np_) + 8 * J)
     return {
+        "k_estep": dict(flops=estep, exec_flops=estep, bytes=ft * (32 + 8 * J)),
         "k_estep_part1": dict(flops=ft * (2 * J * K + 8 * J + 70 + 9 * np_),
                               exec_flops=ft * (2 * J * K + 8 * J + 70 + 9 * np_),
                               bytes=ft * (32 + 8 * J)),

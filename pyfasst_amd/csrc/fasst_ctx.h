@@ -52,7 +52,7 @@ struct fasst_ctx {
   double *h_ll = nullptr;        // pinned host mirror (one value)
   int psd_cap = 0, ll_cap = 0;
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
-  static constexpr int kNK = 13;
+  static constexpr int kNK = 14;
   int prof = 0;
   int ablate = 0;  // FASST_ABLATE (profiling builds of the E-step; never in the product)
   hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};

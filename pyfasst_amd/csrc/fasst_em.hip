@@ -1503,12 +1503,12 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
 
 // ---------------------------------------------------------------- host side
 enum KernelId {
-  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KESTEP2
+  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KESTEP2, KESTEP1
 };
 static const char *kKernelNames[fasst_ctx::kNK] = {
-    "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep_part1", "k_loglik", "k_mix",
+    "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep", "k_loglik", "k_mix",
     "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm", "k_tw_update",
-    "k_estep_part2"};
+    "k_estep_part2", "k_estep_part1"};
 
 static inline void prof_begin(fasst_ctx *c, int id) {
   if (c->prof) {
@@ -1783,9 +1783,9 @@ static void launch_estep(fasst_ctx *c, const EArgs &e) {
       prof_end(c, KESTEP);
       return;
     }
-    prof_begin(c, KESTEP);
+    prof_begin(c, KESTEP1);
     k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
-    prof_end(c, KESTEP);
+    prof_end(c, KESTEP1);
     prof_begin(c, KESTEP2);
     k_estep<T::J, T::NKS, T::RKU, 2, T::AB><<<grid, 256, estep_smem<T>(2), c->stream>>>(e);
     prof_end(c, KESTEP2);

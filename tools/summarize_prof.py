@@ -20,6 +20,8 @@ def short(name):
     m = re.search(r"fasst::k_estep<\d+, \d+, \d+, (\d), \d+>", name)
     if m:
         return "k_estep_part%s" % m.group(1)
+    if "fasst::k_estep_mx<" in name:
+        return "k_estep"
     m = re.search(r"fasst::(k_\w+)", name)
     return m.group(1) if m else name[:40]
 
