@@ -177,6 +177,188 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const GemmArgs g) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// k_gemm44: the same contract on v_mfma_f64_4x4x4_4b (74.7 TF measured on this
+// chip vs 47.7 for 16x16x4, profiles/r1_ubench_fp64.txt).  Lane
+// l = 16 X + 4 b + Y supplies A[m=Y][k=X] and B[k=X][n=Y] of block b and
+// receives D[m=X][n=Y] of block b (tools/probe_mfma4.hip).  Block b of one
+// instruction is rows 16 i + 4 b .. +3 of the wave tile, so the A fragment is
+// a 16 x 4 slice (one double per lane) and the B fragment a 4 x 4 slice that
+// all four blocks share (a broadcast LDS read):
+//   C[16 i + 4 b + X][4 j + Y] += sum_k A[16 i + 4 b + .][k] B[k][4 j + .]
+// A wave owns 16 RM x 4 RN outputs as RM x RN one-double accumulators and
+// reads RM + RN doubles per k-step of 4 (RM x RN MFMAs).  Block = NW waves
+// (WGM x WGN), tile BM = 16 RM WGM by BN = 4 RN WGN, large enough that the
+// L2 feed stays ~20 flop/B.  K advances in kGBK chunks staged in LDS with the
+// next chunk's loads in flight in registers.  LDS layouts are permuted so a
+// lane's RM A values and RN B values of one k are contiguous (ds_read_b128):
+//   A: row 16 i + q (q = 4 b + Y) of wave row wm at [k][64 wm' + q RM + i],
+//      pitch PA = 18 mod 32 doubles: the 16 lanes of every ds_read_b128 group
+//      cover the 64 banks once;
+//   B: column 4 j + Y of wave column wn at [k][wn (4 (RN+2)) + Y (RN+2) + j],
+//      pitch PB = 8 mod 32: distinct (X, Y) hit disjoint banks, equal ones
+//      broadcast.
+constexpr int g44pitch(int x, int r) { return x + ((r - x % 32) + 32) % 32; }
+
+template <bool TA, bool TB, int NB, int NW, int WGM, int RM, int RN>
+__global__ __launch_bounds__(64 * NW, 1) void k_gemm44(const GemmArgs g) {
+  constexpr int NT = 64 * NW, WGN = NW / WGM;
+  static_assert(WGM * WGN == NW && RM % 2 == 0 && RN % 2 == 0, "wave grid / b128 pairs");
+  constexpr int WM = 16 * RM, WN = 4 * RN;            // wave tile
+  constexpr int BM = WM * WGM, BN = WN * WGN;         // block tile
+  constexpr int SBW = 4 * (RN + 2);                   // B columns per wave slab in LDS
+  constexpr int PA = g44pitch(BM, 18), PB = g44pitch(SBW * WGN, 8);
+  constexpr int LA = kGBK * BM / NT, LB = NB * kGBK * BN / NT;
+  static_assert(kGBK * BM % NT == 0 && NB * kGBK * BN % NT == 0, "tile / thread mismatch");
+  constexpr int SA = kGBK * PA, SB = NB * kGBK * PB;  // doubles per LDS buffer
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int X = lane >> 4, bq = (lane >> 2) & 3, Y = lane & 3;
+  const int wm = wv / WGN, wn = wv % WGN;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kb = blockIdx.z * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  // block-uniform: every element of every chunk is inside the matrices
+  const bool interior = m0 + BM <= g.M && n0 + BN <= g.N && (ke - kb) % kGBK == 0;
+  double acc[NB][RM][RN];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[b][i][j] = 0.0;
+
+  // element q of this thread's share of a chunk: (k, m) of A, (b, k, n) of B
+  auto a_km = [&](int q, int &k, int &m) {
+    const int idx = tid + NT * q;
+    if (TA) {
+      k = idx / BM;
+      m = idx % BM;
+    } else {
+      m = idx / kGBK;
+      k = idx % kGBK;
+    }
+  };
+  auto b_bkn = [&](int q, int &b, int &k, int &n) {
+    const int idx = tid + NT * q;
+    b = idx / (kGBK * BN);
+    const int r = idx % (kGBK * BN);
+    if (TB) {
+      n = r / kGBK;
+      k = r % kGBK;
+    } else {
+      k = r / BN;
+      n = r % BN;
+    }
+  };
+  double ra[LA], rb[LB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < LA; ++q) {
+      int k, m;
+      a_km(q, k, m);
+      const int gm = m0 + m, gk = k0 + k;
+      const size_t off = TA ? (size_t)gk * g.lda + gm : (size_t)gm * g.lda + gk;
+      ra[q] = (interior || (gm < g.M && gk < ke)) ? g.A[off] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      int b, k, n;
+      b_bkn(q, b, k, n);
+      const int gn = n0 + n, gk = k0 + k;
+      const size_t off = TB ? (size_t)gn * g.ldb + gk : (size_t)gk * g.ldb + gn;
+      rb[q] = (interior || (gn < g.N && gk < ke)) ? g.B[b][off] : 0.0;
+    }
+  };
+  auto sstore = [&](double *sA, double *sB) {
+#pragma unroll
+    for (int q = 0; q < LA; ++q) {
+      int k, m;
+      a_km(q, k, m);
+      const int w = m / WM, r = m % WM;  // wave row, row in the wave tile
+      sA[k * PA + w * WM + (r & 15) * RM + (r >> 4)] = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < LB; ++q) {
+      int b, k, n;
+      b_bkn(q, b, k, n);
+      const int w = n / WN, c = n % WN;  // wave column, column in the wave tile
+      sB[b * kGBK * PB + k * PB + w * SBW + (c & 3) * (RN + 2) + (c >> 2)] = rb[q];
+    }
+  };
+
+  const int nch = (ke - kb + kGBK - 1) / kGBK;
+  if (nch > 0) {
+    gload(kb);
+    sstore(smem, smem + SA);
+  }
+  __syncthreads();
+  const int aofs = wm * WM + (4 * bq + Y) * RM;
+  const int bofs = wn * SBW + Y * (RN + 2);
+  for (int c = 0; c < nch; ++c) {
+    const double *sA = smem + (c & 1) * (SA + SB);
+    const double *sB = sA + SA;
+    if (c + 1 < nch) gload(kb + (c + 1) * kGBK);
+    // operands of k-step kk + 1 are read while the MFMAs of kk issue
+    double a[2][RM], bv[2][NB][RN];
+    auto lds_ops = [&](int kk, int slot) {
+      const int kr = 4 * kk + X;
+#pragma unroll
+      for (int i = 0; i < RM; i += 2) {
+        const double2 v = *(const double2 *)(sA + kr * PA + aofs + i);
+        a[slot][i] = v.x;
+        a[slot][i + 1] = v.y;
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < RN; j += 2) {
+          const double2 v = *(const double2 *)(sB + b * kGBK * PB + kr * PB + bofs + j);
+          bv[slot][b][j] = v.x;
+          bv[slot][b][j + 1] = v.y;
+        }
+    };
+    lds_ops(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < kGBK / 4; ++kk) {
+      const int cs = kk & 1;
+      if (kk + 1 < kGBK / 4) lds_ops(kk + 1, cs ^ 1);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[b][i][j] =
+                __builtin_amdgcn_mfma_f64_4x4x4f64(a[cs][i], bv[cs][b][j], acc[b][i][j], 0, 0, 0);
+    }
+    if (c + 1 < nch) {
+      double *dA = smem + ((c + 1) & 1) * (SA + SB);
+      sstore(dA, dA + SA);
+    }
+    __syncthreads();
+  }
+  const size_t zoff = (size_t)blockIdx.z * g.slab;
+  const int crow = m0 + wm * WM + 4 * bq + X;
+  const int ccol = n0 + wn * WN + Y;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int row = crow + 16 * i, col = ccol + 4 * j;
+        if (interior || (row < g.M && col < g.N))
+          g.C[b][zoff + (size_t)row * g.ldc + col] = acc[b][i][j];
+      }
+}
+
+template <bool TA, bool TB, int NB, int NW, int WGM, int RM, int RN>
+constexpr size_t gemm44_smem() {
+  constexpr int WGN = NW / WGM, BM = 16 * RM * WGM, SBW = 4 * (RN + 2);
+  return 2 * (size_t)(kGBK * g44pitch(BM, 18) + NB * kGBK * g44pitch(SBW * WGN, 8)) * sizeof(double);
+}
+
 // out[i] = sum_z part[z*slab + i] (fixed order), i < n
 __global__ void k_gemm_reduce(const double *__restrict__ part, int nz, size_t slab,
                               double *__restrict__ out, size_t n);
