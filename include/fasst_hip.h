@@ -78,6 +78,10 @@ int fasst_get_spatial(fasst_ctx *ctx, int j, double *params);
 int fasst_set_spectral(fasst_ctx *ctx, int j, const double *FB, const double *FW,
                        const double *TW, int fb_free, int tw_free);
 int fasst_get_spectral(fasst_ctx *ctx, int j, double *FB, double *FW, double *TW);
+/* FW_frdm_prior of source j ('free' = 1): the FW multiplicative update of
+ * update_spectral_components (audioModel.py:1578-1631) runs between the FB
+ * and TW updates.  Default after fasst_configure: fixed.                     */
+int fasst_set_fw_prior(fasst_ctx *ctx, int j, int fw_free);
 
 /* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j is
  * set when sum(TW_j) < eps: the caller draws the restart (host RNG order).  */

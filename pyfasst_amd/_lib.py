@@ -53,6 +53,7 @@ SIGNATURES = {
     "fasst_set_spectral": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _dp, ctypes.c_int,
                                           ctypes.c_int]),
     "fasst_get_spectral": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _dp]),
+    "fasst_set_fw_prior": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "fasst_renormalize": (ctypes.c_int, [_vp, _ip]),
     "fasst_run": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_double, _dp, _ip, _ip]),
     "fasst_wiener_images": (ctypes.c_int, [_vp, _dp, _dp, _dp]),

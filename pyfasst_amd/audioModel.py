@@ -171,8 +171,8 @@ class FASST(object):
         """Check the model is on the HIP path; return (order, ranks, Ks, conv).
 
         HIP path: stereo; one single-factor NMF spectral component per spatial
-        component (TB empty, TW_constr 'NMF', FW fixed); all spatial
-        components 'inst' or all 'conv'; lambdaCorr == 0.
+        component (TB empty, TW_constr 'NMF'; FB, FW, TW each free or fixed);
+        all spatial components 'inst' or all 'conv'; lambdaCorr == 0.
         """
         if self.audioObject.channels != 2:
             raise AttributeError("Nb channels " + str(self.audioObject.channels) +
@@ -197,8 +197,6 @@ class FASST(object):
                 raise NotImplementedError("time blobs (TB) are outside the HIP path")
             if fac.get('TW_constr', 'NMF') != 'NMF':
                 raise NotImplementedError("TW_constr=%s is outside the HIP path" % fac['TW_constr'])
-            if fac.get('FW_frdm_prior', 'fixed') == 'free':
-                raise NotImplementedError("free FW is outside the HIP path")
         if sorted(owner.keys()) != list(range(J)):
             raise NotImplementedError("every spatial component needs one spectral component")
         types = set(sc['mix_type'] for sc in self.spat_comps.values())
@@ -226,7 +224,8 @@ class FASST(object):
             fac = self.spec_comps[order[j]]['factor'][0]
             eng.set_spectral(j, fac['FB'], fac['FW'], fac['TW'],
                              fac.get('FB_frdm_prior', 'free') == 'free',
-                             fac.get('TW_frdm_prior', 'free') == 'free')
+                             fac.get('TW_frdm_prior', 'free') == 'free',
+                             fac.get('FW_frdm_prior', 'fixed') == 'free')
         return order, Ks, conv
 
     def _download(self, order, Ks, conv, updated_spatial=True):

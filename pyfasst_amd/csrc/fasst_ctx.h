@@ -37,12 +37,14 @@ struct fasst_ctx {
   int J = 0, R = 0, KP = 0, conv = 0, configured = 0;
   int rank[fasst::kMaxJ] = {0}, roff[fasst::kMaxJ + 1] = {0}, K[fasst::kMaxJ] = {0};
   int spat_free[fasst::kMaxJ] = {0}, fb_free[fasst::kMaxJ] = {0}, tw_free[fasst::kMaxJ] = {0};
+  int fw_free[fasst::kMaxJ] = {0};
   fasst::DBuf<double> FB, FW, TW, Wkf, Wkf_new, Wfk_new, FWHt, hatW;
   fasst::DBuf<double2> A, Pinst;
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
   int nsplit_t = 1, fpc_t = 1;  // TW contraction bin chunks
   fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rpmax, rpe, rtpart;
+  fasst::DBuf<double> gden, TWt, pnum, pden;  // FW update (free FW)
   int nchunk_r = 1;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart, [kFlagHalt] halt,
@@ -52,7 +54,7 @@ struct fasst_ctx {
   double *h_ll = nullptr;        // pinned host mirror (one value)
   int psd_cap = 0, ll_cap = 0;
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
-  static constexpr int kNK = 14;
+  static constexpr int kNK = 15;
   int prof = 0;
   int ablate = 0;  // FASST_ABLATE (profiling builds of the E-step; never in the product)
   hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};

@@ -100,7 +100,8 @@ __global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB
 // tile, source): FW and the TW tile staged in LDS, coalesced [t][k] writes.
 __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
                                                const double *__restrict__ TW,
-                                               double *__restrict__ FWHt, int J, int Tp, int KP, const int *halt) {
+                                               double *__restrict__ FWHt, double *__restrict__ TWt,
+                                               int J, int Tp, int KP, const int *halt) {
   HALT_GUARD(halt);
   extern __shared__ __attribute__((aligned(16))) double s_f[];
   double *s_fw = s_f;             // [KP][KP]
@@ -121,6 +122,7 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
     double s = 0.0;
     for (int q = 0; q < KP; ++q) s += s_fw[q * KP + k] * s_tw[q * 64 + tl];
     FWHt[((size_t)j * Tp + t0 + tl) * KP + k] = s;
+    if (TWt) TWt[((size_t)j * Tp + t0 + tl) * KP + k] = s_tw[k * 64 + tl];  // H^T (FW update)
   }
 }
 
@@ -1147,6 +1149,148 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- FW update
+// update_spectral_components, FW branch (audioModel.py:1578-1631), for the
+// sources whose FW_frdm_prior is 'free'.  With one NMF factor other =
+// max(V_old, eps) (N1) and the spatial power of the FW step is
+// vm = max(V_mid, eps), V_mid = (FB_new FW_old) H (comp_spat_comp_power after
+// the FB update, :1582-1588), so
+//   num[k1][k2] = sum_f FB_new[f][k1] sum_t (hat_W / vm^2) other H[k2][t]
+//   den[k1][k2] = sum_f FB_new[f][k1] sum_t (other / vm) H[k2][t]
+// k_fw_contract forms the two ratio tiles (V_old and V_mid on the MFMA pipe,
+// hat_W = rho * other from the E-step) and contracts them over t with H^T
+// (G[f][k] per frame chunk, the k_fb_contract operand layout); k_fw_reduce
+// contracts G with FB_new over bins (partials per bin chunk); k_fw_final
+// applies FW *= (num / max(den, eps))^omega.
+struct FWArgs {
+  const double *TW, *TWt, *Wkf_old, *Wkf_mid, *hatW, *FB;
+  double *gnum, *gden;  // [nchunk][J][Fp][KP]
+  double *pnum, *pden;  // [nfc][J][KP][KP]
+  double *FW;
+  int F, T, Fp, Tp, KP, J, ntt, tpc, nchunk, nfc, fpc;
+  int K[kMaxJ], fw_free[kMaxJ];
+  double omega;
+  const int *halt;
+};
+
+template <int NKC>
+__global__ __launch_bounds__(64) void k_fw_contract(const FWArgs a) {
+  HALT_GUARD(a.halt);
+  constexpr int NKS = 4 * NKC;
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int j = blockIdx.y;
+  if (!a.fw_free[j]) return;
+  const int f0 = blockIdx.x * 16, f = f0 + fl;
+  const int KP = a.KP;
+  double wo[NKS], wmid[NKS];  // B operands of the V tiles: W[k = tq + 4 s][f]
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    wo[s] = a.Wkf_old[((size_t)j * KP + tq + 4 * s) * a.Fp + f];
+    wmid[s] = a.Wkf_mid[((size_t)j * KP + tq + 4 * s) * a.Fp + f];
+  }
+  d4 gn[NKC], gd[NKC];
+#pragma unroll
+  for (int kc = 0; kc < NKC; ++kc) gn[kc] = gd[kc] = d4{0.0, 0.0, 0.0, 0.0};
+  const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
+  const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
+  for (int tt = tb; tt < te; ++tt) {
+    const int t0 = tt * 16;
+    const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
+    d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vm = vo;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const double h = tw[(size_t)(4 * s) * a.Tp];
+      vo = mfma4(h, wo[s], vo);
+      vm = mfma4(h, wmid[s], vm);
+    }
+    double rn[4], rd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 4 * i;
+      const bool ok = t < a.T && f < a.F;
+      const double rho = ok ? rhoj[(size_t)t * a.Fp + f] : 0.0;
+      const double other = fmax(vo[i], kEps);
+      const double rv = 1.0 / fmax(vm[i], kEps);
+      rn[i] = ok ? ((rho * other) * (rv * rv)) * other : 0.0;  // (hat_W / vm^2) other
+      rd[i] = ok ? other * rv : 0.0;                           // other (1 / vm)
+    }
+    const double *ht = a.TWt + ((size_t)j * a.Tp + t0 + tq) * KP + fl;  // H^T[t][k]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) {
+        const double h = ht[(size_t)(4 * i) * KP + kc * 16];
+        gn[kc] = mfma4(rn[i], h, gn[kc]);
+        gd[kc] = mfma4(rd[i], h, gd[kc]);
+      }
+  }
+  const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Fp;
+#pragma unroll
+  for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const size_t o = (base + f0 + tq + 4 * m) * KP + kc * 16 + fl;
+      a.gnum[o] = gn[kc][m];
+      a.gden[o] = gd[kc][m];
+    }
+}
+
+// partial FB_new^T G over the bins of chunk blockIdx.x (G summed over the
+// frame chunks first, in chunk order)
+__global__ __launch_bounds__(256) void k_fw_reduce(const FWArgs a) {
+  HALT_GUARD(a.halt);
+  const int j = blockIdx.y, fc = blockIdx.x;
+  if (!a.fw_free[j]) return;
+  const int KP = a.KP, K = a.K[j];
+  extern __shared__ __attribute__((aligned(16))) double s_g[];  // [fpc][KP] x 3
+  double *s_n = s_g, *s_d = s_g + a.fpc * KP, *s_b = s_g + 2 * a.fpc * KP;
+  const int fb = fc * a.fpc, fe = min(fb + a.fpc, a.F), nf = fe - fb;
+  for (int idx = threadIdx.x; idx < nf * KP; idx += blockDim.x) {
+    const int fl = idx / KP, k = idx % KP, f = fb + fl;
+    double n = 0.0, d = 0.0;
+    for (int c = 0; c < a.nchunk; ++c) {
+      const size_t o = (((size_t)c * a.J + j) * a.Fp + f) * KP + k;
+      n += a.gnum[o];
+      d += a.gden[o];
+    }
+    s_n[idx] = n;
+    s_d[idx] = d;
+    s_b[idx] = a.FB[((size_t)j * a.Fp + f) * KP + k];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+    const int k1 = idx / K, k2 = idx % K;
+    double n = 0.0, d = 0.0;
+    for (int fl = 0; fl < nf; ++fl) {
+      const double b = s_b[fl * KP + k1];
+      n += b * s_n[fl * KP + k2];
+      d += b * s_d[fl * KP + k2];
+    }
+    const size_t o = (((size_t)fc * a.J + j) * KP + k1) * KP + k2;
+    a.pnum[o] = n;
+    a.pden[o] = d;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fw_final(const FWArgs a) {
+  HALT_GUARD(a.halt);
+  const int j = blockIdx.x;
+  if (!a.fw_free[j]) return;
+  const int KP = a.KP, K = a.K[j];
+  double *FW = a.FW + (size_t)j * KP * KP;
+  for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+    const int k1 = idx / K, k2 = idx % K;
+    double n = 0.0, d = 0.0;
+    for (int fc = 0; fc < a.nfc; ++fc) {
+      const size_t o = (((size_t)fc * a.J + j) * KP + k1) * KP + k2;
+      n += a.pnum[o];
+      d += a.pden[o];
+    }
+    const double ratio = n / fmax(d, kEps);
+    FW[k1 * KP + k2] *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
+  }
+}
+
 // ---------------------------------------------------------------- TW update
 struct TArgs {
   const double *TW, *Wkf_old, *Wkf_new, *Wfk_new, *hatW;
@@ -1503,12 +1647,13 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
 
 // ---------------------------------------------------------------- host side
 enum KernelId {
-  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KESTEP2, KESTEP1
+  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KESTEP2, KESTEP1,
+  KFWU
 };
 static const char *kKernelNames[fasst_ctx::kNK] = {
     "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep", "k_loglik", "k_mix",
     "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm", "k_tw_update",
-    "k_estep_part2", "k_estep_part1"};
+    "k_estep_part2", "k_estep_part1", "k_fw_update"};
 
 static inline void prof_begin(fasst_ctx *c, int id) {
   if (c->prof) {
@@ -1588,6 +1733,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
     c->K[j] = K[j];
     c->roff[j + 1] = c->roff[j] + rank[j];
     c->spat_free[j] = c->fb_free[j] = c->tw_free[j] = 1;
+    c->fw_free[j] = 0;
   }
   const int Fp = c->Fp, Tp = c->Tp, KP = c->KP;
   // Launch shapes sized to whole rounds of resident blocks (a partial last
@@ -1642,6 +1788,11 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(epart, (size_t)c->nchunk_e * Fp * c->nacc);
   ALLOC(llpart, (size_t)c->nchunk_e * c->nft);
   ALLOC(bnum, (size_t)c->nchunk_b * J * Fp * KP);
+  // FW update (free FW only, allocated with the model so set_spectral may switch it on)
+  ALLOC(gden, (size_t)c->nchunk_b * J * Fp * KP);
+  ALLOC(TWt, (size_t)J * Tp * KP);
+  ALLOC(pnum, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
+  ALLOC(pden, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(tnum, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
@@ -1867,8 +2018,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   }
   prof_begin(c, KFWH);
+  bool any_fw = false;
+  for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
   k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, (size_t)(c->KP * c->KP + c->KP * 64) * sizeof(double),
-            side>>>(c->FW.p, c->TW.p, c->FWHt.p, J, c->Tp, c->KP, c->halt);
+            side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
+                    c->halt);
   prof_end(c, KFWH);
   FASST_LAUNCH_CHECK();
   k_tw_rowsum<<<J * c->KP, 256, 0, side>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
@@ -2045,6 +2199,53 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
                 c->stream>>>(u);
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
+  if (any_fw) {
+    // FW update (:1578-1631) between the FB and TW updates; W_new = FB_new FW_old
+    // from k_fb_update is the V_mid operand, then W_new is rebuilt with FW_new
+    FWArgs w;
+    w.TW = c->TW.p;
+    w.TWt = c->TWt.p;
+    w.Wkf_old = c->Wkf.p;
+    w.Wkf_mid = c->Wkf_new.p;
+    w.hatW = c->hatW.p;
+    w.FB = c->FB.p;
+    w.gnum = c->bnum.p;
+    w.gden = c->gden.p;
+    w.pnum = c->pnum.p;
+    w.pden = c->pden.p;
+    w.FW = c->FW.p;
+    w.F = c->F;
+    w.T = c->T;
+    w.Fp = c->Fp;
+    w.Tp = c->Tp;
+    w.KP = c->KP;
+    w.J = J;
+    w.ntt = c->ntt;
+    w.tpc = c->tpc_b;
+    w.nchunk = c->nchunk_b;
+    w.fpc = kFwFpc;
+    w.nfc = (c->F + kFwFpc - 1) / kFwFpc;
+    w.omega = omega;
+    w.halt = c->halt;
+    for (int j = 0; j < kMaxJ; ++j) {
+      w.K[j] = j < J ? c->K[j] : 0;
+      w.fw_free[j] = j < J ? c->fw_free[j] : 0;
+    }
+    prof_begin(c, KFWU);
+    const dim3 gc(c->nft, J, c->nchunk_b);
+    switch (nkc) {
+      case 1: k_fw_contract<1><<<gc, 64, 0, c->stream>>>(w); break;
+      case 2: k_fw_contract<2><<<gc, 64, 0, c->stream>>>(w); break;
+      default: k_fw_contract<4><<<gc, 64, 0, c->stream>>>(w); break;
+    }
+    k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
+    k_fw_final<<<J, 256, 0, c->stream>>>(w);
+    k_w_from_fb<<<dim3(c->nft, J), 256, (size_t)(16 * (c->KP + 1) + c->KP * c->KP) * sizeof(double),
+                  c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
+                               c->halt);
+    prof_end(c, KFWU);
+    FASST_LAUNCH_CHECK();
+  }
   switch (nkc) {
     case 1: launch_contract<1>(c, b, t, false); break;
     case 2: launch_contract<2>(c, b, t, false); break;
@@ -2225,6 +2426,13 @@ int fasst_get_spatial(fasst_ctx *c, int j, double *params) {
     for (int r = 0; r < nr; ++r)
       for (int ch = 0; ch < 2; ++ch) p[(size_t)ch * nr + r] = tmp[(size_t)r * 2 + ch];
   }
+  return FASST_OK;
+}
+
+int fasst_set_fw_prior(fasst_ctx *c, int j, int fw_free) {
+  int st = need_model(c, j);
+  if (st) return st;
+  c->fw_free[j] = fw_free ? 1 : 0;
   return FASST_OK;
 }
 

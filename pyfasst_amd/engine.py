@@ -83,12 +83,13 @@ class Engine(object):
         check(lib.fasst_get_spatial(self._h, int(j), dptr(out)), "fasst_get_spatial")
         return out
 
-    def set_spectral(self, j, FB, FW, TW, fb_free, tw_free):
+    def set_spectral(self, j, FB, FW, TW, fb_free, tw_free, fw_free=False):
         FB = np.ascontiguousarray(FB, dtype=np.float64)
         FW = np.ascontiguousarray(FW, dtype=np.float64)
         TW = np.ascontiguousarray(TW, dtype=np.float64)
         check(lib.fasst_set_spectral(self._h, int(j), dptr(FB), dptr(FW), dptr(TW),
                                      int(bool(fb_free)), int(bool(tw_free))), "fasst_set_spectral")
+        check(lib.fasst_set_fw_prior(self._h, int(j), int(bool(fw_free))), "fasst_set_fw_prior")
 
     def get_spectral(self, j, K):
         FB = np.empty((self.F, K))

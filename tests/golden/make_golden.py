@@ -43,6 +43,10 @@ CASES = {
                            tfbpo=12)),
     "em_conv_j1": dict(cls="MultiChanNMFConv", nbComps=1, nbNMFComps=3, spatial_rank=[2],
                        conv=True, n=3000, fs=8000, kw=dict(iter_num=3, wlen=128, hopsize=32)),
+    # FW_frdm_prior 'free' with a dense FW (tests/helpers.py apply_setup)
+    "em_fw_free": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=6, spatial_rank=2,
+                       conv=True, n=5000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64),
+                       setup='fw_free'),
 }
 
 
@@ -76,6 +80,10 @@ def run_case(name):
             spatial_rank=cfg['spatial_rank'], verbose=0, **cfg['kw'])
     if cfg['conv']:
         m.makeItConvolutive()
+    if cfg.get('setup'):
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from helpers import apply_setup
+        apply_setup(m, cfg['setup'])
     out = {'wav': data, 'fs': np.array(cfg['fs']), 'Cx': m.Cx,
            'psd_lim0': np.asarray(m.noise['ann_PSD_lim'][0]),
            'psd_lim1': np.asarray(m.noise['ann_PSD_lim'][1])}

@@ -16,7 +16,23 @@ CASES = {
     "em_conv_j1": (1, 3, [2], True, dict(iter_num=3, wlen=128, hopsize=32)),
     "em_mqt": (2, 6, 2, True, dict(iter_num=3, wlen=256, hopsize=64, transf='mqt', tffmin=200,
                                    tfbpo=12)),
+    # FW_frdm_prior 'free' with a dense positive FW (audioModel.py:1578-1631)
+    "em_fw_free": (3, 6, 2, True, dict(iter_num=4, wlen=256, hopsize=64, _setup='fw_free')),
 }
+
+
+def apply_setup(m, name):
+    """Structure changes applied after construction (and makeItConvolutive),
+    identically to the reference model (make_golden.py) and to the product."""
+    if name == 'fw_free':
+        for k in sorted(m.spec_comps.keys()):
+            fac = m.spec_comps[k]['factor'][0]
+            rs = np.random.RandomState(100 + k)
+            K = fac['FW'].shape[0]
+            fac['FW'] = fac['FW'] + 0.3 * np.abs(rs.randn(K, K))
+            fac['FW_frdm_prior'] = 'free'
+    else:
+        raise ValueError(name)
 
 # tests/golden/cqt.npz cases; mirrors CQT_CASES of tests/golden/make_golden.py
 CQT_CASES = (
@@ -87,4 +103,6 @@ def oracle_model_from_golden(g, case):
     R.init_nmf_inst(m, J, K, rank)
     if conv:
         R.make_convolutive(m)
+    if kw.get('_setup'):
+        apply_setup(m, kw['_setup'])
     return m, X

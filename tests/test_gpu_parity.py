@@ -12,7 +12,7 @@ import pytest
 import scipy.io.wavfile as wf
 
 import fasst_ref as R
-from helpers import CASES, load, oracle_model_from_golden, rel
+from helpers import CASES, apply_setup, load, oracle_model_from_golden, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +28,8 @@ def _am():
 def _product_model(case, g, tmp_path):
     am = _am()
     J, K, rank, conv, kw = CASES[case]
+    kw = dict(kw)
+    setup = kw.pop('_setup', None)
     wav = os.path.join(str(tmp_path), case + ".wav")
     wf.write(wav, int(g['fs']), g['wav'])
     np.random.seed(0)
@@ -35,6 +37,8 @@ def _product_model(case, g, tmp_path):
     m = cls(wav, nbComps=J, nbNMFComps=K, spatial_rank=rank, **kw)
     if conv:
         m.makeItConvolutive()
+    if setup:
+        apply_setup(m, setup)
     return m
 
 
@@ -116,6 +120,7 @@ def test_em_end_to_end_vs_reference(case, tmp_path):
         assert rel(m.spat_comps[j]['params'], g['init_params_%d' % j]) < 1e-14
         assert rel(m.spec_comps[j]['factor'][0]['FB'], g['init_FB_%d' % j]) < 1e-14
         assert rel(m.spec_comps[j]['factor'][0]['TW'], g['init_TW_%d' % j]) < 1e-14
+        assert rel(m.spec_comps[j]['factor'][0]['FW'], g['init_FW_%d' % j]) < 1e-14
     ll = m.estim_param_a_post_model()
     assert abs(ll[0] - g['e_loglik'].real) <= 1e-12 * abs(ll[0])
     assert rel(ll, g['logliks']) < TIGHT
@@ -124,6 +129,7 @@ def test_em_end_to_end_vs_reference(case, tmp_path):
         assert rel(m.spat_comps[j]['params'], g['final_params_%d' % j]) < TIGHT
         assert rel(m.spec_comps[j]['factor'][0]['FB'], g['final_FB_%d' % j]) < TIGHT
         assert rel(m.spec_comps[j]['factor'][0]['TW'], g['final_TW_%d' % j]) < TIGHT
+        assert rel(m.spec_comps[j]['factor'][0]['FW'], g['final_FW_%d' % j]) < TIGHT
     assert rel(m.noise['PSD'], g['final_psd']) < 1e-14
     S = m.separated_images()
     assert rel(np.abs(S), np.abs(g['images'])) < TIGHT
@@ -213,6 +219,36 @@ def test_fixed_components_vs_oracle():
         assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
         assert rel(m.spec_comps[j]['factor'][0]['FB'], o.spec_comps[j]['factor'][0]['FB']) < 1e-8
         assert rel(m.spec_comps[j]['factor'][0]['TW'], o.spec_comps[j]['factor'][0]['TW']) < 1e-8
+
+
+@pytest.mark.parametrize("F,T,J,K,rank,iters,omega,which", [
+    (129, 301, 4, 32, 2, 3, 1.0, "all"),    # C3 structure, every FW free
+    (65, 77, 2, 20, 1, 4, 0.7, "first"),    # K not a multiple of 16, omega != 1, one source
+    (97, 203, 3, 40, 2, 2, 1.0, "all"),     # K padded to 64
+])
+def test_free_fw_vs_oracle(F, T, J, K, rank, iters, omega, which):
+    """FW_frdm_prior 'free' (audioModel.py:1578-1631) with a dense positive FW:
+    the FW update between the FB and TW updates, against the oracle (itself
+    pinned to the reference by the em_fw_free golden case)."""
+    m, o, X = _c3_like(F, T, J, K, rank, iters)
+    for mod in (m, o):
+        mod.nmfUpdateCoeff = omega
+        for j in range(J if which == "all" else 1):
+            fac = mod.spec_comps[j]['factor'][0]
+            rs = np.random.RandomState(50 + j)
+            fac['FW'] = fac['FW'] + 0.2 * np.abs(rs.randn(K, K))
+            fac['FW_frdm_prior'] = 'free'
+        if which != "all":
+            mod.spec_comps[J - 1]['factor'][0]['FB_frdm_prior'] = 'fixed'
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for j in range(J):
+        for key in ('FB', 'FW', 'TW'):
+            assert rel(m.spec_comps[j]['factor'][0][key], o.spec_comps[j]['factor'][0][key]) < 1e-8, \
+                (j, key)
+        assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+    assert rel(np.abs(m.separated_images()), np.abs(o.separated_images(X))) < 1e-8
 
 
 def test_singular_mixing_raises_linalgerror():
