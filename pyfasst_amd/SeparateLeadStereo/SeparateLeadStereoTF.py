@@ -7,8 +7,10 @@ include/fasst_simm.h) and inverted with the SIMM-pipeline istft; and the
 melody tracking `runViterbi` (:1150-1319), whose Viterbi recursion runs on
 the GPU (`viterbi_tracking`, include/fasst_viterbi.h) -- the transition
 matrix and log-density of the HMM are built on the host exactly as the
-reference builds them.  The rest of the pipeline (file handling, F0
-estimation driver, chunking) is outside the accelerated path.
+reference builds them.  `SeparateLeadProcess` (below) drives the chunked WAV
+pipeline of the reference (`autoMelSepAndWrite`, `overlapAddChunks`,
+`writeSeparatedSignals`) on those kernels and on the GPU
+SIMM; only WAV file I/O and the chunk bookkeeping stay on the host.
 """
 import ctypes
 
