@@ -69,6 +69,14 @@ __global__ void k_nmf_h(double *__restrict__ H, const double *__restrict__ num,
     H[i] *= num[i] / fmax(den[i], kNmfEps);
 }
 
+// 1/x for finite normal x > 0: v_rcp_f64 + two Newton steps (<= 1 ulp), as
+// the FASST E-step (fasst_em.hip rcp_nr)
+__device__ __forceinline__ double nmf_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+
 __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -143,17 +151,29 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int tb = (blockIdx.y * 4 + wv) * tpc, te = min(tb + tpc, ntt);
-  for (int tt = tb; tt < te; ++tt) {
+  // the next frame tile's H operands and SX values are loaded while this
+  // tile's MFMAs run (the loop was L2-latency bound)
+  double th[2][NKS], hb[2][4][NKC], sxv[2][FPW][4];
+  auto load = [&](int tt, int slot) {
     const int t0 = tt * 16;
-    double th[NKS], hb[4][NKC];
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) th[s] = t0 + fl < N ? H[(size_t)(4 * s + tq) * N + t0 + fl] : 0.0;
+    for (int s = 0; s < NKS; ++s)
+      th[slot][s] = t0 + fl < N ? H[(size_t)(4 * s + tq) * N + t0 + fl] : 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int t = t0 + tq + 4 * i;
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) hb[i][kc] = t < N ? H[(size_t)(kc * 16 + fl) * N + t] : 0.0;
+      for (int kc = 0; kc < NKC; ++kc)
+        hb[slot][i][kc] = t < N ? H[(size_t)(kc * 16 + fl) * N + t] : 0.0;
+#pragma unroll
+      for (int p = 0; p < FPW; ++p) {
+        const int f = (ft0 + p) * 16 + fl;
+        sxv[slot][p][i] = (f < F && t < N) ? SXt[(size_t)t * F + f] : 0.0;
+      }
     }
+  };
+  auto compute = [&](int tt, int cs) {
+    const int t0 = tt * 16;
 #pragma unroll
     for (int p = 0; p < FPW; ++p) {
       if (ft0 + p >= nft) break;  // wave-uniform
@@ -161,8 +181,8 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
       d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;  // hat at (frame t0+tq+4i, bin f)
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
-        v = nmfma(th[s], wk[p][s], v);
-        v2 = nmfma(th[s + 1], wk[p][s + 1], v2);
+        v = nmfma(th[cs][s], wk[p][s], v);
+        v2 = nmfma(th[cs][s + 1], wk[p][s + 1], v2);
       }
       v += v2;
       double x[4], y[4];
@@ -171,17 +191,26 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
         const int t = t0 + tq + 4 * i;
         const bool ok = f < F && t < N;
         const double h = v[i];
-        const double sx = ok ? SXt[(size_t)t * F + f] : 0.0;
-        x[i] = ok ? sx / fmax(h * h, kNmfEps) : 0.0;
-        y[i] = ok ? 1.0 / fmax(h, kNmfEps) : 0.0;
+        x[i] = ok ? sxv[cs][p][i] * nmf_rcp(fmax(h * h, kNmfEps)) : 0.0;
+        y[i] = ok ? nmf_rcp(fmax(h, kNmfEps)) : 0.0;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) {
-          num[p][kc] = nmfma(x[i], hb[i][kc], num[p][kc]);
-          den[p][kc] = nmfma(y[i], hb[i][kc], den[p][kc]);
+          num[p][kc] = nmfma(x[i], hb[cs][i][kc], num[p][kc]);
+          den[p][kc] = nmfma(y[i], hb[cs][i][kc], den[p][kc]);
         }
+    }
+  };
+  // two tiles per trip so the double-buffer slot is a compile-time index
+  if (tb < te) load(tb, 0);
+  for (int tt = tb; tt < te; tt += 2) {
+    if (tt + 1 < te) load(tt + 1, 1);
+    compute(tt, 0);
+    if (tt + 1 < te) {
+      if (tt + 2 < te) load(tt + 2, 0);
+      compute(tt + 1, 1);
     }
   }
   const size_t slab = (size_t)K * F;
@@ -218,17 +247,28 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int fb = (blockIdx.y * 4 + wv) * fpc, fe = min(fb + fpc, nft);
-  for (int ft = fb; ft < fe; ++ft) {
+  // the next bin tile's W operands and SX values are loaded while this
+  // tile's MFMAs run
+  double ao[2][NKS], bw[2][4][NKC], sxv[2][TPW][4];
+  auto load = [&](int ft, int slot) {
     const int f0 = ft * 16;
-    double ao[NKS], bw[4][NKC];
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) ao[s] = f0 + fl < F ? W[(size_t)(f0 + fl) * K + 4 * s + tq] : 0.0;
+    for (int s = 0; s < NKS; ++s)
+      ao[slot][s] = f0 + fl < F ? W[(size_t)(f0 + fl) * K + 4 * s + tq] : 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = f0 + 4 * i + tq;
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) bw[i][kc] = f < F ? W[(size_t)f * K + kc * 16 + fl] : 0.0;
+      for (int kc = 0; kc < NKC; ++kc) bw[slot][i][kc] = f < F ? W[(size_t)f * K + kc * 16 + fl] : 0.0;
+#pragma unroll
+      for (int p = 0; p < TPW; ++p) {
+        const int t = (tt0 + p) * 16 + fl;
+        sxv[slot][p][i] = (f < F && t < N) ? SX[(size_t)f * N + t] : 0.0;
+      }
     }
+  };
+  auto compute = [&](int ft, int cs) {
+    const int f0 = ft * 16;
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
       if (tt0 + p >= ntt) break;  // wave-uniform
@@ -236,8 +276,8 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
       d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;  // hat at (bin f0+tq+4i, frame t)
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
-        v = nmfma(ao[s], bt[p][s], v);
-        v2 = nmfma(ao[s + 1], bt[p][s + 1], v2);
+        v = nmfma(ao[cs][s], bt[p][s], v);
+        v2 = nmfma(ao[cs][s + 1], bt[p][s + 1], v2);
       }
       v += v2;
       double x[4], y[4];
@@ -246,17 +286,25 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
         const int f = f0 + tq + 4 * i;
         const bool ok = f < F && t < N;
         const double h = v[i];
-        const double sx = ok ? SX[(size_t)f * N + t] : 0.0;
-        x[i] = ok ? sx / fmax(h * h, kNmfEps) : 0.0;
-        y[i] = ok ? 1.0 / fmax(h, kNmfEps) : 0.0;
+        x[i] = ok ? sxv[cs][p][i] * nmf_rcp(fmax(h * h, kNmfEps)) : 0.0;
+        y[i] = ok ? nmf_rcp(fmax(h, kNmfEps)) : 0.0;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) {
-          num[p][kc] = nmfma(x[i], bw[i][kc], num[p][kc]);
-          den[p][kc] = nmfma(y[i], bw[i][kc], den[p][kc]);
+          num[p][kc] = nmfma(x[i], bw[cs][i][kc], num[p][kc]);
+          den[p][kc] = nmfma(y[i], bw[cs][i][kc], den[p][kc]);
         }
+    }
+  };
+  if (fb < fe) load(fb, 0);
+  for (int ft = fb; ft < fe; ft += 2) {
+    if (ft + 1 < fe) load(ft + 1, 1);
+    compute(ft, 0);
+    if (ft + 1 < fe) {
+      if (ft + 2 < fe) load(ft + 2, 0);
+      compute(ft + 1, 1);
     }
   }
   const size_t slab = (size_t)K * N;
@@ -471,7 +519,7 @@ struct nmf_ctx {
   int F = 0, N = 0, K = 0;
   DBuf<double> SX, W, H, hat, X, Y, numT, denT, num, den, s, work;
   // fused path (K % 16 == 0, K <= 64): transposed copies and chunk partials
-  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1;
+  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1, pw = 1;
   DBuf<double> SXt, part;
 };
 
@@ -491,26 +539,35 @@ int model_xy(nmf_ctx *c) {
   return FASST_OK;
 }
 
-constexpr int kNmfFPW = 2, kNmfTPW = 2, kNmfCUs = 256;
+constexpr int kNmfCUs = 256;
 
-template <int NKC>
-static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
+// PW: 16-bin (W update) / 16-frame (H update) tiles per wave
+template <int NKC, int PW>
+static void nmf_fused_pw(nmf_ctx *c, int update_w, int update_h) {
   const int F = c->F, N = c->N, K = c->K;
   const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
   if (update_w) {
-    k_nmf_wnum<NKC, kNmfFPW><<<dim3((nft + kNmfFPW - 1) / kNmfFPW, c->ng_w), 256, 0, c->stream>>>(
+    k_nmf_wnum<NKC, PW><<<dim3((nft + PW - 1) / PW, c->ng_w), 256, 0, c->stream>>>(
         c->W.p, c->H.p, c->SXt.p, c->part.p, F, N, c->tpc_w);
     k_nmf_w_part<<<K, 256, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
   }
   const double *hs = update_w ? c->s.p : nullptr;
   if (update_h) {
-    k_nmf_hnum<NKC, kNmfTPW><<<dim3((ntt + kNmfTPW - 1) / kNmfTPW, c->ng_h), 256, 0, c->stream>>>(
+    k_nmf_hnum<NKC, PW><<<dim3((ntt + PW - 1) / PW, c->ng_h), 256, 0, c->stream>>>(
         c->W.p, c->H.p, hs, c->SX.p, c->part.p, F, N, c->fpc_h);
     k_nmf_h_part<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->part.p, c->ng_h, hs, K,
                                                                 N);
   } else if (update_w) {
     k_nmf_hscale<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->s.p, K, N);
   }
+}
+
+template <int NKC>
+static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
+  if (c->pw == 2)
+    nmf_fused_pw<NKC, 2>(c, update_w, update_h);
+  else
+    nmf_fused_pw<NKC, 1>(c, update_w, update_h);
 }
 
 int nmf_iteration(nmf_ctx *c, int update_w, int update_h) {
@@ -587,11 +644,20 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
   if (const char *v = getenv("FASST_NMF_FUSED")) c->fused = c->fused && atoi(v) != 0;
   if (c->fused) {
     const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
-    const int uw = (nft + kNmfFPW - 1) / kNmfFPW, uh = (ntt + kNmfTPW - 1) / kNmfTPW;
-    int ng = std::max(1, std::min((ntt + 3) / 4, kNmfCUs / uw));
+    // launch geometry: PW tiles per wave along the kept dimension, the
+    // contracted dimension split over 4 waves x ng groups so the grid holds
+    // about `waves` waves (A/B knobs FASST_NMF_PW / FASST_NMF_WAVES)
+    // (C2, F=1025 T=2000 K=64: 2 tiles per wave, ~1024 waves measured best,
+    // 0.103 ms per iteration; 1 tile: 0.106, 2048 waves: 0.124)
+    c->pw = 2;
+    int waves = 4 * kNmfCUs;
+    if (const char *v = getenv("FASST_NMF_PW")) c->pw = atoi(v) == 2 ? 2 : 1;
+    if (const char *v = getenv("FASST_NMF_WAVES")) waves = std::max(4, atoi(v));
+    const int uw = (nft + c->pw - 1) / c->pw, uh = (ntt + c->pw - 1) / c->pw;
+    int ng = std::max(1, std::min((ntt + 3) / 4, waves / (4 * uw)));
     c->tpc_w = (ntt + 4 * ng - 1) / (4 * ng);
     c->ng_w = ((ntt + c->tpc_w - 1) / c->tpc_w + 3) / 4;
-    ng = std::max(1, std::min((nft + 3) / 4, kNmfCUs / uh));
+    ng = std::max(1, std::min((nft + 3) / 4, waves / (4 * uh)));
     c->fpc_h = (nft + 4 * ng - 1) / (4 * ng);
     c->ng_h = ((nft + c->fpc_h - 1) / c->fpc_h + 3) / 4;
     const size_t np = std::max((size_t)c->ng_w * 2 * K * F, (size_t)c->ng_h * 2 * K * N);
