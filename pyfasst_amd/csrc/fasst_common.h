@@ -11,8 +11,8 @@
 namespace fasst {
 
 constexpr double kEps = 1e-10;  // audioModel.py:61, tools/signalTools.py:11
-constexpr int kMaxJ = 4;        // sources handled by the fused E-step
-constexpr int kMaxR = 8;        // total spatial rank
+constexpr int kMaxJ = 8;        // sources (spatial components)
+constexpr int kMaxR = 16;       // total spatial rank
 constexpr int kMaxKP = 64;      // padded NMF components
 constexpr int kFwFpc = 64;      // bins per block of the FW update's f-contraction
 constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge

@@ -150,6 +150,7 @@ struct EArgs {
   double *llpart;                         // [nchunk][nft]
   int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
   int roff[kMaxJ + 1];
+  int store_hat;  // 1: hatW holds hat_W itself (general structures), 0: rho = hat_W / max(V, eps)
   const int *halt;
 };
 
@@ -483,34 +484,46 @@ template <int J>
 struct MXShape {
   static constexpr int NP = J * (J + 1) / 2;
   static constexpr int NPG = (NP + 3) / 4;      // pair groups of 4
-  static constexpr int NSET = 4 + NPG;          // V | P lo | P hi | N | VV groups
+  static constexpr int NVG = (J + 3) / 4;       // source groups of 4
+  static constexpr int SP = NVG, SN = NVG + 2, SV2 = NVG + 3;  // set offsets: P lo/hi, N, VV
+  static constexpr int NSET = NVG + 3 + NPG;    // V groups | P lo | P hi | N | VV groups
   static constexpr int GS = NSET * 64 + 1;      // doubles per bin group (+1: bank skew)
   static constexpr int SLAB = 4 * GS;           // doubles per wave
 };
 
+// the W tile sits in LDS unless it would push the block past 160 KB (J = 8,
+// K = 64); then the V tiles read their W operand from L2
+template <int J, int NKS>
+__host__ __device__ constexpr bool mx_w_in_lds() {
+  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) * sizeof(double) <= 160 * 1024;
+}
 template <int J, int NKS>
 static constexpr size_t estep_mx_smem() {
-  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) * sizeof(double);
+  return (size_t)(4 + (mx_w_in_lds<J, NKS>() ? J * 4 * NKS * 16 : 0) + 4 * MXShape<J>::SLAB) *
+         sizeof(double);
 }
 
 // (the LDS slabs allow two blocks per CU, so the register budget is that of
 // two waves per SIMD: amdgpu_waves_per_eu tells the scheduler, which would
 // otherwise serialise the operand loads to fit three)
+// (more than 4 sources: one block per CU -- the slabs alone pass 80 KB -- so
+// one wave per SIMD and the full 512-register file)
 template <int J, int NKS, int RKU>
-__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_estep_mx(
-    const EArgs a) {
+__global__ __launch_bounds__(256, J > 4 ? 1 : 2)
+__attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) void k_estep_mx(const EArgs a) {
   HALT_GUARD(a.halt);
   using S = MXShape<J>;
-  constexpr int NP = S::NP, NPG = S::NPG;
+  constexpr int NP = S::NP, NPG = S::NPG, NVG = S::NVG;
   constexpr int NACC = 4 * NP + 8 * J;
   constexpr int KP = 4 * NKS;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // per-source Sigma_x coefficients in a static array: the compiler can see
   // that the slab stores never touch them and reuse each read within a tile
   __shared__ double s_cj[J * 4 * 16];      // [J][4][16]
+  constexpr bool WL = mx_w_in_lds<J, NKS>();
   double *s_ll = smem;                     // [4]
-  double *s_w = s_ll + 4;                  // [J][KP][16] W tile
-  double *s_slab = s_w + J * KP * 16;      // [4 waves][SLAB] operand slabs
+  double *s_w = s_ll + 4;                  // [J][KP][16] W tile (if WL)
+  double *s_slab = s_w + (WL ? J * KP * 16 : 0);  // [4 waves][SLAB] operand slabs
   double *s_red = s_w;                     // [4][NACC][16] (epilogue, aliases W + slabs)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -519,10 +532,11 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
   const int f = f0 + fl;
   double *slab = s_slab + wv * S::SLAB;
 
-  for (int idx = tid; idx < J * KP * 16; idx += 256) {
-    const int ff = idx & 15, jk = idx >> 4;
-    s_w[idx] = a.Wkf[(size_t)jk * a.Fp + f0 + ff];
-  }
+  if (WL)
+    for (int idx = tid; idx < J * KP * 16; idx += 256) {
+      const int ff = idx & 15, jk = idx >> 4;
+      s_w[idx] = a.Wkf[(size_t)jk * a.Fp + f0 + ff];
+    }
   // operand slots no point writes (sources >= J, pairs >= NP) stay zero
   for (int idx = tid; idx < 4 * S::SLAB; idx += 256) s_slab[idx] = 0.0;
   if (tid < 16) {
@@ -557,10 +571,11 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
   // reader side: operands of lane (X, b, Y) sit at [group][set][lane]
   const double *rd = slab + lane;
 
-  double xacc[4][2], pacc[4][NPG];  // D operands (4x4 blocks per bin group)
+  double xacc[4][NVG][2], pacc[4][NPG];  // D operands (4x4 blocks per bin group)
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    xacc[g][0] = xacc[g][1] = 0.0;
+#pragma unroll
+    for (int vg = 0; vg < NVG; ++vg) xacc[g][vg][0] = xacc[g][vg][1] = 0.0;
 #pragma unroll
     for (int h = 0; h < NPG; ++h) pacc[g][h] = 0.0;
   }
@@ -573,10 +588,13 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
     int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
     asm volatile("" : "+v"(lofs));
     // all TW operands in flight before the first MFMA (the scheduler would
-    // otherwise pair each load with its MFMA and wait on every one)
-    double twv[J][NKS];
+    // otherwise pair each load with its MFMA and wait on every one); with more
+    // than 32 operands (J > 4 or K > 32 at J = 4) the sources beyond the first
+    // 32 operands load next to their own MFMAs
+    constexpr int JA = (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
+    double twv[JA][NKS];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
+    for (int j = 0; j < JA; ++j) {
       const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
       for (int s = 0; s < NKS; ++s) twv[j][s] = tw[(size_t)(4 * s) * a.Tp];
@@ -596,8 +614,12 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
     for (int j = 0; j < J; ++j) {
       v[j] = d4{0.0, 0.0, 0.0, 0.0};
       const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+      const double *gw = a.Wkf + ((size_t)j * KP + tq) * a.Fp + f;
+      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) v[j] = mfma4(twv[j][s], sw[4 * s * 16], v[j]);
+      for (int s = 0; s < NKS; ++s)
+        v[j] = mfma4(j < JA ? twv[j < JA ? j : 0][s] : tw[(size_t)(4 * s) * a.Tp],
+                     WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
     }
     const double *cj = s_cj + lofs + fl;
 #pragma unroll
@@ -645,25 +667,26 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
       const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
       // this point's MFMA operands -> the wave's slab (reader layout)
 #pragma unroll
-      for (int j = 0; j < J; ++j) wr[0 * 64 + j] = V[j];
-      wr[1 * 64 + 0] = p00r;
-      wr[1 * 64 + 1] = p00i;
-      wr[1 * 64 + 2] = p01r;
-      wr[1 * 64 + 3] = p01i;
-      wr[2 * 64 + 0] = p10r;
-      wr[2 * 64 + 1] = p10i;
-      wr[2 * 64 + 2] = p11r;
-      wr[2 * 64 + 3] = p11i;
-      wr[3 * 64 + 0] = n00;
-      wr[3 * 64 + 1] = n11;
-      wr[3 * 64 + 2] = n01r;
-      wr[3 * 64 + 3] = n01i;
+      for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
+      wr[(S::SP + 0) * 64 + 0] = p00r;
+      wr[(S::SP + 0) * 64 + 1] = p00i;
+      wr[(S::SP + 0) * 64 + 2] = p01r;
+      wr[(S::SP + 0) * 64 + 3] = p01i;
+      wr[(S::SP + 1) * 64 + 0] = p10r;
+      wr[(S::SP + 1) * 64 + 1] = p10i;
+      wr[(S::SP + 1) * 64 + 2] = p11r;
+      wr[(S::SP + 1) * 64 + 3] = p11i;
+      wr[S::SN * 64 + 0] = n00;
+      wr[S::SN * 64 + 1] = n11;
+      wr[S::SN * 64 + 2] = n01r;
+      wr[S::SN * 64 + 3] = n01i;
       {
         int p = 0;
 #pragma unroll
         for (int j1 = 0; j1 < J; ++j1)
 #pragma unroll
-          for (int j2 = j1; j2 < J; ++j2, ++p) wr[(4 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
+          for (int j2 = j1; j2 < J; ++j2, ++p)
+            wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
       }
       // hat_W[j] = mean over the ranks of j of |V^2 a_r^H N a_r + V| (:727-729,
       // :413-414) in the rank-merged form |V^2 (sum_r a_r^H N a_r) / rk + V|
@@ -680,7 +703,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
         const double hw = fabs((Vj * Vj) * (RKU == 1 ? qa : qa * inv_rk[j]) + Vj);
         const double vm = fmax(Vj, kEps);
         const double rv = rcp_nr(vm);
-        __builtin_nontemporal_store((hw * (rv * rv)) * vm,
+        __builtin_nontemporal_store(a.store_hat ? hw : (hw * (rv * rv)) * vm,
                                     a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
       }
       // the slab writes above must land before the cross-lane reads below
@@ -690,18 +713,22 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // all operands of the 4 bin groups in flight at once, then the MFMAs
       // (read -> wait -> MFMA one at a time left the LDS latency exposed)
-      double opd[4][4 + NPG];
+      double opd[4][S::NSET];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int q = 0; q < 4 + NPG; ++q) opd[g][q] = rd[g * S::GS + q * 64];
+        for (int q = 0; q < S::NSET; ++q) opd[g][q] = rd[g * S::GS + q * 64];
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        xacc[g][0] = mfma44(opd[g][0], opd[g][1], xacc[g][0]);
-        xacc[g][1] = mfma44(opd[g][0], opd[g][2], xacc[g][1]);
 #pragma unroll
-        for (int h = 0; h < NPG; ++h) pacc[g][h] = mfma44(opd[g][4 + h], opd[g][3], pacc[g][h]);
+        for (int vg = 0; vg < NVG; ++vg) {
+          xacc[g][vg][0] = mfma44(opd[g][vg], opd[g][S::SP], xacc[g][vg][0]);
+          xacc[g][vg][1] = mfma44(opd[g][vg], opd[g][S::SP + 1], xacc[g][vg][1]);
+        }
+#pragma unroll
+        for (int h = 0; h < NPG; ++h)
+          pacc[g][h] = mfma44(opd[g][S::SV2 + h], opd[g][S::SN], pacc[g][h]);
       }
       // the next point's slab writes must not overtake these reads
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -724,9 +751,13 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(1, 2))) 
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int bin = 4 * g + bb;
-      if (m < J) {
-        red[(4 * NP + 8 * m + n) * 16 + bin] = xacc[g][0];
-        red[(4 * NP + 8 * m + 4 + n) * 16 + bin] = xacc[g][1];
+#pragma unroll
+      for (int vg = 0; vg < NVG; ++vg) {
+        const int j = 4 * vg + m;
+        if (j < J) {
+          red[(4 * NP + 8 * j + n) * 16 + bin] = xacc[g][vg][0];
+          red[(4 * NP + 8 * j + 4 + n) * 16 + bin] = xacc[g][vg][1];
+        }
       }
 #pragma unroll
       for (int h = 0; h < NPG; ++h)
@@ -823,7 +854,7 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 // stored for k_mix_inst.
 __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   HALT_GUARD(a.halt);
-  __shared__ double s_acc[4 * 10 + 8 * kMaxJ];
+  __shared__ double s_acc[4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ];
   __shared__ double2 s_A[kMaxR][2];
   __shared__ double2 s_L[kMaxR][kMaxR + 2];   // [M^T | hat_Rxs^T]
   __shared__ double2 s_H[kMaxR][kMaxR];
@@ -845,9 +876,9 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     s_sv[lane] = sv;
   }
   __syncthreads();
-  const int r1 = lane / R, r2 = lane % R;
-  const bool ent = lane < R * R;
-  if (ent) {
+  // hat_Rss entries (r1, r2), R^2 <= 256: four per lane at most
+  for (int e = lane; e < R * R; e += 64) {
+    const int r1 = e / R, r2 = e % R;
     const int j1 = a.jr[r1], j2 = a.jr[r2];
     const int lo = min(j1, j2), hi = max(j1, j2);
     const int p = lo * J - lo * (lo - 1) / 2 + (hi - lo);
@@ -863,10 +894,16 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     s_H[r1][r2] = v;
   }
   __syncthreads();
-  double2 h = make_double2(0.0, 0.0);
-  if (ent) {
-    const double2 x = s_H[r1][r2], y = s_H[r2][r1];
-    h = cscale(cadd(x, cconj(y)), 0.5);
+  double2 hv[4];  // hermitised entries of this lane (e = lane + 64 q)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = lane + 64 * q;
+    hv[q] = make_double2(0.0, 0.0);
+    if (e < R * R) {
+      const int r1 = e / R, r2 = e % R;
+      const double2 x = s_H[r1][r2], y = s_H[r2][r1];
+      hv[q] = cscale(cadd(x, cconj(y)), 0.5);
+    }
   }
   if (lane < 2 * R) {  // hat_Rxs[f][c][r] = sum_c' Q_j[c][c'] A_r,c' / T
     const int r = lane >> 1, c = lane & 1;
@@ -878,7 +915,11 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   if (!a.conv_update) {
     __syncthreads();
     if (a.rss) {
-      if (ent) a.rss[((size_t)f * R + r1) * R + r2] = h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = lane + 64 * q;
+        if (e < R * R) a.rss[((size_t)f * R + e / R) * R + e % R] = hv[q];
+      }
       if (lane < 2 * R) {
         const int r = lane >> 1, c = lane & 1;
         a.rxs[((size_t)f * 2 + c) * R + r] = s_L[r][R + c];
@@ -886,7 +927,11 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     }
     return;
   }
-  if (ent) s_L[r2][r1] = h;  // L = hermitised(hat_Rss)^T
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // L = hermitised(hat_Rss)^T
+    const int e = lane + 64 * q;
+    if (e < R * R) s_L[e % R][e / R] = hv[q];
+  }
   __syncthreads();
   const int W = R + 2;
   for (int k = 0; k < R; ++k) {
@@ -922,8 +967,8 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     if (lane > k && lane < R) s_mult[lane] = cmul(s_L[lane][k], cdiv(make_double2(1.0, 0.0), s_L[k][k]));
     __syncthreads();
     const int nr = R - k - 1, nc = W - k - 1;
-    if (lane < nr * nc) {
-      const int i = k + 1 + lane / nc, c = k + 1 + lane % nc;
+    for (int e = lane; e < nr * nc; e += 64) {
+      const int i = k + 1 + e / nc, c = k + 1 + e % nc;
       s_L[i][c] = csub(s_L[i][c], cmul(s_mult[i], s_L[k][c]));
     }
     __syncthreads();
@@ -1919,7 +1964,11 @@ static void estep_dispatch(const fasst_ctx *c, F &&f) {
     case 1: estep_dispatch_j<1>(c, f); break;
     case 2: estep_dispatch_j<2>(c, f); break;
     case 3: estep_dispatch_j<3>(c, f); break;
-    default: estep_dispatch_j<4>(c, f); break;
+    case 4: estep_dispatch_j<4>(c, f); break;
+    case 5: estep_dispatch_j<5>(c, f); break;
+    case 6: estep_dispatch_j<6>(c, f); break;
+    case 7: estep_dispatch_j<7>(c, f); break;
+    default: estep_dispatch_j<8>(c, f); break;
   }
 }
 
@@ -1927,19 +1976,21 @@ static void launch_estep(fasst_ctx *c, const EArgs &e) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
     dim3 grid(c->nft, c->nchunk_e);
-    if (!c->estep_split && !T::AB) {
+    if ((!c->estep_split || T::J > 4) && !T::AB) {
       prof_begin(c, KESTEP);
       k_estep_mx<T::J, T::NKS, T::RKU>
           <<<grid, 256, estep_mx_smem<T::J, T::NKS>(), c->stream>>>(e);
       prof_end(c, KESTEP);
       return;
     }
-    prof_begin(c, KESTEP1);
-    k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
-    prof_end(c, KESTEP1);
-    prof_begin(c, KESTEP2);
-    k_estep<T::J, T::NKS, T::RKU, 2, T::AB><<<grid, 256, estep_smem<T>(2), c->stream>>>(e);
-    prof_end(c, KESTEP2);
+    if constexpr (T::J <= 4) {  // round-1 two-pass E-step (A/B measurements only)
+      prof_begin(c, KESTEP1);
+      k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
+      prof_end(c, KESTEP1);
+      prof_begin(c, KESTEP2);
+      k_estep<T::J, T::NKS, T::RKU, 2, T::AB><<<grid, 256, estep_smem<T>(2), c->stream>>>(e);
+      prof_end(c, KESTEP2);
+    }
   });
 }
 
@@ -1949,7 +2000,7 @@ static int estep_occupancy(const fasst_ctx *c) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
     int n1 = 0, n2 = 0;
-    if (!c->estep_split && !T::AB) {
+    if ((!c->estep_split || T::J > 4) && !T::AB) {
       constexpr size_t smem = estep_mx_smem<T::J, T::NKS>();
       (void)hipFuncSetAttribute((const void *)k_estep_mx<T::J, T::NKS, T::RKU>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -1959,11 +2010,13 @@ static int estep_occupancy(const fasst_ctx *c) {
       occ = std::max(1, n1);
       return;
     }
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &n1, k_estep<T::J, T::NKS, T::RKU, 1, T::AB>, 256, estep_smem<T>(1)) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &n2, k_estep<T::J, T::NKS, T::RKU, 2, T::AB>, 256, estep_smem<T>(2)) != hipSuccess)
-      n1 = n2 = 1;
+    if constexpr (T::J <= 4) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &n1, k_estep<T::J, T::NKS, T::RKU, 1, T::AB>, 256, estep_smem<T>(1)) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &n2, k_estep<T::J, T::NKS, T::RKU, 2, T::AB>, 256, estep_smem<T>(2)) != hipSuccess)
+        n1 = n2 = 1;
+    }
     occ = std::max(1, std::min(n1, n2));
   });
   return occ;
@@ -2055,6 +2108,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.tpc = c->tpc_e;
   e.nft = c->nft;
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
+  e.store_hat = 0;
   launch_estep(c, e);
   FASST_LAUNCH_CHECK();
   if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below

@@ -682,7 +682,11 @@ int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double
     case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
     case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
     case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
-    default: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+    case 4: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+    case 5: k_wiener<5><<<grid, 64, 0, c->stream>>>(w); break;
+    case 6: k_wiener<6><<<grid, 64, 0, c->stream>>>(w); break;
+    case 7: k_wiener<7><<<grid, 64, 0, c->stream>>>(w); break;
+    default: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
   }
   FASST_LAUNCH_CHECK();
   k_tf_to_ft<<<dim3(c->ntt, c->nft, J * 2), 256, 0, c->stream>>>(dS.p, hS.p, c->F, c->T, c->Fp, c->Tp);
@@ -753,7 +757,11 @@ int fasst_separate_waveforms(fasst_ctx *c, const double *psd, const double *wind
     case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
     case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
     case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
-    default: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+    case 4: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+    case 5: k_wiener<5><<<grid, 64, 0, c->stream>>>(w); break;
+    case 6: k_wiener<6><<<grid, 64, 0, c->stream>>>(w); break;
+    case 7: k_wiener<7><<<grid, 64, 0, c->stream>>>(w); break;
+    default: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
   }
   FASST_LAUNCH_CHECK();
   // each image's frames are rows of its [Tp][Fp] plane: iSTFT straight from

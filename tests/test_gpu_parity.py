@@ -176,6 +176,10 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (33, 17, 3, 5, 2, 2),        # tiny F and T (one tile), odd K
     (97, 203, 3, 40, [1, 2, 1], 3),  # mixed ranks (general-rank E-step), K padded to 64
     (161, 250, 4, 16, 1, 3),     # rank 1 everywhere, K = 16 (one MFMA k block)
+    (65, 77, 6, 8, 2, 3),        # 6 sources, total rank 12
+    (49, 60, 8, 4, 1, 2),        # 8 sources of rank 1
+    (33, 40, 8, 16, 2, 2),       # 8 sources of rank 2: total rank 16 (the k_mix LU maximum)
+    (57, 70, 5, 36, [3, 2, 3, 2, 3], 2),  # 5 sources, mixed ranks 13, K padded to 64
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
@@ -248,6 +252,32 @@ def test_free_fw_vs_oracle(F, T, J, K, rank, iters, omega, which):
             assert rel(m.spec_comps[j]['factor'][0][key], o.spec_comps[j]['factor'][0][key]) < 1e-8, \
                 (j, key)
         assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+    assert rel(np.abs(m.separated_images()), np.abs(o.separated_images(X))) < 1e-8
+
+
+@pytest.mark.parametrize("J,rank", [(6, 2), (8, 1)])
+def test_inst_many_sources_vs_oracle(J, rank):
+    """'inst' mixing with more than 4 sources (total rank up to 12): the
+    f-averaged real R x R solve of update_mix_matrix (audioModel.py:808-839)."""
+    from pyfasst_amd import synthetic
+    from pyfasst_amd.audioObject import SpectralAudio
+    am = _am()
+    F, T, K = 65, 80, 6
+    X = synthetic.stereo_mixture(F, T, J=J, K_true=3, rank=1, seed=7)
+    np.random.seed(5)
+    m = am.MultiChanNMFInst_FASST(SpectralAudio(X=X), nbComps=J, nbNMFComps=K,
+                                  spatial_rank=rank, iter_num=3, wlen=128, hopsize=32)
+    o = R.RefFASST(iter_num=3)
+    o.set_transform([X[0], X[1]])
+    np.random.seed(5)
+    R.init_nmf_inst(o, J, K, rank)
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for j in range(J):
+        assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+        assert rel(m.spec_comps[j]['factor'][0]['FB'], o.spec_comps[j]['factor'][0]['FB']) < 1e-8
+        assert rel(m.spec_comps[j]['factor'][0]['TW'], o.spec_comps[j]['factor'][0]['TW']) < 1e-8
     assert rel(np.abs(m.separated_images()), np.abs(o.separated_images(X))) < 1e-8
 
 
