@@ -63,17 +63,52 @@ def test_run_viterbi_golden_gpu(tmp_path):
     assert (tmp_path / "pitch.txt").exists()
 
 
-@pytest.mark.parametrize("S,N,seed,kind", [(300, 400, 0, 1), (1093, 160, 1, 1), (138, 50, 2, 1),
-                                          (137, 50, 3, 0)])
-def test_viterbi_large_vs_oracle(S, N, seed, kind):
-    """Both kernel paths around the LDS-resident size (S <= 137: one workgroup;
-    beyond: one launch per frame), vs the oracle."""
+@pytest.mark.parametrize("S,N,seed,kind,force", [
+    (300, 400, 0, 2, None), (1093, 160, 1, 2, None), (138, 50, 2, 2, None), (137, 50, 3, 0, None),
+    (1093, 300, 5, 2, None), (1700, 40, 6, 2, None), (2400, 20, 7, 1, None),
+    (300, 400, 0, 1, "frame"), (1093, 160, 1, 1, "frame"), (138, 50, 2, 1, "frame")])
+def test_viterbi_large_vs_oracle(S, N, seed, kind, force, monkeypatch):
+    """All kernel paths around the LDS-resident size (S <= 137: one workgroup;
+    beyond: one persistent launch exchanging cum through tagged granules, or,
+    forced, one launch per frame), vs the oracle."""
+    if force:
+        monkeypatch.setenv("FASST_VT_PATH", force)
     rs = np.random.RandomState(seed)
     logD = np.log(rs.gamma(0.5, 1.0, size=(S + 1, N)))
     logT, prior = V.melody_transitions(S, 16)
     path = _gpu()(S, N, logD, prior, logT)
     assert _kind() == kind
     np.testing.assert_array_equal(path, V.viterbi_tracking(S, N, logD, prior, logT))
+
+
+@pytest.mark.parametrize("case", ["ties", "nan_block", "zeros"])
+def test_viterbi_persistent_ties_nan(case):
+    """The persistent path with the pyx's tie / NaN rules at a size where the
+    sources of one target are split over several waves (S = 700: 5 parts of
+    140): exact ties, a NaN row, a whole part of NaN sources, -inf frames, and
+    signed zeros (the winner's value is carried by value, its zero sign
+    re-formed from the index)."""
+    rs = np.random.RandomState(8)
+    S, N = 700, 60
+    logD = rs.randint(-2, 1, size=(S, N)).astype(float)
+    logT = rs.randint(-2, 1, size=(S, S)).astype(float)
+    logT[rs.rand(S, S) < 0.3] = -np.inf
+    logT[0, rs.rand(S) < 0.2] = np.nan
+    logT[400, :] = np.nan
+    logD[:, 9] = -np.inf
+    if case == "nan_block":
+        logT[560:, :] = np.nan
+        logT[:140, 3] = np.nan
+    if case == "zeros":
+        logD[:] = 0.0
+        logT = np.where(rs.rand(S, S) < 0.5, 0.0, -0.0)
+        logT[rs.rand(S, S) < 0.2] = -np.inf
+    prior = np.zeros(S)
+    with np.errstate(invalid='ignore'):
+        ref = V.viterbi_tracking(S, N, logD, prior, logT)
+    path = _gpu()(S, N, logD, prior, logT)
+    assert _kind() == 2
+    np.testing.assert_array_equal(path, ref)
 
 
 def test_viterbi_nan_and_inf_rules():
