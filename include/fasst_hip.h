@@ -83,8 +83,22 @@ int fasst_get_spectral(fasst_ctx *ctx, int j, double *FB, double *FW, double *TW
  * and TW updates.  Default after fasst_configure: fixed.                     */
 int fasst_set_fw_prior(fasst_ctx *ctx, int j, int fw_free);
 
-/* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j is
- * set when sum(TW_j) < eps: the caller draws the restart (host RNG order).  */
+/* Several spectral components on spatial component j (comp_spat_comp_power's
+ * sum over spec_comps, audioModel.py:430-498; sequential per-component
+ * update, :1479-1727): source j's FB / FW / TW (set by fasst_set_spectral)
+ * hold the nblk components side by side, component b in columns / rows
+ * [kb[b], kb[b + 1]) (kb[0] = 0, kb[nblk] = K_j, FW block diagonal), in the
+ * reference's spec_comps key order; fb_free[b] / tw_free[b] are component
+ * b's priors.  Restart flags (fasst_run / fasst_renormalize restart_mask)
+ * then count one bit per component: bit (sum of nblk of the sources before
+ * j) + b.  Free FW with several components: fasst_run returns
+ * FASST_ERR_UNSUPPORTED.                                                     */
+int fasst_set_blocks(fasst_ctx *ctx, int j, int nblk, const int *kb, const int *fb_free,
+                     const int *tw_free);
+
+/* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j (or
+ * bit per spectral component, fasst_set_blocks) is set when sum(TW) < eps:
+ * the caller draws the restart (host RNG order).                            */
 int fasst_renormalize(fasst_ctx *ctx, int *restart_mask);
 
 /* n_iter GEM iterations (GEM_iteration, audioModel.py:384-428), with the
@@ -101,6 +115,17 @@ int fasst_run(fasst_ctx *ctx, int n_iter, const double *psd, double omega,
  * the last annealed PSD; X complex128 [2][F][T] or NULL to use the resident
  * STFT; S out complex128 [J][2][F][T].                                       */
 int fasst_wiener_images(fasst_ctx *ctx, const double *psd, const double *X, double *S);
+
+/* Separation sources for fasst_wiener_images / fasst_separate_waveforms
+ * (separate_comps' spec_comp_ind, audioModel.py:1130-1164): source n sums the
+ * terms [term_off[n], term_off[n + 1]); term i is the spectral components in
+ * columns term_mask[i] (bit k = column k, fasst_set_blocks layout) of spatial
+ * component term_j[i] (compute_sigma_comp_2d, :1327-1372).  Sigma_x is the
+ * sum over the sources plus the PSD (compute_inv_sigma_mix_2d, :1374-1394).
+ * nsrc = 0 (the default): one source per spatial component, all columns.
+ * The outputs then hold nsrc sources instead of J.                          */
+int fasst_set_sources(fasst_ctx *ctx, int nsrc, const int *term_off, const int *term_j,
+                      const unsigned long long *term_mask);
 
 /* separate_comps up to the waveforms it writes (audioModel.py:1088-1233):
  * the Wiener images above, then the per-source, per-channel iSTFT

@@ -168,11 +168,16 @@ class FASST(object):
 
     # ---------------------------------------------------------------- structure
     def _structure(self):
-        """Check the model is on the HIP path; return (order, ranks, Ks, conv).
+        """Check the model is on the HIP path; return (order, ranks, Ks, conv),
+        order[j] = the keys of spatial component j's spectral components in
+        the reference's key order (update_spectral_components iterates
+        spec_comps.items(), audioModel.py:1479).
 
-        HIP path: stereo; one single-factor NMF spectral component per spatial
-        component (TB empty, TW_constr 'NMF'; FB, FW, TW each free or fixed);
-        all spatial components 'inst' or all 'conv'; lambdaCorr == 0.
+        HIP path: stereo; single-factor NMF spectral components (TB empty,
+        TW_constr 'NMF'; FB, FW, TW each free or fixed), one or several per
+        spatial component (comp_spat_comp_power sums them, :469-498; free FW
+        only with one per spatial component); all spatial components 'inst' or
+        all 'conv'; lambdaCorr == 0.
         """
         if self.audioObject.channels != 2:
             raise AttributeError("Nb channels " + str(self.audioObject.channels) +
@@ -183,12 +188,9 @@ class FASST(object):
         if sorted(self.spat_comps.keys()) != list(range(J)):
             raise NotImplementedError("spatial components must be numbered 0..J-1")
         owner = {}
-        for k, comp in self.spec_comps.items():
-            j = comp['spat_comp_ind']
-            if j in owner:
-                raise NotImplementedError("several spectral components per spatial component "
-                                          "are outside the HIP path")
-            owner[j] = k
+        for k in sorted(self.spec_comps.keys()):
+            comp = self.spec_comps[k]
+            owner.setdefault(comp['spat_comp_ind'], []).append(k)
             facs = comp['factor']
             if list(facs.keys()) != [0]:
                 raise NotImplementedError("multi-factor spectral components are outside the HIP path")
@@ -198,7 +200,12 @@ class FASST(object):
             if fac.get('TW_constr', 'NMF') != 'NMF':
                 raise NotImplementedError("TW_constr=%s is outside the HIP path" % fac['TW_constr'])
         if sorted(owner.keys()) != list(range(J)):
-            raise NotImplementedError("every spatial component needs one spectral component")
+            raise NotImplementedError("every spatial component needs a spectral component")
+        if any(len(v) > 1 for v in owner.values()) and any(
+                self.spec_comps[k]['factor'][0].get('FW_frdm_prior', 'fixed') == 'free'
+                for k in self.spec_comps):
+            raise NotImplementedError("free FW with several spectral components per spatial "
+                                      "component is outside the HIP path")
         types = set(sc['mix_type'] for sc in self.spat_comps.values())
         if len(types) != 1:
             raise NotImplementedError("mixed inst/conv spatial components are outside the HIP path")
@@ -211,7 +218,7 @@ class FASST(object):
         for j in range(J):
             p = self.spat_comps[j]['params']
             ranks.append(p.shape[0] if conv else p.shape[1])
-            Ks.append(self.spec_comps[owner[j]]['factor'][0]['FB'].shape[1])
+            Ks.append(int(sum(self.spec_comps[k]['factor'][0]['FB'].shape[1] for k in owner[j])))
         return [owner[j] for j in range(J)], ranks, Ks, conv
 
     def _upload(self):
@@ -221,11 +228,23 @@ class FASST(object):
         for j in range(len(order)):
             sc = self.spat_comps[j]
             eng.set_spatial(j, sc['params'], sc['frdm_prior'] == 'free')
-            fac = self.spec_comps[order[j]]['factor'][0]
-            eng.set_spectral(j, fac['FB'], fac['FW'], fac['TW'],
-                             fac.get('FB_frdm_prior', 'free') == 'free',
-                             fac.get('TW_frdm_prior', 'free') == 'free',
-                             fac.get('FW_frdm_prior', 'fixed') == 'free')
+            facs = [self.spec_comps[k]['factor'][0] for k in order[j]]
+            fb_free = [f.get('FB_frdm_prior', 'free') == 'free' for f in facs]
+            tw_free = [f.get('TW_frdm_prior', 'free') == 'free' for f in facs]
+            if len(facs) == 1:
+                FB, FW, TW = facs[0]['FB'], facs[0]['FW'], facs[0]['TW']
+            else:   # the components side by side, FW block diagonal
+                FB = np.hstack([f['FB'] for f in facs])
+                TW = np.vstack([f['TW'] for f in facs])
+                FW = np.zeros((Ks[j], Ks[j]))
+                a = 0
+                for f in facs:
+                    n = f['FB'].shape[1]
+                    FW[a:a + n, a:a + n] = f['FW']
+                    a += n
+            eng.set_spectral(j, FB, FW, TW, any(fb_free), any(tw_free),
+                             facs[0].get('FW_frdm_prior', 'fixed') == 'free')
+            eng.set_blocks(j, np.cumsum([0] + [f['FB'].shape[1] for f in facs]), fb_free, tw_free)
         return order, Ks, conv
 
     def _download(self, order, Ks, conv, updated_spatial=True):
@@ -237,21 +256,36 @@ class FASST(object):
                                                           sc['frdm_prior'] == 'free'):
                 p = p.real.copy()
             sc['params'] = p
-            fac = self.spec_comps[order[j]]['factor'][0]
             FB, FW, TW = eng.get_spectral(j, Ks[j])
-            for key, val in (('FB', FB), ('FW', FW), ('TW', TW)):
-                if isinstance(fac[key], np.ndarray) and fac[key].shape == val.shape \
-                        and fac[key].dtype == val.dtype:
-                    fac[key][...] = val
-                else:
-                    fac[key] = val
+            a = 0
+            for k in order[j]:
+                fac = self.spec_comps[k]['factor'][0]
+                n = fac['FB'].shape[1]
+                parts = (('FB', FB[:, a:a + n]), ('FW', FW[a:a + n, a:a + n]),
+                         ('TW', TW[a:a + n]))
+                if len(order[j]) > 1:
+                    parts = tuple((key, np.ascontiguousarray(val)) for key, val in parts)
+                for key, val in parts:
+                    if isinstance(fac[key], np.ndarray) and fac[key].shape == val.shape \
+                            and fac[key].dtype == val.dtype:
+                        fac[key][...] = val
+                    else:
+                        fac[key] = val
+                a += n
 
     def _restart_tw(self, mask, order):
         """Random TW restart of renormalize_parameters (audioModel.py:2023-2028),
-        drawn on the host RNG in spectral-component order."""
+        drawn on the host RNG in spectral-component key order; mask has one bit
+        per spectral component, spatial component by spatial component."""
+        dead = set()
+        bit = 0
+        for keys in order:
+            for k in keys:
+                if mask & (1 << bit):
+                    dead.add(k)
+                bit += 1
         for k in sorted(self.spec_comps.keys()):
-            j = self.spec_comps[k]['spat_comp_ind']
-            if mask & (1 << j):
+            if k in dead:
                 fac = self.spec_comps[k]['factor'][0]
                 fac['TW'] = np.random.randn(*fac['TW'].shape) ** 2
                 fac['TW'] *= 1e3 * eps
@@ -411,23 +445,41 @@ class FASST(object):
         return Y[src_spat][:, :, :t.datalen_init]
 
     def _separation_plan(self, spec_comp_ind):
-        """(spatial component of each output source, last annealed PSD)."""
+        """Set the engine's separation sources; return (output order, last
+        annealed PSD).  Source n holds the spectral components spec_comp_ind[n]
+        (default: one source per spectral component, audioModel.py:1130-1133):
+        Sigma_n sums, per spatial component, R_j times the power of those of
+        its components (compute_sigma_comp_2d, :1327-1372) and Sigma_x sums
+        the sources (compute_inv_sigma_mix_2d, :1374-1394).  Sources that are
+        whole spatial components, all of them, take the per-spatial-component
+        kernel (outputs reordered); others the source-table kernel."""
         if spec_comp_ind is None:
             spec_comp_ind = {}
             for spec_ind in range(len(self.spec_comps)):
                 spec_comp_ind[spec_ind] = [spec_ind, ]
         order, Ks, conv = self._upload()
-        src_spat = []
+        col = {}
+        for j, keys in enumerate(order):
+            a = 0
+            for k in keys:
+                n = self.spec_comps[k]['factor'][0]['FB'].shape[1]
+                col[k] = (j, a, n)
+                a += n
+        sources = []
         for n in range(len(spec_comp_ind)):
-            spats = np.unique([self.spec_comps[k]['spat_comp_ind'] for k in spec_comp_ind[n]])
-            if len(spats) != 1 or sorted(spec_comp_ind[n]) != [order[spats[0]]]:
-                raise NotImplementedError("sources must map one-to-one to spatial components "
-                                          "on the HIP path")
-            src_spat.append(int(spats[0]))
-        if len(set(src_spat)) != len(src_spat) or len(src_spat) != len(order):
-            raise NotImplementedError("sources must map one-to-one to spatial components")
+            terms = {}
+            for k in spec_comp_ind[n]:
+                j, a, w = col[k]
+                terms[j] = terms.get(j, 0) | (((1 << w) - 1) << a)
+            sources.append(sorted(terms.items()))
+        full = [(j, (1 << Ks[j]) - 1) for j in range(len(order))]
+        whole = all(len(t) == 1 and t[0] == full[t[0][0]] for t in sources)
         psd = np.asarray(self.noise['PSD'], dtype=np.float64) * np.ones(self.nbFreqsSigRepr)
-        return src_spat, psd
+        if whole and sorted(t[0][0] for t in sources) == list(range(len(order))):
+            self._engine.set_sources(None)
+            return [t[0][0] for t in sources], psd
+        self._engine.set_sources(sources)
+        return list(range(len(sources))), psd
 
     def separate_comps(self, dir_results=None, spec_comp_ind=None, suffix=None):
         """Wiener-filter and write one WAV per source (audioModel.py:1088-1236)."""

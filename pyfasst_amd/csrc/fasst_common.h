@@ -16,7 +16,11 @@ constexpr int kMaxR = 16;       // total spatial rank
 constexpr int kMaxKP = 64;      // padded NMF components
 constexpr int kFwFpc = 64;      // bins per block of the FW update's f-contraction
 constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge
-constexpr int kFlagHalt = 1 + kMaxJ, kFlagIter = 2 + kMaxJ, kNFlags = 3 + kMaxJ;
+// several spectral components per spatial component: source j's NMF columns
+// are cut into <= kMaxBlk blocks (one per spectral component); the blocks of
+// all sources (the "slots") carry the TW restart flags
+constexpr int kMaxBlk = 8, kMaxSlot = 16;
+constexpr int kFlagHalt = 1 + kMaxSlot, kFlagIter = 2 + kMaxSlot, kNFlags = 3 + kMaxSlot;
 #ifndef FASST_FPW
 #define FASST_FPW 2
 #endif

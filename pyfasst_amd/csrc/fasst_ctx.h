@@ -38,7 +38,20 @@ struct fasst_ctx {
   int rank[fasst::kMaxJ] = {0}, roff[fasst::kMaxJ + 1] = {0}, K[fasst::kMaxJ] = {0};
   int spat_free[fasst::kMaxJ] = {0}, fb_free[fasst::kMaxJ] = {0}, tw_free[fasst::kMaxJ] = {0};
   int fw_free[fasst::kMaxJ] = {0};
+  // spectral components of source j: column blocks [kb[j][b], kb[j][b + 1]) of
+  // its FB / FW (block diagonal) / TW, in the reference's spec_comps key
+  // order; slot soff[j] + b carries block b's TW restart flag.  multi != 0
+  // when some source has several blocks (the sequential multi-block update)
+  int nblk[fasst::kMaxJ] = {0}, kb[fasst::kMaxJ][fasst::kMaxBlk + 1] = {{0}};
+  int soff[fasst::kMaxJ + 1] = {0}, nslot = 0, maxblk = 0, multi = 0;
+  int bfb[fasst::kMaxJ][fasst::kMaxBlk] = {{0}}, btw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
   fasst::DBuf<double> FB, FW, TW, Wkf, Wkf_new, Wfk_new, FWHt, hatW;
+  fasst::DBuf<double> mplanes, bden;  // multi-block update: ratio planes [3][J][Tp][Fp], FB den
+  // separation sources (fasst_set_sources; nsrc == 0: one per spatial
+  // component): source n sums the terms [toff[n], toff[n + 1]), term i = the
+  // columns tmask[i] (bit k = column k) of spatial component tj[i]
+  int nsrc = 0, toff[fasst::kMaxSlot + 1] = {0}, tj[fasst::kMaxSlot] = {0};
+  unsigned long long tmask[fasst::kMaxSlot] = {0};
   fasst::DBuf<double2> A, Pinst;
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
@@ -47,7 +60,7 @@ struct fasst_ctx {
   fasst::DBuf<double> gden, TWt, pnum, pden;  // FW update (free FW)
   int nchunk_r = 1;
   fasst::DBuf<double2> rss, rxs;
-  fasst::DBuf<int> flags;        // [0] singular, [1..J] TW restart, [kFlagHalt] halt,
+  fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart
   int *h_flags = nullptr;        // pinned host mirror
   const int *halt = nullptr;     // flags + kFlagHalt while fasst_run enqueues a batch

@@ -810,6 +810,22 @@ __global__ void k_loglik(const double *__restrict__ llpart, int n, double *__res
   if (threadIdx.x == 0) out[0] = -(s[0] * inv_FT);
 }
 
+// sum_{c < n} p[c * stride] in index order (bit-identical to the plain loop)
+// with 8 loads in flight: the chunk reductions below were load-latency bound
+__device__ __forceinline__ double chunk_sum(const double *__restrict__ p, size_t stride, int n) {
+  double x = 0.0;
+  int c = 0;
+  for (; c + 8 <= n; c += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(c + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x += v[u];
+  }
+  for (; c < n; ++c) x += p[(size_t)c * stride];
+  return x;
+}
+
 // ---------------------------------------------------------------- mixing
 struct MArgs {
   const double *part;  // [nchunk][Fp][NACC]
@@ -865,7 +881,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   const int NP = J * (J + 1) / 2;
   for (int u = lane; u < NACC; u += 64) {  // NACC = 72 > 64 lanes for J = 4
     double x = 0.0;
-    for (int c = 0; c < a.nchunk; ++c) x += a.part[((size_t)c * a.Fp + f) * NACC + u];
+    x = chunk_sum(a.part + (size_t)f * NACC + u, (size_t)a.Fp * NACC, a.nchunk);
     s_acc[u] = x;
   }
   if (lane < 2 * R) s_A[lane >> 1][lane & 1] = a.A[(size_t)lane * a.Fp + f];
@@ -1072,7 +1088,9 @@ __global__ void k_mix_inst(const IArgs a) {
 // ---------------------------------------------------------------- FB update
 struct BArgs {
   const double *TW, *Wkf, *FWHt, *hatW;
+  const double *hatW2;  // DEN: the denominator ratio plane (multi-block update)
   double *bnum;  // [nchunk][J][Fp][KP]
+  double *bden;  // DEN: [nchunk][J][Fp][KP]
   int F, T, Fp, Tp, KP, J, ntt, nft, tpc;
   int fb_free[kMaxJ];
   const int *halt;
@@ -1087,19 +1105,27 @@ struct BArgs {
 // numerator is contracted here: a plain (F x T).(T x K) product whose rho
 // tiles arrive bins-on-lanes, i.e. already in the A-operand layout, and whose
 // (FW.H)^T B operand is shared by the FPW bin tiles.
-template <int NKC, int FPW>
+// DEN (several spectral components on source j, audioModel.py:1525-1571):
+// the numerator plane is (hat_W_j / V_j^2) other and a second plane
+// other / V_j is contracted into the denominator the same way.
+template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
   const int ft0 = blockIdx.x * FPW, j = blockIdx.y;
   if (!a.fb_free[j]) return;
-  d4 num[FPW][NKC];
+  d4 num[FPW][NKC], den[DEN ? FPW : 1][NKC];
 #pragma unroll
   for (int p = 0; p < FPW; ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) num[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int p = 0; p < (DEN ? FPW : 1); ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
   const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
+  const double *rdj = DEN ? a.hatW2 + (size_t)j * a.Tp * a.Fp : nullptr;
   for (int tt = tb; tt < te; ++tt) {
     const int t0 = tt * 16;
     double fb[4][NKC];
@@ -1120,6 +1146,16 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) num[p][kc] = mfma4(r1[i], fb[i][kc], num[p][kc]);
+      if constexpr (DEN) {
+        double r2[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          r2[i] = t0 + tq + 4 * i < a.T ? rdj[(size_t)(t0 + tq + 4 * i) * a.Fp + f] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kc = 0; kc < NKC; ++kc) den[p][kc] = mfma4(r2[i], fb[i][kc], den[p][kc]);
+      }
     }
   }
   const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Fp;
@@ -1129,22 +1165,27 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc)
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-        a.bnum[(base + (ft0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl] = num[p][kc][m];
+      for (int m = 0; m < 4; ++m) {
+        const size_t o = (base + (ft0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl;
+        a.bnum[o] = num[p][kc][m];
+        if constexpr (DEN) a.bden[o] = den[DEN ? p : 0][kc][m];
+      }
   }
 }
 
 struct UArgs {
   double *FB;
   const double *FW, *bnum, *hsum;
+  const double *bden;  // null: den = FW . rowsum(TW); else contracted per (f, k)
   double *Wkf_new, *Wfk_new;
   int F, Fp, KP, J, nchunk;
   double omega;
-  int K[kMaxJ], fb_free[kMaxJ];
+  int kb0[kMaxJ], kb1[kMaxJ], fb_free[kMaxJ];  // columns [kb0, kb1) are updated
   const int *halt;
 };
 // FB *= (num / max(den, eps))^omega with den = FW . rowsum(TW) (see
-// k_fb_contract), then W_new = FB . FW in both layouts.
+// k_fb_contract) or, for one of several spectral components, the contracted
+// denominator; then W_new = FB . FW in both layouts.
 __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   HALT_GUARD(a.halt);
   // LDS: FW [KP][KP] | FB rows [16][KP] | den [KP] | W_new rows [16][KP + 1]
@@ -1168,10 +1209,14 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
     const int fl = idx / KP, k = idx % KP, f = f0 + fl;
     const size_t o = ((size_t)j * a.Fp + f) * KP + k;
     double fb = a.FB[o];
-    if (a.fb_free[j] && f < a.F && k < a.K[j]) {
+    if (a.fb_free[j] && f < a.F && k >= a.kb0[j] && k < a.kb1[j]) {
       double num = 0.0;
-      for (int c = 0; c < a.nchunk; ++c) num += a.bnum[(((size_t)c * a.J + j) * a.Fp + f) * KP + k];
-      const double ratio = num / fmax(s_den[k], kEps);
+      num = chunk_sum(a.bnum + ((size_t)j * a.Fp + f) * KP + k, (size_t)a.J * a.Fp * KP, a.nchunk);
+      const double den =
+          a.bden ? chunk_sum(a.bden + ((size_t)j * a.Fp + f) * KP + k, (size_t)a.J * a.Fp * KP,
+                             a.nchunk)
+                 : s_den[k];
+      const double ratio = num / fmax(den, kEps);
       fb *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
       a.FB[o] = fb;
     }
@@ -1342,6 +1387,7 @@ struct TArgs {
   double *tnum, *tden;  // [nsplit][J][Tp][KP]
   int F, T, Fp, Tp, KP, J, nft, ntt, fpc;
   int tw_free[kMaxJ];
+  int kb0[kMaxJ], kb1[kMaxJ];  // BLK: the V tiles sum the columns [kb0, kb1) only
   const int *halt;
 };
 
@@ -1353,7 +1399,10 @@ struct TArgs {
 // rho * max(V_old, eps) from the E-step's rho; the W operands (A of the V
 // tiles, B of the contraction) are shared by the TPW frame tiles.  Partial
 // sums per bin chunk go to tnum / tden.
-template <int NKC, int TPW>
+// BLK (one of several spectral components on source j): V_old / V_new are the
+// component's own powers W_c H_c (the reference's spec_comp_ind=[k],
+// audioModel.py:1639-1645), and rho is the plane hat_W_j / max(V_c_old, eps).
+template <int NKC, int TPW, bool BLK = false>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
@@ -1385,6 +1434,10 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
     for (int s = 0; s < NKS; ++s) {
       ao[s] = wo[(size_t)(4 * s) * a.Fp + f0];
       an[s] = wn[(size_t)(4 * s) * a.Fp + f0];
+      if constexpr (BLK) {
+        const int k = tq + 4 * s;
+        if (k < a.kb0[j] || k >= a.kb1[j]) ao[s] = an[s] = 0.0;
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1449,7 +1502,7 @@ struct TUArgs {
   const double *tnum, *tden;
   int T, Tp, KP, J, nsplit;
   double omega;
-  int K[kMaxJ], tw_free[kMaxJ];
+  int kb0[kMaxJ], kb1[kMaxJ], tw_free[kMaxJ];  // rows [kb0, kb1) are updated
   const int *halt;
 };
 // TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
@@ -1480,9 +1533,84 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
     __syncthreads();
     for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
       const int kl = idx / 64, tl = idx % 64, t = t0 + tl, k = kb + kl;
-      if (t < a.T && k < a.K[j]) a.TW[((size_t)j * a.KP + k) * a.Tp + t] *= s_r[kl][tl];
+      if (t < a.T && k >= a.kb0[j] && k < a.kb1[j])
+        a.TW[((size_t)j * a.KP + k) * a.Tp + t] *= s_r[kl][tl];
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------- several spectral components
+// update_spectral_components (audioModel.py:1479-1727) when source j holds
+// several spectral components: they are updated one after the other in the
+// reference's key order (block b of every source at step b), each seeing the
+// components updated before it.  For block c of source j, with
+// V_j = sum of all its components' powers (current parameters), V_c the
+// block's own power and hat_W_j the E-step's posterior power:
+//   FB: num = ((hat_W_j / max(V_j)^2) max(V_c)) (FW H)^T, den = (max(V_c) /
+//       max(V_j)) (FW H)^T (:1513-1575, other = max(V_c): N1)
+//   TW: k_tw_contract<BLK> with V_old / V_new of the block and the plane
+//       rho_c = hat_W_j / max(V_c_old) (:1634-1727, spec_comp_ind=[k])
+// k_multi_prep forms the three planes (rnum, rden, rho_c) of step b from the
+// current W (Wkf, all blocks) and TW; at step 0 it also turns the E-step's
+// rho_j = hat_W_j / max(V_j) back into hat_W_j in place (the later steps need
+// hat_W_j itself, V_j having moved).
+struct MPArgs {
+  const double *TW, *Wkf;
+  double *hatW, *rnum, *rden, *rtw;   // planes [J][Tp][Fp]
+  int F, T, Fp, Tp, KP, J, ntt, tpc, first;
+  int on[kMaxJ], kb0[kMaxJ], kb1[kMaxJ];
+  const int *halt;
+};
+
+template <int NKC>
+__global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
+  HALT_GUARD(a.halt);
+  constexpr int NKS = 4 * NKC;
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int j = blockIdx.y;
+  if (!a.on[j]) return;
+  const int f0 = blockIdx.x * 16, f = f0 + fl;
+  double wj[NKS], wc[NKS];   // B operands of the V tiles: W[k = tq + 4 s][f]
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const int k = tq + 4 * s;
+    const double w = a.Wkf[((size_t)j * a.KP + k) * a.Fp + f];
+    wj[s] = w;
+    wc[s] = k >= a.kb0[j] && k < a.kb1[j] ? w : 0.0;
+  }
+  const size_t pj = (size_t)j * a.Tp * a.Fp;
+  const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
+  for (int tt = tb; tt < te; ++tt) {
+    const int t0 = tt * 16;
+    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+    d4 vj = d4{0.0, 0.0, 0.0, 0.0}, vc = vj;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const double h = tw[(size_t)(4 * s) * a.Tp];
+      vj = mfma4(h, wj[s], vj);
+      vc = mfma4(h, wc[s], vc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = t0 + tq + 4 * i;
+      const size_t o = pj + (size_t)t * a.Fp + f;
+      if (t >= a.T || f >= a.F) {
+        a.rnum[o] = a.rden[o] = a.rtw[o] = 0.0;
+        continue;
+      }
+      const double sj = fmax(vj[i], kEps), sc = fmax(vc[i], kEps);
+      double hw;
+      if (a.first) {
+        hw = a.hatW[o] * sj;   // rho_j max(V_j) (the E-step stored rho_j)
+        a.hatW[o] = hw;
+      } else {
+        hw = a.hatW[o];
+      }
+      a.rnum[o] = (hw / (sj * sj)) * sc;
+      a.rden[o] = sc * (1.0 / sj);
+      a.rtw[o] = hw / sc;
+    }
   }
 }
 
@@ -1493,10 +1621,13 @@ struct RArgs {
   double *scal;   // [J][2 + 2*KP]: e_j, -, w_j[KP], w2_j[KP] (stage 2 -> 3)
   double *pmax;   // [J][nchunk][KP] column maxima of FB per bin chunk
   double *pe;     // [J][nchunk] partial mixing-filter energy (conv)
-  double *tpart;  // [J][nchunk] partial sums of the rescaled TW
+  double *tpart;  // [nslot][nchunk] partial sums of the rescaled TW, per block
   int *flags;
-  int F, T, Fp, Tp, KP, conv, nchunk, tpc, fpc;
+  int F, T, Fp, Tp, KP, conv, nchunk, tpc, fpc, nslot;
   int K[kMaxJ], roff[kMaxJ + 1];
+  // spectral components of source j (column blocks of FB / FW / TW) and the
+  // slot of block 0
+  int nblk[kMaxJ], kb[kMaxJ][kMaxBlk + 1], soff[kMaxJ + 1];
   const int *halt;
 };
 
@@ -1585,11 +1716,15 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   }
   __syncthreads();
   if (threadIdx.x < K) {
+    // FW.mean(axis=0) of the column's own spectral component (block)
     const int cc = threadIdx.x;
+    int b = 0;
+    while (b + 1 < a.nblk[j] && cc >= a.kb[j][b + 1]) ++b;
+    const int r0b = a.kb[j][b], r1b = a.kb[j][b + 1];
     const double *FW = a.FW + (size_t)j * KP * KP;
     double s = 0.0;
-    for (int r = 0; r < K; ++r) s += FW[r * KP + cc] * s_w[r];
-    s /= (double)K;
+    for (int r = r0b; r < r1b; ++r) s += FW[r * KP + cc] * s_w[r];
+    s /= (double)(r1b - r0b);
     s_w2[cc] = s == 0.0 ? 1.0 : s;
   }
   __syncthreads();
@@ -1635,27 +1770,30 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   double *TW = a.TW + (size_t)j * KP * a.Tp;
   const int t0 = c * a.tpc, t1 = min(t0 + a.tpc, a.T);
   const int w = t1 - t0;
-  double tsum = 0.0;
-  if (w > 0)
-    for (int base = threadIdx.x; base < K * w; base += kRnB * blockDim.x) {
-      double x[kRnB];
+  for (int b = 0; b < a.nblk[j]; ++b) {   // one restart sum per spectral component
+    const int rb = a.kb[j][b], nrow = a.kb[j][b + 1] - rb;
+    double tsum = 0.0;
+    if (w > 0)
+      for (int base = threadIdx.x; base < nrow * w; base += kRnB * blockDim.x) {
+        double x[kRnB];
 #pragma unroll
-      for (int u = 0; u < kRnB; ++u) {
-        const int idx = base + u * blockDim.x;
-        x[u] = idx < K * w ? TW[(size_t)(idx / w) * a.Tp + t0 + idx % w] : 0.0;
-      }
+        for (int u = 0; u < kRnB; ++u) {
+          const int idx = base + u * blockDim.x;
+          x[u] = idx < nrow * w ? TW[(size_t)(rb + idx / w) * a.Tp + t0 + idx % w] : 0.0;
+        }
 #pragma unroll
-      for (int u = 0; u < kRnB; ++u) {
-        const int idx = base + u * blockDim.x;
-        if (idx < K * w) {
-          const double y = x[u] * s_w2[idx / w];
-          TW[(size_t)(idx / w) * a.Tp + t0 + idx % w] = y;
-          tsum += y;
+        for (int u = 0; u < kRnB; ++u) {
+          const int idx = base + u * blockDim.x;
+          if (idx < nrow * w) {
+            const double y = x[u] * s_w2[rb + idx / w];
+            TW[(size_t)(rb + idx / w) * a.Tp + t0 + idx % w] = y;
+            tsum += y;
+          }
         }
       }
-    }
-  tsum = block_sum(tsum, s_red);
-  if (threadIdx.x == 0) a.tpart[(size_t)j * a.nchunk + c] = tsum;
+    tsum = block_sum(tsum, s_red);
+    if (threadIdx.x == 0) a.tpart[(size_t)(a.soff[j] + b) * a.nchunk + c] = tsum;
+  }
 }
 
 // Stage 3 (one block): FW = FW w / w2, 'inst' parameters / sqrt(e), and the
@@ -1678,12 +1816,12 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
     }
   }
   __syncthreads();
-  const int j = threadIdx.x;
-  if (j >= J) return;
+  const int sl = threadIdx.x;   // one TW restart test per spectral component
+  if (sl >= a.nslot) return;
   double s = 0.0;
-  for (int c = 0; c < a.nchunk; ++c) s += a.tpart[(size_t)j * a.nchunk + c];
+  for (int c = 0; c < a.nchunk; ++c) s += a.tpart[(size_t)sl * a.nchunk + c];
   const int dead = s < kEps ? 1 : 0;
-  a.flags[1 + j] = dead;
+  a.flags[1 + sl] = dead;
   if (dead) {
     a.flags[kFlagHalt] = 1;
     a.flags[kFlagIter] = iter;
@@ -1779,7 +1917,16 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
     c->roff[j + 1] = c->roff[j] + rank[j];
     c->spat_free[j] = c->fb_free[j] = c->tw_free[j] = 1;
     c->fw_free[j] = 0;
+    c->nblk[j] = 1;   // one spectral component per source until fasst_set_blocks
+    c->kb[j][0] = 0;
+    c->kb[j][1] = K[j];
+    c->bfb[j][0] = c->btw[j][0] = 1;
+    c->soff[j] = j;
   }
+  c->soff[J] = c->nslot = J;
+  c->maxblk = 1;
+  c->multi = 0;
+  c->nsrc = 0;
   const int Fp = c->Fp, Tp = c->Tp, KP = c->KP;
   // Launch shapes sized to whole rounds of resident blocks (a partial last
   // round idles most of the chip): E-step blocks = f tiles x frame chunks,
@@ -1850,7 +1997,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(rscal, (size_t)J * (2 + 2 * KP));
   ALLOC(rpmax, (size_t)J * c->nchunk_r * KP);
   ALLOC(rpe, (size_t)J * c->nchunk_r);
-  ALLOC(rtpart, (size_t)J * c->nchunk_r);
+  ALLOC(rtpart, (size_t)kMaxSlot * c->nchunk_r);
 #undef ALLOC
   c->configured = 1;
   return FASST_OK;
@@ -1897,8 +2044,16 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   r.nchunk = c->nchunk_r;
   r.tpc = (c->T + c->nchunk_r - 1) / c->nchunk_r;
   r.fpc = (c->F + c->nchunk_r - 1) / c->nchunk_r;
-  for (int j = 0; j < kMaxJ; ++j) r.K[j] = j < c->J ? c->K[j] : 0;
-  for (int j = 0; j <= kMaxJ; ++j) r.roff[j] = j <= c->J ? c->roff[j] : c->R;
+  r.nslot = c->nslot;
+  for (int j = 0; j < kMaxJ; ++j) {
+    r.K[j] = j < c->J ? c->K[j] : 0;
+    r.nblk[j] = j < c->J ? c->nblk[j] : 0;
+    for (int b = 0; b <= kMaxBlk; ++b) r.kb[j][b] = j < c->J ? c->kb[j][b] : 0;
+  }
+  for (int j = 0; j <= kMaxJ; ++j) {
+    r.roff[j] = j <= c->J ? c->roff[j] : c->R;
+    r.soff[j] = j <= c->J ? c->soff[j] : c->nslot;
+  }
   prof_begin(c, KREN);
   k_renorm_stats<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
   k_renorm_apply<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
@@ -2057,6 +2212,139 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
   return e == hipSuccess ? std::max(1, n) : 1;
 }
 
+// Spectral update of a model with several spectral components on some source
+// (see k_multi_prep): step b updates block b of every source that has one
+// (FB, then TW), all launches on c->stream; W = FB FW of the step's result
+// becomes the next step's current W.
+static int multi_spectral(fasst_ctx *c, double omega) {
+  const int J = c->J, nkc = c->KP / 16;
+  const size_t plane = (size_t)J * c->Tp * c->Fp;
+  for (int b = 0; b < c->maxblk; ++b) {
+    MPArgs mp;
+    mp.TW = c->TW.p;
+    mp.Wkf = c->Wkf.p;
+    mp.hatW = c->hatW.p;
+    mp.rnum = c->mplanes.p;
+    mp.rden = c->mplanes.p + plane;
+    mp.rtw = c->mplanes.p + 2 * plane;
+    mp.F = c->F;
+    mp.T = c->T;
+    mp.Fp = c->Fp;
+    mp.Tp = c->Tp;
+    mp.KP = c->KP;
+    mp.J = J;
+    mp.ntt = c->ntt;
+    mp.tpc = c->tpc_b;
+    mp.first = b == 0;
+    mp.halt = c->halt;
+    BArgs bb;
+    bb.TW = c->TW.p;
+    bb.Wkf = c->Wkf.p;
+    bb.FWHt = c->FWHt.p;
+    bb.hatW = mp.rnum;
+    bb.hatW2 = mp.rden;
+    bb.bnum = c->bnum.p;
+    bb.bden = c->bden.p;
+    bb.halt = c->halt;
+    bb.F = c->F;
+    bb.T = c->T;
+    bb.Fp = c->Fp;
+    bb.Tp = c->Tp;
+    bb.KP = c->KP;
+    bb.J = J;
+    bb.ntt = c->ntt;
+    bb.nft = c->nft;
+    bb.tpc = c->tpc_b;
+    UArgs u;
+    u.FB = c->FB.p;
+    u.FW = c->FW.p;
+    u.bnum = c->bnum.p;
+    u.bden = c->bden.p;
+    u.hsum = c->hsum.p;
+    u.Wkf_new = c->Wkf_new.p;
+    u.Wfk_new = c->Wfk_new.p;
+    u.halt = c->halt;
+    u.F = c->F;
+    u.Fp = c->Fp;
+    u.KP = c->KP;
+    u.J = J;
+    u.nchunk = c->nchunk_b;
+    u.omega = omega;
+    TArgs t;
+    t.TW = c->TW.p;
+    t.Wkf_old = c->Wkf.p;
+    t.Wkf_new = c->Wkf_new.p;
+    t.Wfk_new = c->Wfk_new.p;
+    t.hatW = mp.rtw;
+    t.tnum = c->tnum.p;
+    t.tden = c->tden.p;
+    t.halt = c->halt;
+    t.F = c->F;
+    t.T = c->T;
+    t.Fp = c->Fp;
+    t.Tp = c->Tp;
+    t.KP = c->KP;
+    t.J = J;
+    t.nft = c->nft;
+    t.ntt = c->ntt;
+    t.fpc = c->fpc_t;
+    TUArgs tu;
+    tu.TW = c->TW.p;
+    tu.tnum = c->tnum.p;
+    tu.tden = c->tden.p;
+    tu.halt = c->halt;
+    tu.T = c->T;
+    tu.Tp = c->Tp;
+    tu.KP = c->KP;
+    tu.J = J;
+    tu.nsplit = c->nsplit_t;
+    tu.omega = omega;
+    for (int j = 0; j < kMaxJ; ++j) {
+      const bool has = j < J && b < c->nblk[j];
+      mp.on[j] = has;
+      const int k0 = has ? c->kb[j][b] : 0, k1 = has ? c->kb[j][b + 1] : 0;
+      mp.kb0[j] = u.kb0[j] = t.kb0[j] = tu.kb0[j] = k0;
+      mp.kb1[j] = u.kb1[j] = t.kb1[j] = tu.kb1[j] = k1;
+      bb.fb_free[j] = u.fb_free[j] = has && c->bfb[j][b];
+      t.tw_free[j] = tu.tw_free[j] = has && c->btw[j][b];
+    }
+    const dim3 gp(c->nft, J, c->nchunk_b);
+    const dim3 gb((c->nft + kFPW - 1) / kFPW, J, c->nchunk_b);
+    const dim3 gt((c->ntt + kTPW - 1) / kTPW, J, c->nsplit_t);
+    switch (nkc) {
+      case 1:
+        k_multi_prep<1><<<gp, 64, 0, c->stream>>>(mp);
+        k_fb_contract<1, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
+        break;
+      case 2:
+        k_multi_prep<2><<<gp, 64, 0, c->stream>>>(mp);
+        k_fb_contract<2, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
+        break;
+      default:
+        k_multi_prep<4><<<gp, 64, 0, c->stream>>>(mp);
+        k_fb_contract<4, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
+        break;
+    }
+    FASST_LAUNCH_CHECK();
+    k_fb_update<<<dim3(c->nft, J), 256,
+                  (size_t)(c->KP * c->KP + 16 * c->KP + c->KP + 16 * (c->KP + 1)) * sizeof(double),
+                  c->stream>>>(u);
+    FASST_LAUNCH_CHECK();
+    switch (nkc) {
+      case 1: k_tw_contract<1, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
+      case 2: k_tw_contract<2, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
+      default: k_tw_contract<4, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
+    }
+    FASST_LAUNCH_CHECK();
+    k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
+    FASST_LAUNCH_CHECK();
+    // the step's W = FB FW is the current W of the next step
+    FASST_HIP(hipMemcpyAsync(c->Wkf.p, c->Wkf_new.p, (size_t)J * c->KP * c->Fp * sizeof(double),
+                             hipMemcpyDeviceToDevice, c->stream));
+  }
+  return FASST_OK;
+}
+
 // One GEM iteration, all launches asynchronous on c->stream.
 static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
                          int iter) {
@@ -2174,6 +2462,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     }
   }
   (void)all_free;
+  if (c->multi) {
+    int st2 = multi_spectral(c, omega);
+    if (st2) return st2;
+    return launch_renorm(c, iter);
+  }
   // spectral update: FB then TW (one NMF factor per source)
   BArgs b;
   b.TW = c->TW.p;
@@ -2234,9 +2527,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   u.J = J;
   u.nchunk = c->nchunk_b;
   u.omega = omega;
+  u.bden = nullptr;
   for (int j = 0; j < kMaxJ; ++j) {
     const bool in = j < J;
-    tu.K[j] = u.K[j] = in ? c->K[j] : 0;
+    tu.kb0[j] = u.kb0[j] = t.kb0[j] = 0;
+    tu.kb1[j] = u.kb1[j] = t.kb1[j] = in ? c->K[j] : 0;
     t.tw_free[j] = tu.tw_free[j] = in ? c->tw_free[j] : 0;
     b.fb_free[j] = u.fb_free[j] = in ? c->fb_free[j] : 0;
   }
@@ -2411,6 +2706,8 @@ int fasst_destroy(fasst_ctx *c) {
     c->rpmax.release();
     c->rpe.release();
     c->rtpart.release();
+    c->mplanes.release();
+    c->bden.release();
     for (int i = 0; i < fasst_ctx::kNK; ++i) {
       if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
       if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
@@ -2486,7 +2783,61 @@ int fasst_get_spatial(fasst_ctx *c, int j, double *params) {
 int fasst_set_fw_prior(fasst_ctx *c, int j, int fw_free) {
   int st = need_model(c, j);
   if (st) return st;
+
   c->fw_free[j] = fw_free ? 1 : 0;
+  return FASST_OK;
+}
+
+int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb_free,
+                     const int *tw_free) {
+  int st = need_model(c, j);
+  if (st) return st;
+  if (nblk < 1 || nblk > kMaxBlk || !kb || !fb_free || !tw_free) {
+    set_error("source %d: %d spectral components (1..%d on the HIP path)", j, nblk, kMaxBlk);
+    return nblk > kMaxBlk ? FASST_ERR_UNSUPPORTED : FASST_ERR_SHAPE;
+  }
+  if (kb[0] != 0 || kb[nblk] != c->K[j]) {
+    set_error("source %d: component blocks must cover its %d columns", j, c->K[j]);
+    return FASST_ERR_SHAPE;
+  }
+  for (int b = 0; b < nblk; ++b)
+    if (kb[b + 1] <= kb[b]) {
+      set_error("source %d: empty or unordered component block %d", j, b);
+      return FASST_ERR_SHAPE;
+    }
+  int nslot = 0, maxblk = 0;
+  for (int i = 0; i < c->J; ++i) {
+    const int n = i == j ? nblk : c->nblk[i];
+    nslot += n;
+    maxblk = std::max(maxblk, n);
+  }
+  if (nslot > kMaxSlot) {
+    set_error("%d spectral components in all (max %d on the HIP path)", nslot, kMaxSlot);
+    return FASST_ERR_UNSUPPORTED;
+  }
+  DeviceGuard g(c->device);
+  if (maxblk > 1) {
+    const size_t plane = (size_t)c->J * c->Tp * c->Fp;
+    if (c->mplanes.n < 3 * plane && (st = c->mplanes.alloc(3 * plane))) return st;
+    const size_t nb = (size_t)c->nchunk_b * c->J * c->Fp * c->KP;
+    if (c->bden.n < nb && (st = c->bden.alloc(nb))) return st;
+  }
+  c->nblk[j] = nblk;
+  for (int b = 0; b <= nblk; ++b) c->kb[j][b] = kb[b];
+  bool fbf = false, twf = false;
+  for (int b = 0; b < nblk; ++b) {
+    c->bfb[j][b] = fb_free[b] ? 1 : 0;
+    c->btw[j][b] = tw_free[b] ? 1 : 0;
+    fbf |= c->bfb[j][b] != 0;
+    twf |= c->btw[j][b] != 0;
+  }
+  c->fb_free[j] = fbf;
+  c->tw_free[j] = twf;
+  c->soff[0] = 0;
+  for (int i = 0; i < c->J; ++i) c->soff[i + 1] = c->soff[i] + c->nblk[i];
+  c->nslot = nslot;
+  c->maxblk = maxblk;
+  c->multi = maxblk > 1;
   return FASST_OK;
 }
 
@@ -2498,6 +2849,10 @@ int fasst_set_spectral(fasst_ctx *c, int j, const double *FB, const double *FW, 
   const int K = c->K[j], KP = c->KP;
   c->fb_free[j] = fb_free ? 1 : 0;
   c->tw_free[j] = tw_free ? 1 : 0;
+  if (c->nblk[j] == 1) {
+    c->bfb[j][0] = c->fb_free[j];
+    c->btw[j][0] = c->tw_free[j];
+  }
   FASST_HIP(hipMemsetAsync(c->FW.p + (size_t)j * KP * KP, 0, (size_t)KP * KP * sizeof(double),
                            c->stream));
   FASST_HIP(hipMemcpy2DAsync(c->FB.p + (size_t)j * c->Fp * KP, KP * sizeof(double), FB,
@@ -2546,8 +2901,8 @@ int fasst_renormalize(fasst_ctx *c, int *restart_mask) {
                            hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));
   int mask = 0;
-  for (int j = 0; j < c->J; ++j)
-    if (c->h_flags[1 + j]) mask |= 1 << j;
+  for (int sl = 0; sl < c->nslot; ++sl)
+    if (c->h_flags[1 + sl]) mask |= 1 << sl;
   if (restart_mask) *restart_mask = mask;
   return FASST_OK;
 }
@@ -2557,6 +2912,13 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   int st = need_model(c, 0);
   if (st) return st;
   if (n_iter < 0 || (n_iter > 0 && (!psd || !logliks))) return FASST_ERR_SHAPE;
+  if (c->multi)
+    for (int j = 0; j < c->J; ++j)
+      if (c->fw_free[j]) {
+        set_error("free FW with several spectral components per spatial component is outside "
+                  "the HIP path");
+        return FASST_ERR_UNSUPPORTED;
+      }
   DeviceGuard g(c->device);
   if (iters_done) *iters_done = 0;
   if (restart_mask) *restart_mask = 0;
@@ -2600,8 +2962,8 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
     return FASST_ERR_SINGULAR;
   }
   int mask = 0;
-  for (int j = 0; j < c->J; ++j)
-    if (c->h_flags[1 + j]) mask |= 1 << j;
+  for (int sl = 0; sl < c->nslot; ++sl)
+    if (c->h_flags[1 + sl]) mask |= 1 << sl;
   if (mask) done = c->h_flags[kFlagIter] + 1;
   if (iters_done) *iters_done = done;
   FASST_HIP(hipMemcpy(logliks, c->ll.p, (size_t)done * sizeof(double), hipMemcpyDeviceToHost));

@@ -352,6 +352,99 @@ __global__ __launch_bounds__(64) void k_wiener(const WArgs a) {
   }
 }
 
+
+// Sources made of spectral components (separate_comps with spec_comp_ind,
+// audioModel.py:1130-1164): Sigma_n = sum over the terms of n of R_j V_{j,C}
+// with V_{j,C} = W_j[:, C] H_j[C, :] (compute_sigma_comp_2d on the
+// components C of n in spatial component j), Sigma_x = sum_n Sigma_n + psd
+// (compute_inv_sigma_mix_2d).  Two passes per tile: Sigma_x from every term,
+// then each source's Wiener gain and images (its V tiles re-formed).
+struct WSArgs {
+  const double *TW, *Wkf, *coef, *psd;
+  const double2 *X;
+  double2 *S;   // [nsrc][2][Tp][Fp]
+  int F, T, Fp, Tp, KP, nsrc;
+  int toff[kMaxSlot + 1], tj[kMaxSlot];
+  unsigned long long tmask[kMaxSlot];
+};
+
+__device__ __forceinline__ d4 ws_term_v(const WSArgs &a, int i, int t0, int f, int tq, int fl) {
+  const int j = a.tj[i];
+  const unsigned long long m = a.tmask[i];
+  const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+  const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
+  d4 v = d4{0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < (a.KP >> 2); ++s) {
+    const int k = tq + 4 * s;
+    const double w = (m >> k) & 1ull ? wk[(size_t)(4 * s) * a.Fp] : 0.0;
+    v = mfma4b(tw[(size_t)(4 * s) * a.Tp], w, v);
+  }
+  return v;
+}
+
+// Sigma_n of source n at this tile (its terms summed in order)
+__device__ __forceinline__ void ws_source(const WSArgs &a, int n, int t0, int f, int tq, int fl,
+                                          d4 &s0, d4 &s1, d4 &sr, d4 &si) {
+  s0 = s1 = sr = si = d4{0.0, 0.0, 0.0, 0.0};
+  for (int i = a.toff[n]; i < a.toff[n + 1]; ++i) {
+    const d4 v = ws_term_v(a, i, t0, f, tq, fl);
+    const int j = a.tj[i];
+    s0 += a.coef[(size_t)(j * 4 + 0) * a.Fp + f] * v;
+    s1 += a.coef[(size_t)(j * 4 + 1) * a.Fp + f] * v;
+    sr += a.coef[(size_t)(j * 4 + 2) * a.Fp + f] * v;
+    si += a.coef[(size_t)(j * 4 + 3) * a.Fp + f] * v;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_wiener_src(const WSArgs a) {
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int t0 = blockIdx.x * 16, f0 = blockIdx.y * 16, f = f0 + fl;
+  d4 d0 = d4{0.0, 0.0, 0.0, 0.0}, d1 = d0, orr = d0, oi = d0;
+  for (int n = 0; n < a.nsrc; ++n) {
+    d4 s0, s1, sr, si;
+    ws_source(a, n, t0, f, tq, fl, s0, s1, sr, si);
+    d0 += s0;
+    d1 += s1;
+    orr += sr;
+    oi += si;
+  }
+  const double psd = a.psd[f];
+  d4 i0, i1, ior, ioi;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double e0 = d0[q] + psd, e1 = d1[q] + psd;
+    double det = e0 * e1 - (orr[q] * orr[q] + oi[q] * oi[q]);
+    const double dg = det + kEps;
+    det = (dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0)) * fmax(fabs(det), kEps);
+    i0[q] = e1 / det;
+    i1[q] = e0 / det;
+    ior[q] = -orr[q] / det;
+    ioi[q] = -oi[q] / det;
+  }
+  const size_t plane = (size_t)a.Tp * a.Fp;
+  for (int n = 0; n < a.nsrc; ++n) {
+    d4 s0, s1, sr, si;
+    ws_source(a, n, t0, f, tq, fl, s0, s1, sr, si);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const size_t o = (size_t)(t0 + tq + 4 * q) * a.Fp + f;
+      // WG = Sigma_n Sigma_x^-1 (compute_Wiener_gain_2d, audioModel.py:1453-1465)
+      const double pr = sr[q] * ior[q] + si[q] * ioi[q], pi = si[q] * ior[q] - sr[q] * ioi[q];
+      const double w00r = pr + s0[q] * i0[q], w00i = pi;
+      const double w11r = pr + s1[q] * i1[q], w11i = -pi;
+      const double w01r = s0[q] * ior[q] + sr[q] * i1[q], w01i = s0[q] * ioi[q] + si[q] * i1[q];
+      const double w10r = sr[q] * i0[q] + s1[q] * ior[q], w10i = -si[q] * i0[q] - s1[q] * ioi[q];
+      const double2 x0 = a.X[o], x1 = a.X[plane + o];
+      a.S[((size_t)n * 2 + 0) * plane + o] =
+          make_double2(w00r * x0.x - w00i * x0.y + (w01r * x1.x - w01i * x1.y),
+                       w00r * x0.y + w00i * x0.x + (w01r * x1.y + w01i * x1.x));
+      a.S[((size_t)n * 2 + 1) * plane + o] =
+          make_double2(w10r * x0.x - w10i * x0.y + (w11r * x1.x - w11i * x1.y),
+                       w10r * x0.y + w10i * x0.x + (w11r * x1.y + w11i * x1.x));
+    }
+  }
+}
+
 __global__ void k_inv_herm(int n, const double *__restrict__ d, const double2 *__restrict__ off,
                            double *__restrict__ id, double2 *__restrict__ ioff,
                            double *__restrict__ det_out) {
@@ -366,6 +459,60 @@ __global__ void k_inv_herm(int n, const double *__restrict__ d, const double2 *_
     id[n + i] = d0 / det;
     det_out[i] = det;
   }
+}
+
+
+// Wiener images of the separation sources into dS [nsrc][2][Tp][Fp] (nsrc =
+// J when no source table is set)
+static int launch_wiener(fasst_ctx *c, const double *coef, const double *dpsd, double2 *dS) {
+  const dim3 grid(c->ntt, c->nft);
+  if (c->nsrc > 0) {
+    WSArgs w;
+    w.TW = c->TW.p;
+    w.Wkf = c->Wkf.p;
+    w.coef = coef;
+    w.psd = dpsd;
+    w.X = c->X.p;
+    w.S = dS;
+    w.F = c->F;
+    w.T = c->T;
+    w.Fp = c->Fp;
+    w.Tp = c->Tp;
+    w.KP = c->KP;
+    w.nsrc = c->nsrc;
+    for (int i = 0; i <= kMaxSlot; ++i) w.toff[i] = i <= c->nsrc ? c->toff[i] : c->toff[c->nsrc];
+    for (int i = 0; i < kMaxSlot; ++i) {
+      w.tj[i] = c->tj[i];
+      w.tmask[i] = c->tmask[i];
+    }
+    k_wiener_src<<<grid, 64, 0, c->stream>>>(w);
+    FASST_LAUNCH_CHECK();
+    return FASST_OK;
+  }
+  WArgs w;
+  w.TW = c->TW.p;
+  w.Wkf = c->Wkf.p;
+  w.coef = coef;
+  w.psd = dpsd;
+  w.X = c->X.p;
+  w.S = dS;
+  w.F = c->F;
+  w.T = c->T;
+  w.Fp = c->Fp;
+  w.Tp = c->Tp;
+  w.KP = c->KP;
+  switch (c->J) {
+    case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
+    case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
+    case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
+    case 4: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
+    case 5: k_wiener<5><<<grid, 64, 0, c->stream>>>(w); break;
+    case 6: k_wiener<6><<<grid, 64, 0, c->stream>>>(w); break;
+    case 7: k_wiener<7><<<grid, 64, 0, c->stream>>>(w); break;
+    default: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
+  }
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
 }
 
 static int check_fft(int nfft, int wlen, int hop) {
@@ -637,6 +784,43 @@ int fasst_set_stft(fasst_ctx *c, const double *X) {
   return FASST_OK;
 }
 
+int fasst_set_sources(fasst_ctx *c, int nsrc, const int *term_off, const int *term_j,
+                      const unsigned long long *term_mask) {
+  if (!c || !c->configured) {
+    set_error("fasst_set_sources: context not configured");
+    return FASST_ERR_SHAPE;
+  }
+  if (nsrc == 0) {
+    c->nsrc = 0;
+    return FASST_OK;
+  }
+  if (nsrc < 0 || nsrc > kMaxSlot || !term_off || !term_j || !term_mask || term_off[0] != 0 ||
+      term_off[nsrc] > kMaxSlot) {
+    set_error("fasst_set_sources: %d sources (max %d terms in all)", nsrc, kMaxSlot);
+    return nsrc > kMaxSlot ? FASST_ERR_UNSUPPORTED : FASST_ERR_SHAPE;
+  }
+  for (int n = 0; n < nsrc; ++n)
+    if (term_off[n + 1] <= term_off[n]) {
+      set_error("fasst_set_sources: source %d has no component", n);
+      return FASST_ERR_SHAPE;
+    }
+  for (int i = 0; i < term_off[nsrc]; ++i) {
+    const int j = term_j[i];
+    if (j < 0 || j >= c->J || !term_mask[i] ||
+        (c->K[j] < 64 && (term_mask[i] >> c->K[j]) != 0ull)) {
+      set_error("fasst_set_sources: bad term %d (spatial component %d)", i, j);
+      return FASST_ERR_SHAPE;
+    }
+  }
+  c->nsrc = nsrc;
+  for (int n = 0; n <= nsrc; ++n) c->toff[n] = term_off[n];
+  for (int i = 0; i < term_off[nsrc]; ++i) {
+    c->tj[i] = term_j[i];
+    c->tmask[i] = term_mask[i];
+  }
+  return FASST_OK;
+}
+
 int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double *S) {
   if (!c || !c->configured || !psd || !S) {
     set_error("fasst_wiener_images: context not configured");
@@ -649,14 +833,14 @@ int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double
     set_error("fasst_wiener_images: no STFT available (set_audio / set_stft / X argument)");
     return FASST_ERR_SHAPE;
   }
-  const int J = c->J;
+  const int J = c->J, NS = c->nsrc > 0 ? c->nsrc : J;
   DBuf<double> dpsd, coef;
   DBuf<int> droff;
   DBuf<double2> dS, hS;
   const size_t plane = (size_t)c->Tp * c->Fp;
   if ((st = dpsd.alloc(c->Fp)) || (st = coef.alloc((size_t)J * 4 * c->Fp)) ||
-      (st = droff.alloc(kMaxJ + 1)) || (st = dS.alloc((size_t)J * 2 * plane)) ||
-      (st = hS.alloc((size_t)J * 2 * c->F * c->T)))
+      (st = droff.alloc(kMaxJ + 1)) || (st = dS.alloc((size_t)NS * 2 * plane)) ||
+      (st = hS.alloc((size_t)NS * 2 * c->F * c->T)))
     return st;
   FASST_HIP(hipMemcpyAsync(dpsd.p, psd, c->F * sizeof(double), hipMemcpyHostToDevice, c->stream));
   FASST_HIP(hipMemcpyAsync(droff.p, c->roff, (J + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
@@ -665,31 +849,8 @@ int fasst_wiener_images(fasst_ctx *c, const double *psd, const double *X, double
   if ((st = launch_w_old(c))) return st;
   k_mixcoef<<<(c->Fp + 255) / 256, 256, 0, c->stream>>>(c->A.p, coef.p, J, droff.p, c->F, c->Fp);
   FASST_LAUNCH_CHECK();
-  WArgs w;
-  w.TW = c->TW.p;
-  w.Wkf = c->Wkf.p;
-  w.coef = coef.p;
-  w.psd = dpsd.p;
-  w.X = c->X.p;
-  w.S = dS.p;
-  w.F = c->F;
-  w.T = c->T;
-  w.Fp = c->Fp;
-  w.Tp = c->Tp;
-  w.KP = c->KP;
-  const dim3 grid(c->ntt, c->nft);
-  switch (J) {
-    case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
-    case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
-    case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
-    case 4: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
-    case 5: k_wiener<5><<<grid, 64, 0, c->stream>>>(w); break;
-    case 6: k_wiener<6><<<grid, 64, 0, c->stream>>>(w); break;
-    case 7: k_wiener<7><<<grid, 64, 0, c->stream>>>(w); break;
-    default: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
-  }
-  FASST_LAUNCH_CHECK();
-  k_tf_to_ft<<<dim3(c->ntt, c->nft, J * 2), 256, 0, c->stream>>>(dS.p, hS.p, c->F, c->T, c->Fp, c->Tp);
+  if ((st = launch_wiener(c, coef.p, dpsd.p, dS.p))) return st;
+  k_tf_to_ft<<<dim3(c->ntt, c->nft, NS * 2), 256, 0, c->stream>>>(dS.p, hS.p, c->F, c->T, c->Fp, c->Tp);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipMemcpyAsync(S, hS.p, hS.n * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));
@@ -716,16 +877,16 @@ int fasst_separate_waveforms(fasst_ctx *c, const double *psd, const double *wind
   }
   DeviceGuard g(c->device);
   if ((st = fft_smem(nfft))) return st;
-  const int J = c->J, T = c->T;
+  const int J = c->J, T = c->T, NS = c->nsrc > 0 ? c->nsrc : J;
   const size_t plane = (size_t)c->Tp * c->Fp;
   const int len_out = hop * (T - 1) + wlen - wlen / 2;  // istft (stft.py:108-129)
   DBuf<double> dpsd, coef, dw, daw, dframes, dy;
   DBuf<int> droff;
   DBuf<double2> dS, dtw;
   if ((st = dpsd.alloc(c->Fp)) || (st = coef.alloc((size_t)J * 4 * c->Fp)) ||
-      (st = droff.alloc(kMaxJ + 1)) || (st = dS.alloc((size_t)J * 2 * plane)) ||
+      (st = droff.alloc(kMaxJ + 1)) || (st = dS.alloc((size_t)NS * 2 * plane)) ||
       (st = dw.alloc(wlen)) || (st = daw.alloc(wlen)) || (st = dtw.alloc(nfft / 2)) ||
-      (st = dframes.alloc((size_t)T * wlen)) || (st = dy.alloc((size_t)J * 2 * len_out)))
+      (st = dframes.alloc((size_t)T * wlen)) || (st = dy.alloc((size_t)NS * 2 * len_out)))
     return st;
   auto tw = twiddles(nfft, +1);
   FASST_HIP(hipMemcpyAsync(dpsd.p, psd, c->F * sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -740,33 +901,10 @@ int fasst_separate_waveforms(fasst_ctx *c, const double *psd, const double *wind
   if ((st = launch_w_old(c))) return st;
   k_mixcoef<<<(c->Fp + 255) / 256, 256, 0, c->stream>>>(c->A.p, coef.p, J, droff.p, c->F, c->Fp);
   FASST_LAUNCH_CHECK();
-  WArgs w;
-  w.TW = c->TW.p;
-  w.Wkf = c->Wkf.p;
-  w.coef = coef.p;
-  w.psd = dpsd.p;
-  w.X = c->X.p;
-  w.S = dS.p;
-  w.F = c->F;
-  w.T = c->T;
-  w.Fp = c->Fp;
-  w.Tp = c->Tp;
-  w.KP = c->KP;
-  const dim3 grid(c->ntt, c->nft);
-  switch (J) {
-    case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
-    case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
-    case 3: k_wiener<3><<<grid, 64, 0, c->stream>>>(w); break;
-    case 4: k_wiener<4><<<grid, 64, 0, c->stream>>>(w); break;
-    case 5: k_wiener<5><<<grid, 64, 0, c->stream>>>(w); break;
-    case 6: k_wiener<6><<<grid, 64, 0, c->stream>>>(w); break;
-    case 7: k_wiener<7><<<grid, 64, 0, c->stream>>>(w); break;
-    default: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
-  }
-  FASST_LAUNCH_CHECK();
+  if ((st = launch_wiener(c, coef.p, dpsd.p, dS.p))) return st;
   // each image's frames are rows of its [Tp][Fp] plane: iSTFT straight from
   // HBM (k_istft_frames takes the row stride), only waveforms leave the card
-  for (int q = 0; q < 2 * J; ++q) {
+  for (int q = 0; q < 2 * NS; ++q) {
     k_istft_frames<<<T, 256, nfft * sizeof(double2), c->stream>>>(
         dS.p + (size_t)q * plane, c->Fp, dw.p, wlen, dtw.p, nfft, ilog2(nfft), dframes.p);
     FASST_LAUNCH_CHECK();

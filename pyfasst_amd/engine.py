@@ -91,6 +91,15 @@ class Engine(object):
                                      int(bool(fb_free)), int(bool(tw_free))), "fasst_set_spectral")
         check(lib.fasst_set_fw_prior(self._h, int(j), int(bool(fw_free))), "fasst_set_fw_prior")
 
+    def set_blocks(self, j, kb, fb_free, tw_free):
+        """Spectral components of source j side by side in its columns
+        [kb[b], kb[b + 1]) (fasst_set_blocks)."""
+        kb = np.ascontiguousarray(kb, dtype=np.int32)
+        fb = np.ascontiguousarray(fb_free, dtype=np.int32)
+        tw = np.ascontiguousarray(tw_free, dtype=np.int32)
+        check(lib.fasst_set_blocks(self._h, int(j), kb.size - 1, iptr(kb), iptr(fb), iptr(tw)),
+              "fasst_set_blocks")
+
     def get_spectral(self, j, K):
         FB = np.empty((self.F, K))
         FW = np.empty((K, K))
@@ -132,12 +141,31 @@ class Engine(object):
         n = lib.fasst_kernel_times(self._h, dptr(ms), cnt, nk)
         return {lib.fasst_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(n) if cnt[i]}
 
+    def set_sources(self, sources):
+        """Separation sources (fasst_set_sources): None = one per spatial
+        component; else a list, per source, of (spatial component, column
+        mask) terms."""
+        if sources is None:
+            check(lib.fasst_set_sources(self._h, 0, None, None, None), "fasst_set_sources")
+            self.nsrc = None
+            return
+        off = np.cumsum([0] + [len(t) for t in sources]).astype(np.int32)
+        tj = np.array([j for t in sources for j, _ in t] or [0], dtype=np.int32)
+        tm = np.array([m for t in sources for _, m in t] or [0], dtype=np.uint64)
+        check(lib.fasst_set_sources(self._h, len(sources), iptr(off), iptr(tj),
+                                    tm.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))),
+              "fasst_set_sources")
+        self.nsrc = len(sources)
+
+    def _nsrc(self):
+        return getattr(self, 'nsrc', None) or len(self.structure[0])
+
     def separate_waveforms(self, psd, window, analysis_window, nfft, hop):
-        """Wiener images + per-image iSTFT on the device: [J, 2, len] float64."""
+        """Wiener images + per-image iSTFT on the device: [nsrc, 2, len] float64."""
         psd = np.ascontiguousarray(psd, dtype=np.float64)
         w = np.ascontiguousarray(window, dtype=np.float64)
         aw = np.ascontiguousarray(analysis_window, dtype=np.float64)
-        J = len(self.structure[0])
+        J = self._nsrc()
         n = int(hop) * (self.T - 1) + w.size - w.size // 2
         out = np.empty((J, 2, n))
         check(lib.fasst_separate_waveforms(self._h, dptr(psd), dptr(w), dptr(aw), w.size,
@@ -147,7 +175,7 @@ class Engine(object):
 
     def wiener_images(self, psd, X=None):
         psd = np.ascontiguousarray(psd, dtype=np.float64)
-        J = len(self.structure[0])
+        J = self._nsrc()
         out = np.empty((J, 2, self.F, self.T), dtype=np.complex128)
         xp = None
         if X is not None:

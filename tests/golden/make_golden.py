@@ -47,6 +47,14 @@ CASES = {
     "em_fw_free": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=6, spatial_rank=2,
                        conv=True, n=5000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64),
                        setup='fw_free'),
+    # several spectral components per spatial component (tests/helpers.py
+    # apply_setup 'multi_spec': unequal column blocks, interleaved keys)
+    "em_multi": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=8, spatial_rank=2,
+                     conv=True, n=5000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64),
+                     setup='multi_spec'),
+    "em_multi_inst": dict(cls="MultiChanNMFInst_FASST", nbComps=2, nbNMFComps=8,
+                          spatial_rank=1, conv=False, n=6000, fs=8000,
+                          kw=dict(iter_num=5, wlen=256, hopsize=128), setup='multi_spec'),
 }
 
 
@@ -89,6 +97,7 @@ def run_case(name):
            'psd_lim1': np.asarray(m.noise['ann_PSD_lim'][1])}
 
     def dump(prefix):
+        out['%snspec' % prefix] = np.array(len(m.spec_comps))
         for j, sc in m.spat_comps.items():
             out['%sparams_%d' % (prefix, j)] = np.array(sc['params'])
         for k, comp in m.spec_comps.items():

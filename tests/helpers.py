@@ -18,7 +18,16 @@ CASES = {
                                    tfbpo=12)),
     # FW_frdm_prior 'free' with a dense positive FW (audioModel.py:1578-1631)
     "em_fw_free": (3, 6, 2, True, dict(iter_num=4, wlen=256, hopsize=64, _setup='fw_free')),
+    # several spectral components per spatial component (audioModel.py:430-498,
+    # 1479-1727), keys interleaved over the spatial components, a fixed FB and
+    # a fixed TW among them
+    "em_multi": (3, 8, 2, True, dict(iter_num=4, wlen=256, hopsize=64, _setup='multi_spec')),
+    "em_multi_inst": (2, 8, 1, False, dict(iter_num=5, wlen=256, hopsize=128,
+                                           _setup='multi_spec')),
 }
+
+# column blocks of the 'multi_spec' setup: spatial component j -> block widths
+MULTI_SPLITS = {0: [3, 2, 3], 1: [4, 4], 2: [8]}
 
 
 def apply_setup(m, name):
@@ -31,6 +40,31 @@ def apply_setup(m, name):
             K = fac['FW'].shape[0]
             fac['FW'] = fac['FW'] + 0.3 * np.abs(rs.randn(K, K))
             fac['FW_frdm_prior'] = 'free'
+    elif name == 'multi_spec':
+        import copy
+        pieces = {}
+        for k in sorted(m.spec_comps.keys()):
+            comp = m.spec_comps[k]
+            j = comp['spat_comp_ind']
+            fac = comp['factor'][0]
+            a = 0
+            pieces[j] = []
+            for n in MULTI_SPLITS[j]:
+                f = copy.deepcopy(fac)
+                f['FB'] = np.array(fac['FB'][:, a:a + n])
+                f['FW'] = np.array(fac['FW'][a:a + n, a:a + n])
+                f['TW'] = np.array(fac['TW'][a:a + n])
+                pieces[j].append({'spat_comp_ind': j, 'factor': {0: f}})
+                a += n
+        new, key = {}, 0
+        for pos in range(max(len(v) for v in pieces.values())):
+            for j in sorted(pieces):
+                if pos < len(pieces[j]):
+                    new[key] = pieces[j][pos]
+                    key += 1
+        new[2]['factor'][0]['FB_frdm_prior'] = 'fixed'
+        new[3]['factor'][0]['TW_frdm_prior'] = 'fixed'
+        m.spec_comps = new
     else:
         raise ValueError(name)
 
@@ -68,6 +102,12 @@ def sub_f(F):
 def sub_t(T):
     """Frames kept in the full-size fixtures (about 40, and the last)."""
     return np.unique(np.r_[np.arange(0, T, max(1, T // 40)), T - 1])
+
+
+def spec_keys(g, J):
+    """Spectral component keys of a golden EM case (one per spatial component
+    unless the case recorded its count)."""
+    return range(int(g['init_nspec'])) if 'init_nspec' in g else range(J)
 
 
 def load(name):

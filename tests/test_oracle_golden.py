@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import fasst_ref as R
-from helpers import CASES, CQT_CASES, load, oracle_model_from_golden, rel
+from helpers import CASES, CQT_CASES, load, oracle_model_from_golden, rel, spec_keys
 
 
 def test_inv_herm_known_answer():
@@ -75,6 +75,7 @@ def test_em_golden(case):
     np.testing.assert_array_equal(m.Cx, g['Cx'])
     for j in range(J):
         np.testing.assert_array_equal(np.array(m.spat_comps[j]['params']), g['init_params_%d' % j])
+    for j in spec_keys(g, J):
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FB'], g['init_FB_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['init_TW_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FW'], g['init_FW_%d' % j])
@@ -82,6 +83,7 @@ def test_em_golden(case):
     np.testing.assert_array_equal(ll, g['logliks'])
     for j in range(J):
         np.testing.assert_array_equal(np.array(m.spat_comps[j]['params']), g['final_params_%d' % j])
+    for j in spec_keys(g, J):
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FB'], g['final_FB_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['final_TW_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FW'], g['final_FW_%d' % j])
