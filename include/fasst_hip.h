@@ -88,13 +88,12 @@ int fasst_set_fw_prior(fasst_ctx *ctx, int j, int fw_free);
  * update, :1479-1727): source j's FB / FW / TW (set by fasst_set_spectral)
  * hold the nblk components side by side, component b in columns / rows
  * [kb[b], kb[b + 1]) (kb[0] = 0, kb[nblk] = K_j, FW block diagonal), in the
- * reference's spec_comps key order; fb_free[b] / tw_free[b] are component
- * b's priors.  Restart flags (fasst_run / fasst_renormalize restart_mask)
- * then count one bit per component: bit (sum of nblk of the sources before
- * j) + b.  Free FW with several components: fasst_run returns
- * FASST_ERR_UNSUPPORTED.                                                     */
+ * reference's spec_comps key order; fb_free[b] / fw_free[b] / tw_free[b] are
+ * component b's priors.  Restart flags (fasst_run / fasst_renormalize
+ * restart_mask) then count one bit per component: bit (sum of nblk of the
+ * sources before j) + b.                                                      */
 int fasst_set_blocks(fasst_ctx *ctx, int j, int nblk, const int *kb, const int *fb_free,
-                     const int *tw_free);
+                     const int *fw_free, const int *tw_free);
 
 /* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j (or
  * bit per spectral component, fasst_set_blocks) is set when sum(TW) < eps:

@@ -175,8 +175,8 @@ class FASST(object):
 
         HIP path: stereo; single-factor NMF spectral components (TB empty,
         TW_constr 'NMF'; FB, FW, TW each free or fixed), one or several per
-        spatial component (comp_spat_comp_power sums them, :469-498; free FW
-        only with one per spatial component); all spatial components 'inst' or
+        spatial component (comp_spat_comp_power sums them, :469-498); all
+        spatial components 'inst' or
         all 'conv'; lambdaCorr == 0.
         """
         if self.audioObject.channels != 2:
@@ -201,11 +201,6 @@ class FASST(object):
                 raise NotImplementedError("TW_constr=%s is outside the HIP path" % fac['TW_constr'])
         if sorted(owner.keys()) != list(range(J)):
             raise NotImplementedError("every spatial component needs a spectral component")
-        if any(len(v) > 1 for v in owner.values()) and any(
-                self.spec_comps[k]['factor'][0].get('FW_frdm_prior', 'fixed') == 'free'
-                for k in self.spec_comps):
-            raise NotImplementedError("free FW with several spectral components per spatial "
-                                      "component is outside the HIP path")
         types = set(sc['mix_type'] for sc in self.spat_comps.values())
         if len(types) != 1:
             raise NotImplementedError("mixed inst/conv spatial components are outside the HIP path")
@@ -230,6 +225,7 @@ class FASST(object):
             eng.set_spatial(j, sc['params'], sc['frdm_prior'] == 'free')
             facs = [self.spec_comps[k]['factor'][0] for k in order[j]]
             fb_free = [f.get('FB_frdm_prior', 'free') == 'free' for f in facs]
+            fw_free = [f.get('FW_frdm_prior', 'fixed') == 'free' for f in facs]
             tw_free = [f.get('TW_frdm_prior', 'free') == 'free' for f in facs]
             if len(facs) == 1:
                 FB, FW, TW = facs[0]['FB'], facs[0]['FW'], facs[0]['TW']
@@ -242,9 +238,9 @@ class FASST(object):
                     n = f['FB'].shape[1]
                     FW[a:a + n, a:a + n] = f['FW']
                     a += n
-            eng.set_spectral(j, FB, FW, TW, any(fb_free), any(tw_free),
-                             facs[0].get('FW_frdm_prior', 'fixed') == 'free')
-            eng.set_blocks(j, np.cumsum([0] + [f['FB'].shape[1] for f in facs]), fb_free, tw_free)
+            eng.set_spectral(j, FB, FW, TW, any(fb_free), any(tw_free), any(fw_free))
+            eng.set_blocks(j, np.cumsum([0] + [f['FB'].shape[1] for f in facs]), fb_free, fw_free,
+                           tw_free)
         return order, Ks, conv
 
     def _download(self, order, Ks, conv, updated_spatial=True):

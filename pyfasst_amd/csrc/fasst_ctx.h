@@ -45,6 +45,7 @@ struct fasst_ctx {
   int nblk[fasst::kMaxJ] = {0}, kb[fasst::kMaxJ][fasst::kMaxBlk + 1] = {{0}};
   int soff[fasst::kMaxJ + 1] = {0}, nslot = 0, maxblk = 0, multi = 0;
   int bfb[fasst::kMaxJ][fasst::kMaxBlk] = {{0}}, btw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
+  int bfw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
   fasst::DBuf<double> FB, FW, TW, Wkf, Wkf_new, Wfk_new, FWHt, hatW;
   fasst::DBuf<double> mplanes, bden;  // multi-block update: ratio planes [3][J][Tp][Fp], FB den
   // separation sources (fasst_set_sources; nsrc == 0: one per spatial

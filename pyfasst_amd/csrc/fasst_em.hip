@@ -1259,11 +1259,15 @@ struct FWArgs {
   double *FW;
   int F, T, Fp, Tp, KP, J, ntt, tpc, nchunk, nfc, fpc;
   int K[kMaxJ], fw_free[kMaxJ];
+  int kb0[kMaxJ], kb1[kMaxJ];  // the FW block [kb0, kb1)^2 updated (BLK: the V tiles too)
   double omega;
   const int *halt;
 };
 
-template <int NKC>
+// BLK (one of several spectral components on source j): V_old / V_mid are the
+// component's own powers (comp_spat_comp_power(..., spec_comp_ind=[k]),
+// :1582-1588) and rho is the plane hat_W_j / max(V_c_old, eps).
+template <int NKC, bool BLK = false>
 __global__ __launch_bounds__(64) void k_fw_contract(const FWArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
@@ -1277,6 +1281,10 @@ __global__ __launch_bounds__(64) void k_fw_contract(const FWArgs a) {
   for (int s = 0; s < NKS; ++s) {
     wo[s] = a.Wkf_old[((size_t)j * KP + tq + 4 * s) * a.Fp + f];
     wmid[s] = a.Wkf_mid[((size_t)j * KP + tq + 4 * s) * a.Fp + f];
+    if constexpr (BLK) {
+      const int k = tq + 4 * s;
+      if (k < a.kb0[j] || k >= a.kb1[j]) wo[s] = wmid[s] = 0.0;
+    }
   }
   d4 gn[NKC], gd[NKC];
 #pragma unroll
@@ -1376,6 +1384,7 @@ __global__ __launch_bounds__(256) void k_fw_final(const FWArgs a) {
       n += a.pnum[o];
       d += a.pden[o];
     }
+    if (k1 < a.kb0[j] || k1 >= a.kb1[j] || k2 < a.kb0[j] || k2 >= a.kb1[j]) continue;
     const double ratio = n / fmax(d, kEps);
     FW[k1 * KP + k2] *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
   }
@@ -1921,6 +1930,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
     c->kb[j][0] = 0;
     c->kb[j][1] = K[j];
     c->bfb[j][0] = c->btw[j][0] = 1;
+    c->bfw[j][0] = 0;
     c->soff[j] = j;
   }
   c->soff[J] = c->nslot = J;
@@ -2330,6 +2340,56 @@ static int multi_spectral(fasst_ctx *c, double omega) {
                   (size_t)(c->KP * c->KP + 16 * c->KP + c->KP + 16 * (c->KP + 1)) * sizeof(double),
                   c->stream>>>(u);
     FASST_LAUNCH_CHECK();
+    bool any_fw = false;
+    for (int j = 0; j < J; ++j) any_fw |= b < c->nblk[j] && c->bfw[j][b];
+    if (any_fw) {
+      // FW update of the step's components (:1578-1631): V_mid = (FB_new FW) H
+      // of the component, then W_new rebuilt with FW_new
+      FWArgs w;
+      w.TW = c->TW.p;
+      w.TWt = c->TWt.p;
+      w.Wkf_old = c->Wkf.p;
+      w.Wkf_mid = c->Wkf_new.p;
+      w.hatW = mp.rtw;
+      w.FB = c->FB.p;
+      w.gnum = c->bnum.p;
+      w.gden = c->gden.p;
+      w.pnum = c->pnum.p;
+      w.pden = c->pden.p;
+      w.FW = c->FW.p;
+      w.F = c->F;
+      w.T = c->T;
+      w.Fp = c->Fp;
+      w.Tp = c->Tp;
+      w.KP = c->KP;
+      w.J = J;
+      w.ntt = c->ntt;
+      w.tpc = c->tpc_b;
+      w.nchunk = c->nchunk_b;
+      w.fpc = kFwFpc;
+      w.nfc = (c->F + kFwFpc - 1) / kFwFpc;
+      w.omega = omega;
+      w.halt = c->halt;
+      for (int j = 0; j < kMaxJ; ++j) {
+        const bool has = j < J && b < c->nblk[j];
+        w.K[j] = j < J ? c->K[j] : 0;
+        w.fw_free[j] = has && c->bfw[j][b];
+        w.kb0[j] = has ? c->kb[j][b] : 0;
+        w.kb1[j] = has ? c->kb[j][b + 1] : 0;
+      }
+      const dim3 gc(c->nft, J, c->nchunk_b);
+      switch (nkc) {
+        case 1: k_fw_contract<1, true><<<gc, 64, 0, c->stream>>>(w); break;
+        case 2: k_fw_contract<2, true><<<gc, 64, 0, c->stream>>>(w); break;
+        default: k_fw_contract<4, true><<<gc, 64, 0, c->stream>>>(w); break;
+      }
+      k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
+      k_fw_final<<<J, 256, 0, c->stream>>>(w);
+      k_w_from_fb<<<dim3(c->nft, J), 256, (size_t)(16 * (c->KP + 1) + c->KP * c->KP) * sizeof(double),
+                    c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
+                                 c->halt);
+      FASST_LAUNCH_CHECK();
+    }
     switch (nkc) {
       case 1: k_tw_contract<1, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
       case 2: k_tw_contract<2, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
@@ -2579,6 +2639,8 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     for (int j = 0; j < kMaxJ; ++j) {
       w.K[j] = j < J ? c->K[j] : 0;
       w.fw_free[j] = j < J ? c->fw_free[j] : 0;
+      w.kb0[j] = 0;
+      w.kb1[j] = w.K[j];
     }
     prof_begin(c, KFWU);
     const dim3 gc(c->nft, J, c->nchunk_b);
@@ -2785,14 +2847,15 @@ int fasst_set_fw_prior(fasst_ctx *c, int j, int fw_free) {
   if (st) return st;
 
   c->fw_free[j] = fw_free ? 1 : 0;
+  if (c->nblk[j] == 1) c->bfw[j][0] = c->fw_free[j];
   return FASST_OK;
 }
 
 int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb_free,
-                     const int *tw_free) {
+                     const int *fw_free, const int *tw_free) {
   int st = need_model(c, j);
   if (st) return st;
-  if (nblk < 1 || nblk > kMaxBlk || !kb || !fb_free || !tw_free) {
+  if (nblk < 1 || nblk > kMaxBlk || !kb || !fb_free || !fw_free || !tw_free) {
     set_error("source %d: %d spectral components (1..%d on the HIP path)", j, nblk, kMaxBlk);
     return nblk > kMaxBlk ? FASST_ERR_UNSUPPORTED : FASST_ERR_SHAPE;
   }
@@ -2824,14 +2887,17 @@ int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb
   }
   c->nblk[j] = nblk;
   for (int b = 0; b <= nblk; ++b) c->kb[j][b] = kb[b];
-  bool fbf = false, twf = false;
+  bool fbf = false, twf = false, fwf = false;
   for (int b = 0; b < nblk; ++b) {
     c->bfb[j][b] = fb_free[b] ? 1 : 0;
+    c->bfw[j][b] = fw_free[b] ? 1 : 0;
     c->btw[j][b] = tw_free[b] ? 1 : 0;
     fbf |= c->bfb[j][b] != 0;
+    fwf |= c->bfw[j][b] != 0;
     twf |= c->btw[j][b] != 0;
   }
   c->fb_free[j] = fbf;
+  c->fw_free[j] = fwf;
   c->tw_free[j] = twf;
   c->soff[0] = 0;
   for (int i = 0; i < c->J; ++i) c->soff[i + 1] = c->soff[i] + c->nblk[i];
@@ -2912,13 +2978,6 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   int st = need_model(c, 0);
   if (st) return st;
   if (n_iter < 0 || (n_iter > 0 && (!psd || !logliks))) return FASST_ERR_SHAPE;
-  if (c->multi)
-    for (int j = 0; j < c->J; ++j)
-      if (c->fw_free[j]) {
-        set_error("free FW with several spectral components per spatial component is outside "
-                  "the HIP path");
-        return FASST_ERR_UNSUPPORTED;
-      }
   DeviceGuard g(c->device);
   if (iters_done) *iters_done = 0;
   if (restart_mask) *restart_mask = 0;

@@ -91,14 +91,15 @@ class Engine(object):
                                      int(bool(fb_free)), int(bool(tw_free))), "fasst_set_spectral")
         check(lib.fasst_set_fw_prior(self._h, int(j), int(bool(fw_free))), "fasst_set_fw_prior")
 
-    def set_blocks(self, j, kb, fb_free, tw_free):
+    def set_blocks(self, j, kb, fb_free, fw_free, tw_free):
         """Spectral components of source j side by side in its columns
         [kb[b], kb[b + 1]) (fasst_set_blocks)."""
         kb = np.ascontiguousarray(kb, dtype=np.int32)
         fb = np.ascontiguousarray(fb_free, dtype=np.int32)
+        fw = np.ascontiguousarray(fw_free, dtype=np.int32)
         tw = np.ascontiguousarray(tw_free, dtype=np.int32)
-        check(lib.fasst_set_blocks(self._h, int(j), kb.size - 1, iptr(kb), iptr(fb), iptr(tw)),
-              "fasst_set_blocks")
+        check(lib.fasst_set_blocks(self._h, int(j), kb.size - 1, iptr(kb), iptr(fb), iptr(fw),
+                                   iptr(tw)), "fasst_set_blocks")
 
     def get_spectral(self, j, K):
         FB = np.empty((self.F, K))

@@ -399,12 +399,29 @@ def test_multi_component_tw_restart_vs_oracle():
         assert rel(m.spec_comps[k]['factor'][0]['TW'], o.spec_comps[k]['factor'][0]['TW']) < 1e-8
 
 
-def test_multi_component_free_fw_fails_loudly():
-    m, o, X = _c3_like(33, 40, 2, 8, 1, 1)
-    _split_spec(m, {0: [4, 4], 1: [8]})
-    m.spec_comps[0]['factor'][0]['FW_frdm_prior'] = 'free'
-    with pytest.raises(NotImplementedError):
-        m.estim_param_a_post_model()
+@pytest.mark.parametrize("omega", [1.0, 0.7])
+def test_multi_component_free_fw_vs_oracle(omega):
+    """Free FW (audioModel.py:1578-1631) on some of several spectral components
+    per spatial component: the FW step of a component uses its own V_k
+    (spec_comp_ind=[k]) between its FB and TW steps."""
+    m, o, X = _c3_like(97, 150, 3, 24, 2, 3)
+    for mod in (m, o):
+        mod.nmfUpdateCoeff = omega
+        _split_spec(mod, {0: [10, 14], 1: [8, 8, 8], 2: [24]}, ((4, 'FB'),))
+        for k, seed in ((0, 60), (3, 61), (2, 62)):
+            fac = mod.spec_comps[k]['factor'][0]
+            n = fac['FW'].shape[0]
+            fac['FW'] = fac['FW'] + 0.2 * np.abs(np.random.RandomState(seed).randn(n, n))
+            fac['FW_frdm_prior'] = 'free'
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for k in sorted(o.spec_comps):
+        for key in ('FB', 'FW', 'TW'):
+            assert rel(m.spec_comps[k]['factor'][0][key], o.spec_comps[k]['factor'][0][key]) < 1e-8, \
+                (k, key)
+    groups = _spatial_groups(m)
+    assert rel(np.abs(m.separated_images(groups)), np.abs(o.separated_images(X, groups))) < 1e-8
 
 
 def test_singular_mixing_raises_linalgerror():
