@@ -57,6 +57,8 @@ struct fasst_ctx {
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
   int nsplit_t = 1, fpc_t = 1;  // TW contraction bin chunks
+  int eb_split = 1;             // E-step / FB numerator interleaved over frame ranges
+  int nce_run = 1, ncb_run = 1; // partial-sum chunks the current iteration wrote
   fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rpmax, rpe, rtpart;
   fasst::DBuf<double> gden, TWt, pnum, pden;  // FW update (free FW)
   int nchunk_r = 1;

@@ -149,6 +149,7 @@ struct EArgs {
   double *part;                           // [nchunk][Fp][NACC]
   double *llpart;                         // [nchunk][nft]
   int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
+  int ybase, tbase;  // this launch's chunks start at partial ybase, frame tile tbase (ntt = end)
   int roff[kMaxJ + 1];
   int store_hat;  // 1: hatW holds hat_W itself (general structures), 0: rho = hat_W / max(V, eps)
   const int *halt;
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
   // non-positive / non-finite terms map to -inf / NaN / inf like log().
   double ll = 0.0, lm = 1.0, lev = 0.0, lspec = 0.0;
 
-  const int tb = blockIdx.y * a.tpc;
+  const int tb = a.tbase + blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
   // V^T tile of frame tile tt (all sources) on the MFMA pipe
   auto tile_v = [&](int tt, d4 *v, int lofs) {
@@ -451,10 +452,10 @@ __global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_
     const int u = idx >> 4, ff = idx & 15;
     const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
                      s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
-    a.part[((size_t)blockIdx.y * a.Fp + f0 + ff) * NTOT + UOFF + u] = x;
+    a.part[((size_t)(a.ybase + blockIdx.y) * a.Fp + f0 + ff) * NTOT + UOFF + u] = x;
   }
   if (PART == 1 && tid == 0)
-    a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+    a.llpart[(a.ybase + blockIdx.y) * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
 }
 
 // Single-pass E-step with the per-bin t-reductions on the matrix cores.
@@ -581,7 +582,7 @@ __attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) void k_estep_mx(const EAr
   }
   double ll = 0.0, lm = 1.0, lev = 0.0, lspec = 0.0;
 
-  const int tb = blockIdx.y * a.tpc;
+  const int tb = a.tbase + blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
   for (int tt = tb + wv; tt < te; tt += 4) {
     const int t0 = tt * 16;
@@ -772,10 +773,10 @@ __attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) void k_estep_mx(const EAr
     const int u = idx >> 4, ff = idx & 15;
     const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
                      s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
-    a.part[((size_t)blockIdx.y * a.Fp + f0 + ff) * NACC + u] = x;
+    a.part[((size_t)(a.ybase + blockIdx.y) * a.Fp + f0 + ff) * NACC + u] = x;
   }
   if (tid == 0)
-    a.llpart[blockIdx.y * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+    a.llpart[(a.ybase + blockIdx.y) * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
 }
 
 // sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
@@ -1092,6 +1093,7 @@ struct BArgs {
   double *bnum;  // [nchunk][J][Fp][KP]
   double *bden;  // DEN: [nchunk][J][Fp][KP]
   int F, T, Fp, Tp, KP, J, ntt, nft, tpc;
+  int zbase, tbase;  // this launch's chunks start at partial zbase, frame tile tbase (ntt = end)
   int fb_free[kMaxJ];
   const int *halt;
 };
@@ -1123,7 +1125,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   for (int p = 0; p < (DEN ? FPW : 1); ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
-  const int tb = blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
+  const int tb = a.tbase + blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
   const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
   const double *rdj = DEN ? a.hatW2 + (size_t)j * a.Tp * a.Fp : nullptr;
   for (int tt = tb; tt < te; ++tt) {
@@ -1158,7 +1160,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       }
     }
   }
-  const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Fp;
+  const size_t base = ((size_t)(a.zbase + blockIdx.z) * a.J + j) * a.Fp;
 #pragma unroll
   for (int p = 0; p < FPW; ++p) {
     if (ft0 + p >= a.nft) break;
@@ -1967,6 +1969,8 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
   c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
+  c->eb_split = 1;
+  if (const char *v = getenv("FASST_EB_SPLIT")) c->eb_split = std::max(1, std::min(atoi(v), 8));
   if (getenv("FASST_VERBOSE"))
     fprintf(stderr,
             "fasst: %d CUs; estep %d chunks (cap %ld blocks); fb %d chunks (cap %ld); tw %d "
@@ -1987,9 +1991,10 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(hatW, (size_t)J * Tp * Fp);
   ALLOC(A, (size_t)R * 2 * Fp);
   ALLOC(Pinst, (size_t)R * 2);
-  ALLOC(epart, (size_t)c->nchunk_e * Fp * c->nacc);
-  ALLOC(llpart, (size_t)c->nchunk_e * c->nft);
-  ALLOC(bnum, (size_t)c->nchunk_b * J * Fp * KP);
+  // (+8 chunks: the interleaved E-step / FB ranges round their chunks up)
+  ALLOC(epart, (size_t)(c->nchunk_e + 8) * Fp * c->nacc);
+  ALLOC(llpart, (size_t)(c->nchunk_e + 8) * c->nft);
+  ALLOC(bnum, (size_t)(c->nchunk_b + 8) * J * Fp * KP);
   // FW update (free FW only, allocated with the model so set_spectral may switch it on)
   ALLOC(gden, (size_t)c->nchunk_b * J * Fp * KP);
   ALLOC(TWt, (size_t)J * Tp * KP);
@@ -2137,10 +2142,10 @@ static void estep_dispatch(const fasst_ctx *c, F &&f) {
   }
 }
 
-static void launch_estep(fasst_ctx *c, const EArgs &e) {
+static void launch_estep(fasst_ctx *c, const EArgs &e, int ny) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
-    dim3 grid(c->nft, c->nchunk_e);
+    dim3 grid(c->nft, ny);
     if ((!c->estep_split || T::J > 4) && !T::AB) {
       prof_begin(c, KESTEP);
       k_estep_mx<T::J, T::NKS, T::RKU>
@@ -2188,11 +2193,11 @@ static int estep_occupancy(const fasst_ctx *c) {
 }
 
 template <int NKC>
-static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb) {
+static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb, int nz = 0) {
   if (fb) {
     prof_begin(c, KFBC);
-    k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, c->nchunk_b), 64, 0,
-                               c->stream>>>(b);
+    k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, nz ? nz : c->nchunk_b), 64,
+                               0, c->stream>>>(b);
     prof_end(c, KFBC);
   } else {
     prof_begin(c, KTWC);
@@ -2265,6 +2270,7 @@ static int multi_spectral(fasst_ctx *c, double omega) {
     bb.ntt = c->ntt;
     bb.nft = c->nft;
     bb.tpc = c->tpc_b;
+    bb.zbase = bb.tbase = 0;
     UArgs u;
     u.FB = c->FB.p;
     u.FW = c->FW.p;
@@ -2457,11 +2463,69 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.nft = c->nft;
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
   e.store_hat = 0;
-  launch_estep(c, e);
-  FASST_LAUNCH_CHECK();
-  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
+  e.ybase = e.tbase = 0;
+  BArgs b;
+  b.TW = c->TW.p;
+  b.Wkf = c->Wkf.p;
+  b.FWHt = c->FWHt.p;
+  b.hatW = c->hatW.p;
+  b.hatW2 = nullptr;
+  b.bnum = c->bnum.p;
+  b.bden = nullptr;
+  b.halt = c->halt;
+  b.F = c->F;
+  b.T = c->T;
+  b.Fp = c->Fp;
+  b.Tp = c->Tp;
+  b.KP = c->KP;
+  b.J = J;
+  b.ntt = c->ntt;
+  b.nft = c->nft;
+  b.tpc = c->tpc_b;
+  b.zbase = b.tbase = 0;
+  for (int j = 0; j < kMaxJ; ++j) b.fb_free[j] = j < J ? c->fb_free[j] : 0;
+  const int nkc = c->KP / 16;
+  // E-step and FB numerator interleaved over eb_split frame ranges: each
+  // range's rho is contracted right after it is written, while it is still in
+  // the 256 MB infinity cache (FASST_EB_SPLIT)
+  const int S = c->multi ? 1 : c->eb_split;
+  bool fb_done = false;
+  c->nce_run = c->nchunk_e;
+  c->ncb_run = c->nchunk_b;
+  if (S > 1) {
+    int ye = 0, zb = 0;
+    for (int sc = 0; sc < S; ++sc) {
+      const int T0 = (int)((long)sc * c->ntt / S), T1 = (int)((long)(sc + 1) * c->ntt / S);
+      if (T1 <= T0) continue;
+      const int ne = (T1 - T0 + c->tpc_e - 1) / c->tpc_e, nb = (T1 - T0 + c->tpc_b - 1) / c->tpc_b;
+      e.ybase = ye;
+      e.tbase = T0;
+      e.ntt = T1;
+      launch_estep(c, e, ne);
+      FASST_LAUNCH_CHECK();
+      if (fork && sc == 0) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // FWHt
+      b.zbase = zb;
+      b.tbase = T0;
+      b.ntt = T1;
+      switch (nkc) {
+        case 1: launch_contract<1>(c, b, TArgs(), true, nb); break;
+        case 2: launch_contract<2>(c, b, TArgs(), true, nb); break;
+        default: launch_contract<4>(c, b, TArgs(), true, nb); break;
+      }
+      FASST_LAUNCH_CHECK();
+      ye += ne;
+      zb += nb;
+    }
+    c->nce_run = ye;
+    c->ncb_run = zb;
+    fb_done = true;
+  } else {
+    launch_estep(c, e, c->nchunk_e);
+    FASST_LAUNCH_CHECK();
+    if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
+  }
   prof_begin(c, KLL);
-  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
+  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nce_run * c->nft, ll_dev,
                                      1.0 / ((double)c->F * (double)c->T), c->halt);
   prof_end(c, KLL);
   FASST_LAUNCH_CHECK();
@@ -2486,7 +2550,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     m.Fp = c->Fp;
     m.J = J;
     m.R = c->R;
-    m.nchunk = c->nchunk_e;
+    m.nchunk = c->nce_run;
     m.nacc = c->nacc;
     m.conv_update = c->conv ? 1 : 0;
     m.invT = 1.0 / (double)c->T;
@@ -2528,22 +2592,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     return launch_renorm(c, iter);
   }
   // spectral update: FB then TW (one NMF factor per source)
-  BArgs b;
-  b.TW = c->TW.p;
-  b.Wkf = c->Wkf.p;
-  b.FWHt = c->FWHt.p;
-  b.hatW = c->hatW.p;
-  b.bnum = c->bnum.p;
-  b.halt = c->halt;
-  b.F = c->F;
-  b.T = c->T;
-  b.Fp = c->Fp;
-  b.Tp = c->Tp;
-  b.KP = c->KP;
-  b.J = J;
-  b.ntt = c->ntt;
-  b.nft = c->nft;
-  b.tpc = c->tpc_b;
   TArgs t;
   t.TW = c->TW.p;
   t.Wkf_old = c->Wkf.p;
@@ -2585,7 +2633,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   u.Fp = c->Fp;
   u.KP = c->KP;
   u.J = J;
-  u.nchunk = c->nchunk_b;
+  u.nchunk = c->ncb_run;
   u.omega = omega;
   u.bden = nullptr;
   for (int j = 0; j < kMaxJ; ++j) {
@@ -2593,15 +2641,16 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     tu.kb0[j] = u.kb0[j] = t.kb0[j] = 0;
     tu.kb1[j] = u.kb1[j] = t.kb1[j] = in ? c->K[j] : 0;
     t.tw_free[j] = tu.tw_free[j] = in ? c->tw_free[j] : 0;
-    b.fb_free[j] = u.fb_free[j] = in ? c->fb_free[j] : 0;
+    u.fb_free[j] = in ? c->fb_free[j] : 0;
   }
-  const int nkc = c->KP / 16;
-  switch (nkc) {
-    case 1: launch_contract<1>(c, b, t, true); break;
-    case 2: launch_contract<2>(c, b, t, true); break;
-    default: launch_contract<4>(c, b, t, true); break;
+  if (!fb_done) {
+    switch (nkc) {
+      case 1: launch_contract<1>(c, b, t, true); break;
+      case 2: launch_contract<2>(c, b, t, true); break;
+      default: launch_contract<4>(c, b, t, true); break;
+    }
+    FASST_LAUNCH_CHECK();
   }
-  FASST_LAUNCH_CHECK();
   prof_begin(c, KFBU);
   k_fb_update<<<dim3(c->nft, J), 256,
                 (size_t)(c->KP * c->KP + 16 * c->KP + c->KP + 16 * (c->KP + 1)) * sizeof(double),
