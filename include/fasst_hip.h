@@ -95,6 +95,14 @@ int fasst_set_fw_prior(fasst_ctx *ctx, int j, int fw_free);
 int fasst_set_blocks(fasst_ctx *ctx, int j, int nblk, const int *kb, const int *fb_free,
                      const int *fw_free, const int *tw_free);
 
+/* lambdaCorr (audioModel.py:1484-1507 and the corrPen terms of :1544-1719):
+ * the inter-source correlation penalty of the spectral updates.  With
+ * lambda > 0 the components are updated one at a time in the reference's
+ * spec_comps key order: component q is block seq_b[q] of spatial component
+ * seq_j[q] (fasst_set_blocks layout; nseq = every component, once).
+ * lambda = 0 (the default after fasst_configure) switches it off.           */
+int fasst_set_corr(fasst_ctx *ctx, double lambda, int nseq, const int *seq_j, const int *seq_b);
+
 /* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j (or
  * bit per spectral component, fasst_set_blocks) is set when sum(TW) < eps:
  * the caller draws the restart (host RNG order).                            */

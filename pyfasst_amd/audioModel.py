@@ -176,14 +176,12 @@ class FASST(object):
         HIP path: stereo; single-factor NMF spectral components (TB empty,
         TW_constr 'NMF'; FB, FW, TW each free or fixed), one or several per
         spatial component (comp_spat_comp_power sums them, :469-498); all
-        spatial components 'inst' or
-        all 'conv'; lambdaCorr == 0.
+        spatial components 'inst' or all 'conv'; any lambdaCorr >= 0 (the
+        inter-source correlation penalty, :1484-1719).
         """
         if self.audioObject.channels != 2:
             raise AttributeError("Nb channels " + str(self.audioObject.channels) +
                                  " not implemented yet")
-        if self.lambdaCorr > 0:
-            raise NotImplementedError("lambdaCorr > 0 is outside the HIP path")
         J = len(self.spat_comps)
         if sorted(self.spat_comps.keys()) != list(range(J)):
             raise NotImplementedError("spatial components must be numbered 0..J-1")
@@ -241,6 +239,12 @@ class FASST(object):
             eng.set_spectral(j, FB, FW, TW, any(fb_free), any(tw_free), any(fw_free))
             eng.set_blocks(j, np.cumsum([0] + [f['FB'].shape[1] for f in facs]), fb_free, fw_free,
                            tw_free)
+        if self.lambdaCorr > 0:   # components one at a time in key order (:1479)
+            pos = {k: (j, b) for j, keys in enumerate(order) for b, k in enumerate(keys)}
+            seq = [pos[k] for k in sorted(self.spec_comps.keys())]
+            eng.set_corr(self.lambdaCorr, [j for j, _ in seq], [b for _, b in seq])
+        else:
+            eng.set_corr(0.0)
         return order, Ks, conv
 
     def _download(self, order, Ks, conv, updated_spatial=True):

@@ -47,7 +47,11 @@ struct fasst_ctx {
   int bfb[fasst::kMaxJ][fasst::kMaxBlk] = {{0}}, btw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
   int bfw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
   fasst::DBuf<double> FB, FW, TW, Wkf, Wkf_new, Wfk_new, FWHt, hatW;
-  fasst::DBuf<double> mplanes, bden;  // multi-block update: ratio planes [3][J][Tp][Fp], FB den
+  fasst::DBuf<double> mplanes, bden;  // multi-block update: ratio planes [5][J][Tp][Fp], FB den
+  // lambdaCorr > 0 (fasst_set_corr): the components go one at a time in the
+  // reference's key order (seq_j[q], seq_b[q]) through the multi-block path
+  double lambda = 0.0;
+  int nseq = 0, seq_j[fasst::kMaxSlot] = {0}, seq_b[fasst::kMaxSlot] = {0};
   // separation sources (fasst_set_sources; nsrc == 0: one per spatial
   // component): source n sums the terms [toff[n], toff[n + 1]), term i = the
   // columns tmask[i] (bit k = column k) of spatial component tj[i]

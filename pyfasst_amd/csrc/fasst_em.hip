@@ -1262,6 +1262,7 @@ struct FWArgs {
   int F, T, Fp, Tp, KP, J, ntt, tpc, nchunk, nfc, fpc;
   int K[kMaxJ], fw_free[kMaxJ];
   int kb0[kMaxJ], kb1[kMaxJ];  // the FW block [kb0, kb1)^2 updated (BLK: the V tiles too)
+  const double *cp, *pw;       // LAM: corrPen / powers planes of k_multi_prep
   double omega;
   const int *halt;
 };
@@ -1269,7 +1270,7 @@ struct FWArgs {
 // BLK (one of several spectral components on source j): V_old / V_mid are the
 // component's own powers (comp_spat_comp_power(..., spec_comp_ind=[k]),
 // :1582-1588) and rho is the plane hat_W_j / max(V_c_old, eps).
-template <int NKC, bool BLK = false>
+template <int NKC, bool BLK = false, bool LAM = false>
 __global__ __launch_bounds__(64) void k_fw_contract(const FWArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
@@ -1311,8 +1312,16 @@ __global__ __launch_bounds__(64) void k_fw_contract(const FWArgs a) {
       const double rho = ok ? rhoj[(size_t)t * a.Fp + f] : 0.0;
       const double other = fmax(vo[i], kEps);
       const double rv = 1.0 / fmax(vm[i], kEps);
-      rn[i] = ok ? ((rho * other) * (rv * rv)) * other : 0.0;  // (hat_W / vm^2) other
-      rd[i] = ok ? other * rv : 0.0;                           // other (1 / vm)
+      if constexpr (LAM) {   // corrPen terms (audioModel.py:1596-1628)
+        const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f;
+        const double cp = ok ? a.cp[o] : 0.0, pw = ok ? a.pw[o] : 1.0;
+        const double vmm = fmax(vm[i], kEps);
+        rn[i] = ok ? ((rho * other) * (rv * rv) + cp * (2.0 * (vmm / pw))) * other : 0.0;
+        rd[i] = ok ? other * (rv + cp) : 0.0;
+      } else {
+        rn[i] = ok ? ((rho * other) * (rv * rv)) * other : 0.0;  // (hat_W / vm^2) other
+        rd[i] = ok ? other * rv : 0.0;                           // other (1 / vm)
+      }
     }
     const double *ht = a.TWt + ((size_t)j * a.Tp + t0 + tq) * KP + fl;  // H^T[t][k]
 #pragma unroll
@@ -1399,6 +1408,7 @@ struct TArgs {
   int F, T, Fp, Tp, KP, J, nft, ntt, fpc;
   int tw_free[kMaxJ];
   int kb0[kMaxJ], kb1[kMaxJ];  // BLK: the V tiles sum the columns [kb0, kb1) only
+  const double *cp, *pw;       // LAM: corrPen / powers planes of k_multi_prep
   const int *halt;
 };
 
@@ -1413,7 +1423,7 @@ struct TArgs {
 // BLK (one of several spectral components on source j): V_old / V_new are the
 // component's own powers W_c H_c (the reference's spec_comp_ind=[k],
 // audioModel.py:1639-1645), and rho is the plane hat_W_j / max(V_c_old, eps).
-template <int NKC, int TPW, bool BLK = false>
+template <int NKC, int TPW, bool BLK = false, bool LAM = false>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
@@ -1481,8 +1491,15 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
         const double rv = rcp_nr(vm);
         const bool ok = tok && f0 + tq + 4 * i < a.F;
         const double hw = h[i] * other;  // hat_W from the E-step's rho
-        r3[i] = ok ? other * (hw * (rv * rv)) : 0.0;
-        r4[i] = ok ? other * rv : 0.0;
+        if constexpr (LAM) {   // corrPen terms (audioModel.py:1650-1719)
+          const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + tq + 4 * i;
+          const double cp = ok ? a.cp[o] : 0.0, pw = ok ? a.pw[o] : 1.0;
+          r3[i] = ok ? other * (hw * (rv * rv) + cp * (2.0 * (vm / pw))) : 0.0;
+          r4[i] = ok ? other * (rv + cp) : 0.0;
+        } else {
+          r3[i] = ok ? other * (hw * (rv * rv)) : 0.0;
+          r4[i] = ok ? other * rv : 0.0;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -1569,12 +1586,23 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
 struct MPArgs {
   const double *TW, *Wkf;
   double *hatW, *rnum, *rden, *rtw;   // planes [J][Tp][Fp]
+  double *rcp, *rpow;                 // LAM: corrPen and max(sum_j V_j, eps) planes
+  double lambda;
   int F, T, Fp, Tp, KP, J, ntt, tpc, first;
   int on[kMaxJ], kb0[kMaxJ], kb1[kMaxJ];
   const int *halt;
 };
 
-template <int NKC>
+// LAM (lambdaCorr > 0, audioModel.py:1484-1507, :1544-1569): the planes
+// carry the inter-source correlation penalty of the component's FB step,
+//   powers = max(sum_j' V_j', eps) (comp_spat_cmps_powers, summed in source
+//   order), minus = max(powers - max(V_j, eps), eps) (the reference's
+//   `np.all(minus >= 0)` branch always holds: a sum of non-negative powers is
+//   never below one of its terms), cp = lambda minus / max(powers^2, eps)
+//   rden = other (1/max(V_j) + cp), rnum = (hat_W/max(V_j)^2 + cp 2 (max(V_j)/powers)) other
+// and cp / powers go to two more planes for the FW / TW steps, which use the
+// same cp with the component's own power (:1596-1620, :1650-1719).
+template <int NKC, bool LAM = false>
 __global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
@@ -1595,12 +1623,26 @@ __global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
   for (int tt = tb; tt < te; ++tt) {
     const int t0 = tt * 16;
     const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
-    d4 vj = d4{0.0, 0.0, 0.0, 0.0}, vc = vj;
+    d4 vj = d4{0.0, 0.0, 0.0, 0.0}, vc = vj, vall = vj;
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       const double h = tw[(size_t)(4 * s) * a.Tp];
       vj = mfma4(h, wj[s], vj);
       vc = mfma4(h, wc[s], vc);
+    }
+    if constexpr (LAM) {
+      for (int jj = 0; jj < a.J; ++jj) {   // sum_j' V_j' in source order
+        d4 v = d4{0.0, 0.0, 0.0, 0.0};
+        if (jj == j) {
+          v = vj;
+        } else {
+          const double *twj = a.TW + ((size_t)jj * a.KP + tq) * a.Tp + t0 + fl;
+          const double *wk = a.Wkf + ((size_t)jj * a.KP + tq) * a.Fp + f;
+          for (int s = 0; s < NKS; ++s)
+            v = mfma4(twj[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v);
+        }
+        vall += v;
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1608,6 +1650,7 @@ __global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
       const size_t o = pj + (size_t)t * a.Fp + f;
       if (t >= a.T || f >= a.F) {
         a.rnum[o] = a.rden[o] = a.rtw[o] = 0.0;
+        if constexpr (LAM) a.rcp[o] = a.rpow[o] = 0.0;
         continue;
       }
       const double sj = fmax(vj[i], kEps), sc = fmax(vc[i], kEps);
@@ -1618,8 +1661,18 @@ __global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
       } else {
         hw = a.hatW[o];
       }
-      a.rnum[o] = (hw / (sj * sj)) * sc;
-      a.rden[o] = sc * (1.0 / sj);
+      if constexpr (LAM) {
+        const double pw = fmax(vall[i], kEps);
+        const double minus = fmax(pw - sj, kEps);
+        const double cp = a.lambda * minus / fmax(pw * pw, kEps);
+        a.rden[o] = sc * (1.0 / sj + cp);
+        a.rnum[o] = (hw / (sj * sj) + cp * (2.0 * (sj / pw))) * sc;
+        a.rcp[o] = cp;
+        a.rpow[o] = pw;
+      } else {
+        a.rnum[o] = (hw / (sj * sj)) * sc;
+        a.rden[o] = sc * (1.0 / sj);
+      }
       a.rtw[o] = hw / sc;
     }
   }
@@ -1939,6 +1992,8 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   c->maxblk = 1;
   c->multi = 0;
   c->nsrc = 0;
+  c->lambda = 0.0;
+  c->nseq = 0;
   const int Fp = c->Fp, Tp = c->Tp, KP = c->KP;
   // Launch shapes sized to whole rounds of resident blocks (a partial last
   // round idles most of the chip): E-step blocks = f tiles x frame chunks,
@@ -2231,10 +2286,14 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
 // (see k_multi_prep): step b updates block b of every source that has one
 // (FB, then TW), all launches on c->stream; W = FB FW of the step's result
 // becomes the next step's current W.
-static int multi_spectral(fasst_ctx *c, double omega) {
+// one step: block b of every source that has one (only_j < 0), or of source
+// only_j alone (lambdaCorr > 0: the penalty couples the sources, so the
+// components go one at a time in the reference's key order)
+static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
   const int J = c->J, nkc = c->KP / 16;
   const size_t plane = (size_t)J * c->Tp * c->Fp;
-  for (int b = 0; b < c->maxblk; ++b) {
+  const bool lam = c->lambda > 0.0;
+  {
     MPArgs mp;
     mp.TW = c->TW.p;
     mp.Wkf = c->Wkf.p;
@@ -2242,6 +2301,9 @@ static int multi_spectral(fasst_ctx *c, double omega) {
     mp.rnum = c->mplanes.p;
     mp.rden = c->mplanes.p + plane;
     mp.rtw = c->mplanes.p + 2 * plane;
+    mp.rcp = c->mplanes.p + 3 * plane;
+    mp.rpow = c->mplanes.p + 4 * plane;
+    mp.lambda = c->lambda;
     mp.F = c->F;
     mp.T = c->T;
     mp.Fp = c->Fp;
@@ -2315,8 +2377,10 @@ static int multi_spectral(fasst_ctx *c, double omega) {
     tu.J = J;
     tu.nsplit = c->nsplit_t;
     tu.omega = omega;
+    t.cp = mp.rcp;
+    t.pw = mp.rpow;
     for (int j = 0; j < kMaxJ; ++j) {
-      const bool has = j < J && b < c->nblk[j];
+      const bool has = j < J && b < c->nblk[j] && (only_j < 0 || j == only_j);
       mp.on[j] = has;
       const int k0 = has ? c->kb[j][b] : 0, k1 = has ? c->kb[j][b + 1] : 0;
       mp.kb0[j] = u.kb0[j] = t.kb0[j] = tu.kb0[j] = k0;
@@ -2329,15 +2393,18 @@ static int multi_spectral(fasst_ctx *c, double omega) {
     const dim3 gt((c->ntt + kTPW - 1) / kTPW, J, c->nsplit_t);
     switch (nkc) {
       case 1:
-        k_multi_prep<1><<<gp, 64, 0, c->stream>>>(mp);
+        if (lam) k_multi_prep<1, true><<<gp, 64, 0, c->stream>>>(mp);
+        else k_multi_prep<1><<<gp, 64, 0, c->stream>>>(mp);
         k_fb_contract<1, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
         break;
       case 2:
-        k_multi_prep<2><<<gp, 64, 0, c->stream>>>(mp);
+        if (lam) k_multi_prep<2, true><<<gp, 64, 0, c->stream>>>(mp);
+        else k_multi_prep<2><<<gp, 64, 0, c->stream>>>(mp);
         k_fb_contract<2, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
         break;
       default:
-        k_multi_prep<4><<<gp, 64, 0, c->stream>>>(mp);
+        if (lam) k_multi_prep<4, true><<<gp, 64, 0, c->stream>>>(mp);
+        else k_multi_prep<4><<<gp, 64, 0, c->stream>>>(mp);
         k_fb_contract<4, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
         break;
     }
@@ -2347,7 +2414,7 @@ static int multi_spectral(fasst_ctx *c, double omega) {
                   c->stream>>>(u);
     FASST_LAUNCH_CHECK();
     bool any_fw = false;
-    for (int j = 0; j < J; ++j) any_fw |= b < c->nblk[j] && c->bfw[j][b];
+    for (int j = 0; j < J; ++j) any_fw |= b < c->nblk[j] && c->bfw[j][b] && (only_j < 0 || j == only_j);
     if (any_fw) {
       // FW update of the step's components (:1578-1631): V_mid = (FB_new FW) H
       // of the component, then W_new rebuilt with FW_new
@@ -2376,8 +2443,10 @@ static int multi_spectral(fasst_ctx *c, double omega) {
       w.nfc = (c->F + kFwFpc - 1) / kFwFpc;
       w.omega = omega;
       w.halt = c->halt;
+      w.cp = mp.rcp;
+      w.pw = mp.rpow;
       for (int j = 0; j < kMaxJ; ++j) {
-        const bool has = j < J && b < c->nblk[j];
+        const bool has = j < J && b < c->nblk[j] && (only_j < 0 || j == only_j);
         w.K[j] = j < J ? c->K[j] : 0;
         w.fw_free[j] = has && c->bfw[j][b];
         w.kb0[j] = has ? c->kb[j][b] : 0;
@@ -2385,9 +2454,18 @@ static int multi_spectral(fasst_ctx *c, double omega) {
       }
       const dim3 gc(c->nft, J, c->nchunk_b);
       switch (nkc) {
-        case 1: k_fw_contract<1, true><<<gc, 64, 0, c->stream>>>(w); break;
-        case 2: k_fw_contract<2, true><<<gc, 64, 0, c->stream>>>(w); break;
-        default: k_fw_contract<4, true><<<gc, 64, 0, c->stream>>>(w); break;
+        case 1:
+          if (lam) k_fw_contract<1, true, true><<<gc, 64, 0, c->stream>>>(w);
+          else k_fw_contract<1, true><<<gc, 64, 0, c->stream>>>(w);
+          break;
+        case 2:
+          if (lam) k_fw_contract<2, true, true><<<gc, 64, 0, c->stream>>>(w);
+          else k_fw_contract<2, true><<<gc, 64, 0, c->stream>>>(w);
+          break;
+        default:
+          if (lam) k_fw_contract<4, true, true><<<gc, 64, 0, c->stream>>>(w);
+          else k_fw_contract<4, true><<<gc, 64, 0, c->stream>>>(w);
+          break;
       }
       k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
       k_fw_final<<<J, 256, 0, c->stream>>>(w);
@@ -2397,9 +2475,18 @@ static int multi_spectral(fasst_ctx *c, double omega) {
       FASST_LAUNCH_CHECK();
     }
     switch (nkc) {
-      case 1: k_tw_contract<1, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
-      case 2: k_tw_contract<2, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
-      default: k_tw_contract<4, kTPW, true><<<gt, 64, 0, c->stream>>>(t); break;
+      case 1:
+        if (lam) k_tw_contract<1, kTPW, true, true><<<gt, 64, 0, c->stream>>>(t);
+        else k_tw_contract<1, kTPW, true><<<gt, 64, 0, c->stream>>>(t);
+        break;
+      case 2:
+        if (lam) k_tw_contract<2, kTPW, true, true><<<gt, 64, 0, c->stream>>>(t);
+        else k_tw_contract<2, kTPW, true><<<gt, 64, 0, c->stream>>>(t);
+        break;
+      default:
+        if (lam) k_tw_contract<4, kTPW, true, true><<<gt, 64, 0, c->stream>>>(t);
+        else k_tw_contract<4, kTPW, true><<<gt, 64, 0, c->stream>>>(t);
+        break;
     }
     FASST_LAUNCH_CHECK();
     k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
@@ -2408,6 +2495,18 @@ static int multi_spectral(fasst_ctx *c, double omega) {
     FASST_HIP(hipMemcpyAsync(c->Wkf.p, c->Wkf_new.p, (size_t)J * c->KP * c->Fp * sizeof(double),
                              hipMemcpyDeviceToDevice, c->stream));
   }
+  return FASST_OK;
+}
+
+static int multi_spectral(fasst_ctx *c, double omega) {
+  int st;
+  if (c->lambda > 0.0) {
+    for (int q = 0; q < c->nseq; ++q)
+      if ((st = multi_step(c, omega, c->seq_b[q], c->seq_j[q]))) return st;
+    return FASST_OK;
+  }
+  for (int b = 0; b < c->maxblk; ++b)
+    if ((st = multi_step(c, omega, b, -1))) return st;
   return FASST_OK;
 }
 
@@ -2930,7 +3029,7 @@ int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb
   DeviceGuard g(c->device);
   if (maxblk > 1) {
     const size_t plane = (size_t)c->J * c->Tp * c->Fp;
-    if (c->mplanes.n < 3 * plane && (st = c->mplanes.alloc(3 * plane))) return st;
+    if (c->mplanes.n < 5 * plane && (st = c->mplanes.alloc(5 * plane))) return st;
     const size_t nb = (size_t)c->nchunk_b * c->J * c->Fp * c->KP;
     if (c->bden.n < nb && (st = c->bden.alloc(nb))) return st;
   }
@@ -2952,7 +3051,41 @@ int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb
   for (int i = 0; i < c->J; ++i) c->soff[i + 1] = c->soff[i] + c->nblk[i];
   c->nslot = nslot;
   c->maxblk = maxblk;
-  c->multi = maxblk > 1;
+  c->multi = maxblk > 1 || c->lambda > 0.0;
+  return FASST_OK;
+}
+
+int fasst_set_corr(fasst_ctx *c, double lambda, int nseq, const int *seq_j, const int *seq_b) {
+  int st = need_model(c, 0);
+  if (st) return st;
+  if (!(lambda >= 0.0) || (lambda > 0.0 && (nseq < 1 || nseq > kMaxSlot || !seq_j || !seq_b))) {
+    set_error("fasst_set_corr: lambda %g with %d components", lambda, nseq);
+    return FASST_ERR_SHAPE;
+  }
+  if (lambda > 0.0) {
+    int seen[kMaxJ][kMaxBlk] = {{0}};
+    for (int q = 0; q < nseq; ++q) {
+      const int j = seq_j[q], b = seq_b[q];
+      if (j < 0 || j >= c->J || b < 0 || b >= c->nblk[j] || seen[j][b]++) {
+        set_error("fasst_set_corr: bad component (%d, %d) at position %d", j, b, q);
+        return FASST_ERR_SHAPE;
+      }
+      c->seq_j[q] = j;
+      c->seq_b[q] = b;
+    }
+    if (nseq != c->nslot) {
+      set_error("fasst_set_corr: %d components given, the model has %d", nseq, c->nslot);
+      return FASST_ERR_SHAPE;
+    }
+    DeviceGuard g(c->device);
+    const size_t plane = (size_t)c->J * c->Tp * c->Fp;
+    if (c->mplanes.n < 5 * plane && (st = c->mplanes.alloc(5 * plane))) return st;
+    const size_t nb = (size_t)c->nchunk_b * c->J * c->Fp * c->KP;
+    if (c->bden.n < nb && (st = c->bden.alloc(nb))) return st;
+  }
+  c->lambda = lambda;
+  c->nseq = lambda > 0.0 ? nseq : 0;
+  c->multi = c->maxblk > 1 || lambda > 0.0;
   return FASST_OK;
 }
 

@@ -101,6 +101,13 @@ class Engine(object):
         check(lib.fasst_set_blocks(self._h, int(j), kb.size - 1, iptr(kb), iptr(fb), iptr(fw),
                                    iptr(tw)), "fasst_set_blocks")
 
+    def set_corr(self, lam, seq_j=(), seq_b=()):
+        """lambdaCorr and the spectral components' key order (fasst_set_corr)."""
+        sj = np.ascontiguousarray(list(seq_j) or [0], dtype=np.int32)
+        sb = np.ascontiguousarray(list(seq_b) or [0], dtype=np.int32)
+        check(lib.fasst_set_corr(self._h, float(lam), len(seq_j), iptr(sj), iptr(sb)),
+              "fasst_set_corr")
+
     def get_spectral(self, j, K):
         FB = np.empty((self.F, K))
         FW = np.empty((K, K))

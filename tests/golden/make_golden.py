@@ -55,6 +55,14 @@ CASES = {
     "em_multi_inst": dict(cls="MultiChanNMFInst_FASST", nbComps=2, nbNMFComps=8,
                           spatial_rank=1, conv=False, n=6000, fs=8000,
                           kw=dict(iter_num=5, wlen=256, hopsize=128), setup='multi_spec'),
+    # lambdaCorr > 0 (audioModel.py:1484-1719), one and several components per source
+    "em_lambda": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=8, spatial_rank=2,
+                      conv=True, n=5000, fs=8000,
+                      kw=dict(iter_num=4, wlen=256, hopsize=64, lambdaCorr=0.4)),
+    "em_lambda_multi": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=8, spatial_rank=2,
+                            conv=True, n=5000, fs=8000,
+                            kw=dict(iter_num=3, wlen=256, hopsize=64, lambdaCorr=0.7),
+                            setup='multi_spec'),
 }
 
 

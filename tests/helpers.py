@@ -24,6 +24,10 @@ CASES = {
     "em_multi": (3, 8, 2, True, dict(iter_num=4, wlen=256, hopsize=64, _setup='multi_spec')),
     "em_multi_inst": (2, 8, 1, False, dict(iter_num=5, wlen=256, hopsize=128,
                                            _setup='multi_spec')),
+    # lambdaCorr > 0: the inter-source correlation penalty (audioModel.py:1484-1719)
+    "em_lambda": (3, 8, 2, True, dict(iter_num=4, wlen=256, hopsize=64, lambdaCorr=0.4)),
+    "em_lambda_multi": (3, 8, 2, True, dict(iter_num=3, wlen=256, hopsize=64, lambdaCorr=0.7,
+                                            _setup='multi_spec')),
 }
 
 # column blocks of the 'multi_spec' setup: spatial component j -> block widths
@@ -136,7 +140,8 @@ def oracle_model_from_golden(g, case):
                            fmax=kw.get('tffmax', 18000), bins=kw.get('tfbpo', 48),
                            fs=int(g['fs']), linFTLen=wlen, atomHopFactor=hop / float(wlen))
         X = [t.forward(x[:, c]) for c in range(2)]
-    okw = {k: v for k, v in kw.items() if k in ('iter_num', 'sim_ann_opt', 'nmfUpdateCoeff')}
+    okw = {k: v for k, v in kw.items() if k in ('iter_num', 'sim_ann_opt', 'nmfUpdateCoeff',
+                                              'lambdaCorr')}
     m = R.RefFASST(**okw)
     m.set_transform(X)
     np.random.seed(0)

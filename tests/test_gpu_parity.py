@@ -424,6 +424,40 @@ def test_multi_component_free_fw_vs_oracle(omega):
     assert rel(np.abs(m.separated_images(groups)), np.abs(o.separated_images(X, groups))) < 1e-8
 
 
+@pytest.mark.parametrize("lam,splits,fw", [
+    (0.3, None, False),                                  # one component per source
+    (0.5, {0: [10, 14], 1: [8, 8, 8], 2: [24]}, False),  # several, keys interleaved
+    (0.2, {0: [12, 12], 1: [24], 2: [6, 18]}, True),     # with free FW on some components
+])
+def test_lambda_corr_vs_oracle(lam, splits, fw):
+    """lambdaCorr > 0 (audioModel.py:1484-1507 and the corrPen terms of the FB /
+    FW / TW steps, :1544-1719): every component updated one at a time in key
+    order against the powers of all sources, vs the oracle (pinned to the
+    reference by the em_lambda / em_lambda_multi golden cases)."""
+    m, o, X = _c3_like(97, 150, 3, 24, 2, 3)
+    for mod in (m, o):
+        mod.lambdaCorr = lam
+        if splits:
+            _split_spec(mod, splits, ((3, 'TW'),))
+        if fw:
+            for k, seed in ((0, 70), (4, 71)):
+                fac = mod.spec_comps[k]['factor'][0]
+                n = fac['FW'].shape[0]
+                fac['FW'] = fac['FW'] + 0.2 * np.abs(np.random.RandomState(seed).randn(n, n))
+                fac['FW_frdm_prior'] = 'free'
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for k in sorted(o.spec_comps):
+        for key in ('FB', 'FW', 'TW'):
+            assert rel(m.spec_comps[k]['factor'][0][key], o.spec_comps[k]['factor'][0][key]) < 1e-8, \
+                (k, key)
+    for j in range(3):
+        assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+    groups = _spatial_groups(m)
+    assert rel(np.abs(m.separated_images(groups)), np.abs(o.separated_images(X, groups))) < 1e-8
+
+
 def test_singular_mixing_raises_linalgerror():
     """A silent source makes hat_Rss[f] singular: LinAlgError('Singular Matrix')
     as the reference's conv solve (audioModel.py:855-861)."""
@@ -453,10 +487,6 @@ def test_tw_restart_vs_oracle():
 
 def test_unsupported_structures_fail_loudly():
     m, o, X = _c3_like(33, 40, 2, 4, 1, 1)
-    m.lambdaCorr = 0.1
-    with pytest.raises(NotImplementedError):
-        m.estim_param_a_post_model()
-    m.lambdaCorr = 0.
     m.spec_comps[0]['factor'][0]['TW_constr'] = 'HMM'
     with pytest.raises(NotImplementedError):
         m.estim_param_a_post_model()
