@@ -63,6 +63,10 @@ CASES = {
                             conv=True, n=5000, fs=8000,
                             kw=dict(iter_num=3, wlen=256, hopsize=64, lambdaCorr=0.7),
                             setup='multi_spec'),
+    # time blobs on the three components (tests/helpers.py apply_setup 'tb')
+    "em_tb": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=8, spatial_rank=2,
+                  conv=True, n=5000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64),
+                  setup='tb'),
 }
 
 
@@ -113,6 +117,8 @@ def run_case(name):
             out['%sFB_%d' % (prefix, k)] = np.array(f['FB'])
             out['%sFW_%d' % (prefix, k)] = np.array(f['FW'])
             out['%sTW_%d' % (prefix, k)] = np.array(f['TW'])
+            if len(f['TB']):
+                out['%sTB_%d' % (prefix, k)] = np.array(f['TB'])
     dump('init_')
     # one E-step on the initial state (pins compute_suff_stat itself)
     if m.noise['sim_ann_opt'] == 'ann':

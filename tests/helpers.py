@@ -28,7 +28,13 @@ CASES = {
     "em_lambda": (3, 8, 2, True, dict(iter_num=4, wlen=256, hopsize=64, lambdaCorr=0.4)),
     "em_lambda_multi": (3, 8, 2, True, dict(iter_num=3, wlen=256, hopsize=64, lambdaCorr=0.7,
                                             _setup='multi_spec')),
+    # time blobs H = TW.TB (audioModel.py:1665-1691, 1931-1978, 2029-2033): TB
+    # free with TW free, TB free with TW fixed, TB fixed
+    "em_tb": (3, 8, 2, True, dict(iter_num=4, wlen=256, hopsize=64, _setup='tb')),
 }
+
+# time blobs of the 'tb' setup: spectral component key -> (L, TB prior, TW prior)
+TB_SETUP = {0: (4, 'free', 'free'), 1: (6, 'free', 'fixed'), 2: (3, 'fixed', 'free')}
 
 # column blocks of the 'multi_spec' setup: spatial component j -> block widths
 MULTI_SPLITS = {0: [3, 2, 3], 1: [4, 4], 2: [8]}
@@ -69,6 +75,16 @@ def apply_setup(m, name):
         new[2]['factor'][0]['FB_frdm_prior'] = 'fixed'
         new[3]['factor'][0]['TW_frdm_prior'] = 'fixed'
         m.spec_comps = new
+    elif name == 'tb':
+        for k, (L, tb_prior, tw_prior) in TB_SETUP.items():
+            fac = m.spec_comps[k]['factor'][0]
+            K, T = fac['TW'].shape
+            rs = np.random.RandomState(300 + k)
+            TB = np.abs(rs.randn(L, T)) + 0.2
+            TW = np.abs(rs.randn(K, L)) + 0.2
+            TW *= fac['TW'].mean() / np.dot(TW, TB).mean()
+            fac['TW'], fac['TB'] = TW, TB
+            fac['TB_frdm_prior'], fac['TW_frdm_prior'] = tb_prior, tw_prior
     else:
         raise ValueError(name)
 

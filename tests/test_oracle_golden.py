@@ -79,6 +79,8 @@ def test_em_golden(case):
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FB'], g['init_FB_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['init_TW_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FW'], g['init_FW_%d' % j])
+        if 'init_TB_%d' % j in g:
+            np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TB'], g['init_TB_%d' % j])
     ll = m.estim_param_a_post_model()
     np.testing.assert_array_equal(ll, g['logliks'])
     for j in range(J):
@@ -87,6 +89,8 @@ def test_em_golden(case):
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FB'], g['final_FB_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TW'], g['final_TW_%d' % j])
         np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['FW'], g['final_FW_%d' % j])
+        if 'final_TB_%d' % j in g:
+            np.testing.assert_array_equal(m.spec_comps[j]['factor'][0]['TB'], g['final_TB_%d' % j])
     S = m.separated_images(X)
     assert rel(np.abs(S), np.abs(g['images'])) == 0.0
 
