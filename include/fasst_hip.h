@@ -103,6 +103,21 @@ int fasst_set_blocks(fasst_ctx *ctx, int j, int nblk, const int *kb, const int *
  * lambda = 0 (the default after fasst_configure) switches it off.           */
 int fasst_set_corr(fasst_ctx *ctx, double lambda, int nseq, const int *seq_j, const int *seq_b);
 
+/* Time blobs of component b of source j (H = TW.TB, audioModel.py:486-487;
+ * set through setComponentParameter(..., 'TB', ...), :2082): TW is the
+ * component's factor TW (rows x L, rows = its fasst_set_blocks width), TB the
+ * L x T time blobs, tb_free = TB_frdm_prior == 'free'.  The device keeps both
+ * and writes H into the component's rows of the source's TW (whatever
+ * fasst_set_spectral put there); TW then updates through TB (:1665-1691), TB
+ * by :1931-1978, renormalisation :2029-2033.  L = 0 removes them; call after
+ * fasst_set_blocks (which drops the time blobs of the source it changes).
+ * A restart bit of such a component means sum(TW) < eps: the caller redraws
+ * TW and performs the TB renormalisation (fasst_get_tb's TB is then not yet
+ * divided by its row means).                                                 */
+int fasst_set_tb(fasst_ctx *ctx, int j, int b, int L, const double *TW, const double *TB,
+                 int tb_free);
+int fasst_get_tb(fasst_ctx *ctx, int j, int b, double *TW, double *TB);
+
 /* renormalize_parameters (audioModel.py:1980-2040).  restart_mask bit j (or
  * bit per spectral component, fasst_set_blocks) is set when sum(TW) < eps:
  * the caller draws the restart (host RNG order).                            */

@@ -56,6 +56,9 @@ SIGNATURES = {
     "fasst_set_fw_prior": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "fasst_set_blocks": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _ip, _ip, _ip, _ip]),
     "fasst_set_corr": (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_int, _ip, _ip]),
+    "fasst_set_tb": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp,
+                                    ctypes.c_int]),
+    "fasst_get_tb": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _dp, _dp]),
     "fasst_renormalize": (ctypes.c_int, [_vp, _ip]),
     "fasst_run": (ctypes.c_int, [_vp, ctypes.c_int, _dp, ctypes.c_double, _dp, _ip, _ip]),
     "fasst_wiener_images": (ctypes.c_int, [_vp, _dp, _dp, _dp]),

@@ -173,11 +173,11 @@ class FASST(object):
         the reference's key order (update_spectral_components iterates
         spec_comps.items(), audioModel.py:1479).
 
-        HIP path: stereo; single-factor NMF spectral components (TB empty,
-        TW_constr 'NMF'; FB, FW, TW each free or fixed), one or several per
-        spatial component (comp_spat_comp_power sums them, :469-498); all
-        spatial components 'inst' or all 'conv'; any lambdaCorr >= 0 (the
-        inter-source correlation penalty, :1484-1719).
+        HIP path: stereo; single-factor NMF spectral components (TW_constr
+        'NMF'; FB, FW, TW each free or fixed; time blobs TB, free or fixed, or
+        none), one or several per spatial component (comp_spat_comp_power sums
+        them, :469-498); all spatial components 'inst' or all 'conv'; any
+        lambdaCorr >= 0 (the inter-source correlation penalty, :1484-1719).
         """
         if self.audioObject.channels != 2:
             raise AttributeError("Nb channels " + str(self.audioObject.channels) +
@@ -194,7 +194,11 @@ class FASST(object):
                 raise NotImplementedError("multi-factor spectral components are outside the HIP path")
             fac = facs[0]
             if len(fac['TB']):
-                raise NotImplementedError("time blobs (TB) are outside the HIP path")
+                TB = np.asarray(fac['TB'])
+                if TB.ndim != 2 or TB.shape[1] != self.nbFramesSigRepr or \
+                        np.shape(fac['TW']) != (fac['FB'].shape[1], TB.shape[0]):
+                    raise ValueError("time blobs of spectral component %d: TW %s, TB %s"
+                                     % (k, np.shape(fac['TW']), TB.shape))
             if fac.get('TW_constr', 'NMF') != 'NMF':
                 raise NotImplementedError("TW_constr=%s is outside the HIP path" % fac['TW_constr'])
         if sorted(owner.keys()) != list(range(J)):
@@ -225,11 +229,14 @@ class FASST(object):
             fb_free = [f.get('FB_frdm_prior', 'free') == 'free' for f in facs]
             fw_free = [f.get('FW_frdm_prior', 'fixed') == 'free' for f in facs]
             tw_free = [f.get('TW_frdm_prior', 'free') == 'free' for f in facs]
+            # a component with time blobs: the device forms H = TW.TB (fasst_set_tb)
+            TWs = [np.zeros((f['FB'].shape[1], self.nbFramesSigRepr)) if len(f['TB'])
+                   else f['TW'] for f in facs]
             if len(facs) == 1:
-                FB, FW, TW = facs[0]['FB'], facs[0]['FW'], facs[0]['TW']
+                FB, FW, TW = facs[0]['FB'], facs[0]['FW'], TWs[0]
             else:   # the components side by side, FW block diagonal
                 FB = np.hstack([f['FB'] for f in facs])
-                TW = np.vstack([f['TW'] for f in facs])
+                TW = np.vstack(TWs)
                 FW = np.zeros((Ks[j], Ks[j]))
                 a = 0
                 for f in facs:
@@ -239,6 +246,9 @@ class FASST(object):
             eng.set_spectral(j, FB, FW, TW, any(fb_free), any(tw_free), any(fw_free))
             eng.set_blocks(j, np.cumsum([0] + [f['FB'].shape[1] for f in facs]), fb_free, fw_free,
                            tw_free)
+            for b, f in enumerate(facs):
+                if len(f['TB']):
+                    eng.set_tb(j, b, f['TW'], f['TB'], f.get('TB_frdm_prior') == 'free')
         if self.lambdaCorr > 0:   # components one at a time in key order (:1479)
             pos = {k: (j, b) for j, keys in enumerate(order) for b, k in enumerate(keys)}
             seq = [pos[k] for k in sorted(self.spec_comps.keys())]
@@ -258,11 +268,14 @@ class FASST(object):
             sc['params'] = p
             FB, FW, TW = eng.get_spectral(j, Ks[j])
             a = 0
-            for k in order[j]:
+            for b, k in enumerate(order[j]):
                 fac = self.spec_comps[k]['factor'][0]
                 n = fac['FB'].shape[1]
                 parts = (('FB', FB[:, a:a + n]), ('FW', FW[a:a + n, a:a + n]),
                          ('TW', TW[a:a + n]))
+                if len(fac['TB']):   # the factor TW and TB, not H
+                    TWs, TB = eng.get_tb(j, b, n, np.shape(fac['TB'])[0])
+                    parts = parts[:2] + (('TW', TWs), ('TB', TB))
                 if len(order[j]) > 1:
                     parts = tuple((key, np.ascontiguousarray(val)) for key, val in parts)
                 for key, val in parts:
@@ -291,6 +304,11 @@ class FASST(object):
                 fac['TW'] *= 1e3 * eps
                 if self.verbose:
                     print("    renorm: reinitialized TW for spec", k, "factor", 0)
+                if len(fac['TB']):   # the rest of the renormalisation (:2029-2033)
+                    w = fac['TB'].mean(axis=1)
+                    w[w == 0] = 1.
+                    fac['TB'] /= np.vstack(w)
+                    fac['TW'] *= w
 
     # ---------------------------------------------------------------- EM
     def _annealed_psd(self, i):

@@ -20,6 +20,7 @@ constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge
 // are cut into <= kMaxBlk blocks (one per spectral component); the blocks of
 // all sources (the "slots") carry the TW restart flags
 constexpr int kMaxBlk = 8, kMaxSlot = 16;
+constexpr int kMaxTB = 64;  // time blobs per spectral component
 constexpr int kFlagHalt = 1 + kMaxSlot, kFlagIter = 2 + kMaxSlot, kNFlags = 3 + kMaxSlot;
 #ifndef FASST_FPW
 #define FASST_FPW 2

@@ -46,8 +46,17 @@ struct fasst_ctx {
   int soff[fasst::kMaxJ + 1] = {0}, nslot = 0, maxblk = 0, multi = 0;
   int bfb[fasst::kMaxJ][fasst::kMaxBlk] = {{0}}, btw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
   int bfw[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
+  // time blobs (fasst_set_tb): block b of source j with tbl[j][b] = L > 0 has
+  // H = TW.TB; its factor TW (block rows x L) and TB (L x Tp) live in
+  // tb[j][b] (layout tb_layout in fasst_em.hip) and the block's rows of TW
+  // hold H; btb[j][b]: TB free.  Any time blob routes through the multi path
+  fasst::DBuf<double> tb[fasst::kMaxJ][fasst::kMaxBlk];
+  int tbl[fasst::kMaxJ][fasst::kMaxBlk] = {{0}}, btb[fasst::kMaxJ][fasst::kMaxBlk] = {{0}};
+  int anytb = 0;
   fasst::DBuf<double> FB, FW, TW, Wkf, Wkf_new, Wfk_new, FWHt, hatW;
-  fasst::DBuf<double> mplanes, bden;  // multi-block update: ratio planes [5][J][Tp][Fp], FB den
+  // multi-block update: ratio planes [6][J][Tp][Fp] (rnum, rden, rho_c, corrPen,
+  // powers, and with time blobs max(V_c, eps)), FB den
+  fasst::DBuf<double> mplanes, bden;
   // lambdaCorr > 0 (fasst_set_corr): the components go one at a time in the
   // reference's key order (seq_j[q], seq_b[q]) through the multi-block path
   double lambda = 0.0;

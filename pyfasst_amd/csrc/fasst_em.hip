@@ -1409,6 +1409,7 @@ struct TArgs {
   int tw_free[kMaxJ];
   int kb0[kMaxJ], kb1[kMaxJ];  // BLK: the V tiles sum the columns [kb0, kb1) only
   const double *cp, *pw;       // LAM: corrPen / powers planes of k_multi_prep
+  const double *oth;           // TBQ: max(V_c, eps) plane of k_multi_prep
   const int *halt;
 };
 
@@ -1423,7 +1424,10 @@ struct TArgs {
 // BLK (one of several spectral components on source j): V_old / V_new are the
 // component's own powers W_c H_c (the reference's spec_comp_ind=[k],
 // audioModel.py:1639-1645), and rho is the plane hat_W_j / max(V_c_old, eps).
-template <int NKC, int TPW, bool BLK = false, bool LAM = false>
+// TBQ (the TB step of a component with time blobs, :1931-1978): H has moved
+// since the step's start, so other = max(V_c_old, eps) comes from a plane,
+// hatW is hat_W_j itself, and num's ratio is hat_W / max(V_new^2, eps).
+template <int NKC, int TPW, bool BLK = false, bool LAM = false, bool TBQ = false>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
@@ -1453,7 +1457,7 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
     double ao[NKS], an[NKS], bw[4][NKC];
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
-      ao[s] = wo[(size_t)(4 * s) * a.Fp + f0];
+      ao[s] = TBQ ? 0.0 : wo[(size_t)(4 * s) * a.Fp + f0];
       an[s] = wn[(size_t)(4 * s) * a.Fp + f0];
       if constexpr (BLK) {
         const int k = tq + 4 * s;
@@ -1475,9 +1479,11 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
-        vo = mfma4(ao[s], bt[p][s], vo);
+        if constexpr (!TBQ) {
+          vo = mfma4(ao[s], bt[p][s], vo);
+          vo2 = mfma4(ao[s + 1], bt[p][s + 1], vo2);
+        }
         vn = mfma4(an[s], bt[p][s], vn);
-        vo2 = mfma4(ao[s + 1], bt[p][s + 1], vo2);
         vn2 = mfma4(an[s + 1], bt[p][s + 1], vn2);
       }
       vo += vo2;
@@ -1486,18 +1492,24 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       double r3[4], r4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const double other = fmax(vo[i], kEps);
         const double vm = fmax(vn[i], kEps);
         const double rv = rcp_nr(vm);
         const bool ok = tok && f0 + tq + 4 * i < a.F;
-        const double hw = h[i] * other;  // hat_W from the E-step's rho
+        const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + tq + 4 * i;
+        double other, q;
+        if constexpr (TBQ) {
+          other = ok ? a.oth[o] : 0.0;
+          q = h[i] / fmax(vm * vm, kEps);   // hat_W / max(V^2, eps) (:1971-1973)
+        } else {
+          other = fmax(vo[i], kEps);
+          q = (h[i] * other) * (rv * rv);   // hat_W from the E-step's rho
+        }
         if constexpr (LAM) {   // corrPen terms (audioModel.py:1650-1719)
-          const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + tq + 4 * i;
           const double cp = ok ? a.cp[o] : 0.0, pw = ok ? a.pw[o] : 1.0;
-          r3[i] = ok ? other * (hw * (rv * rv) + cp * (2.0 * (vm / pw))) : 0.0;
+          r3[i] = ok ? other * (q + cp * (2.0 * (vm / pw))) : 0.0;
           r4[i] = ok ? other * (rv + cp) : 0.0;
         } else {
-          r3[i] = ok ? other * (hw * (rv * rv)) : 0.0;
+          r3[i] = ok ? other * q : 0.0;
           r4[i] = ok ? other * rv : 0.0;
         }
       }
@@ -1587,6 +1599,7 @@ struct MPArgs {
   const double *TW, *Wkf;
   double *hatW, *rnum, *rden, *rtw;   // planes [J][Tp][Fp]
   double *rcp, *rpow;                 // LAM: corrPen and max(sum_j V_j, eps) planes
+  double *roth;                       // time blobs: max(V_c, eps) at the step's start
   double lambda;
   int F, T, Fp, Tp, KP, J, ntt, tpc, first;
   int on[kMaxJ], kb0[kMaxJ], kb1[kMaxJ];
@@ -1651,6 +1664,7 @@ __global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
       if (t >= a.T || f >= a.F) {
         a.rnum[o] = a.rden[o] = a.rtw[o] = 0.0;
         if constexpr (LAM) a.rcp[o] = a.rpow[o] = 0.0;
+        if (a.roth) a.roth[o] = 0.0;
         continue;
       }
       const double sj = fmax(vj[i], kEps), sc = fmax(vc[i], kEps);
@@ -1674,6 +1688,7 @@ __global__ __launch_bounds__(64) void k_multi_prep(const MPArgs a) {
         a.rden[o] = sc * (1.0 / sj);
       }
       a.rtw[o] = hw / sc;
+      if (a.roth) a.roth[o] = sc;
     }
   }
 }
@@ -1692,6 +1707,7 @@ struct RArgs {
   // spectral components of source j (column blocks of FB / FW / TW) and the
   // slot of block 0
   int nblk[kMaxJ], kb[kMaxJ][kMaxBlk + 1], soff[kMaxJ + 1];
+  unsigned tbmask;   // slots with time blobs: their restart test is k_tb_renorm's
   const int *halt;
 };
 
@@ -1881,7 +1897,7 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
   }
   __syncthreads();
   const int sl = threadIdx.x;   // one TW restart test per spectral component
-  if (sl >= a.nslot) return;
+  if (sl >= a.nslot || (a.tbmask >> sl & 1u)) return;
   double s = 0.0;
   for (int c = 0; c < a.nchunk; ++c) s += a.tpart[(size_t)sl * a.nchunk + c];
   const int dead = s < kEps ? 1 : 0;
@@ -1890,6 +1906,210 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
     a.flags[kFlagHalt] = 1;
     a.flags[kFlagIter] = iter;
   }
+}
+
+// ---------------------------------------------------------------- time blobs
+// A spectral component with time blobs (TB, audioModel.py:430-498) has
+// H = TW TB.  Its factor TW ("TWs", block rows x L) and TB (L x T) live in the
+// slot buffer tb[j][b] (tb_layout) and the block's rows of the model TW hold
+// H, so every other kernel (E-step, FB / FW / TW contractions, Wiener) reads
+// H unchanged.  Both updates reuse the block's TW contraction, which leaves
+// G = W^T R over f per frame in tnum / tden (W = FB FW of the block):
+//   TW step (:1665-1691): num = G TB^T, den likewise        (k_tb_tw_red)
+//   TB step (:1931-1978): num = TWs^T G, with R's ratio hat_W / max(V^2, eps)
+//                         (k_tw_contract<TBQ>, then k_tb_tb_upd)
+// the reference's (W TWs)^T R reassociated; H is rebuilt after each (k_tb_h).
+struct TBLayout {
+  size_t tws, tb, num, den, n;   // offsets (doubles) in the slot buffer, total
+};
+__host__ __device__ inline TBLayout tb_layout(int kbw, int L, int Tp) {
+  TBLayout o;
+  o.tws = 0;
+  o.tb = (size_t)kbw * L;
+  o.num = o.tb + (size_t)L * Tp;
+  o.den = o.num + (size_t)kbw * L;
+  o.n = o.den + (size_t)kbw * L;
+  return o;
+}
+
+struct TBArgs {
+  double *tb[kMaxJ];   // the step's slot buffer per source (null: no time blobs)
+  int L[kMaxJ], kb0[kMaxJ], kbw[kMaxJ];
+  double *TW;
+  const double *tnum, *tden;   // [nsplit][J][Tp][KP] of k_tw_contract
+  int T, Tp, KP, J, nsplit;
+  double omega;
+  // iter >= 0 (renormalisation): a halt raised in this same iteration does not
+  // stop the kernel (the host reads a consistent TWs / TB), an earlier one does
+  const int *flags;
+  int iter;
+  const int *halt;
+};
+
+__device__ inline bool tb_halted(const int *halt, const int *flags, int iter) {
+  if (!halt || !*(volatile const int *)halt) return false;
+  return iter < 0 || *(volatile const int *)(flags + kFlagIter) < iter;
+}
+
+// TW step: num[k][l] = sum_t G_num[t][k] TB[l][t] (chunks summed first), one
+// block per (blob, 16 rows, source)
+__global__ __launch_bounds__(256) void k_tb_tw_red(const TBArgs a) {
+  if (tb_halted(a.halt, a.flags, a.iter)) return;
+  __shared__ double s_red[256];
+  const int l = blockIdx.x, k0 = blockIdx.y * 16, j = blockIdx.z;
+  if (!a.tb[j] || l >= a.L[j] || k0 >= a.kbw[j]) return;
+  const int L = a.L[j], kbw = a.kbw[j], nk = min(16, kbw - k0);
+  const TBLayout o = tb_layout(kbw, L, a.Tp);
+  const double *TB = a.tb[j] + o.tb + (size_t)l * a.Tp;
+  double num[16], den[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) num[i] = den[i] = 0.0;
+  for (int t = threadIdx.x; t < a.T; t += blockDim.x) {
+    const double bl = TB[t];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i < nk) {
+        double sn = 0.0, sd = 0.0;
+        for (int c = 0; c < a.nsplit; ++c) {
+          const size_t q = (((size_t)c * a.J + j) * a.Tp + t) * a.KP + a.kb0[j] + k0 + i;
+          sn += a.tnum[q];
+          sd += a.tden[q];
+        }
+        num[i] += sn * bl;
+        den[i] += sd * bl;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i < nk) {
+      const double rn = block_sum(num[i], s_red), rd = block_sum(den[i], s_red);
+      if (threadIdx.x == 0) {
+        a.tb[j][o.num + (size_t)(k0 + i) * L + l] = rn;
+        a.tb[j][o.den + (size_t)(k0 + i) * L + l] = rd;
+      }
+    }
+  }
+}
+
+// TWs *= (num / max(den, eps))^omega   (:1718-1726)
+__global__ __launch_bounds__(256) void k_tb_tw_apply(const TBArgs a) {
+  if (tb_halted(a.halt, a.flags, a.iter)) return;
+  const int j = blockIdx.x;
+  if (!a.tb[j]) return;
+  const TBLayout o = tb_layout(a.kbw[j], a.L[j], a.Tp);
+  double *p = a.tb[j];
+  for (int i = threadIdx.x; i < a.kbw[j] * a.L[j]; i += blockDim.x) {
+    const double r = p[o.num + i] / fmax(p[o.den + i], kEps);
+    p[o.tws + i] *= a.omega == 1.0 ? r : pow(r, a.omega);
+  }
+}
+
+// TB step: num[l][t] = sum_k TWs[k][l] G_num[t][k], TB *= (num / max(den,
+// eps))^omega (:1974-1977); 64 frames per block, accumulators in LDS
+__global__ __launch_bounds__(64) void k_tb_tb_upd(const TBArgs a) {
+  if (tb_halted(a.halt, a.flags, a.iter)) return;
+  extern __shared__ double s_tb[];
+  const int j = blockIdx.y;
+  if (!a.tb[j]) return;
+  const int L = a.L[j], kbw = a.kbw[j], tid = threadIdx.x;
+  const TBLayout o = tb_layout(kbw, L, a.Tp);
+  double *s_tw = s_tb, *s_num = s_tb + kbw * L, *s_den = s_num + 64 * L;
+  for (int i = tid; i < kbw * L; i += 64) s_tw[i] = a.tb[j][o.tws + i];
+  for (int l = 0; l < L; ++l) s_num[l * 64 + tid] = s_den[l * 64 + tid] = 0.0;
+  __syncthreads();
+  const int t = blockIdx.x * 64 + tid;
+  if (t >= a.T) return;
+  for (int k = 0; k < kbw; ++k) {
+    double sn = 0.0, sd = 0.0;
+    for (int c = 0; c < a.nsplit; ++c) {
+      const size_t q = (((size_t)c * a.J + j) * a.Tp + t) * a.KP + a.kb0[j] + k;
+      sn += a.tnum[q];
+      sd += a.tden[q];
+    }
+    for (int l = 0; l < L; ++l) {
+      const double w = s_tw[k * L + l];
+      s_num[l * 64 + tid] += w * sn;
+      s_den[l * 64 + tid] += w * sd;
+    }
+  }
+  double *TB = a.tb[j] + o.tb;
+  for (int l = 0; l < L; ++l) {
+    const double r = s_num[l * 64 + tid] / fmax(s_den[l * 64 + tid], kEps);
+    TB[(size_t)l * a.Tp + t] *= a.omega == 1.0 ? r : pow(r, a.omega);
+  }
+}
+
+// H = TWs TB into the block's rows of TW (padding frames stay zero)
+__global__ __launch_bounds__(256) void k_tb_h(const TBArgs a) {
+  if (tb_halted(a.halt, a.flags, a.iter)) return;
+  extern __shared__ double s_tw[];
+  const int j = blockIdx.y;
+  if (!a.tb[j]) return;
+  const int L = a.L[j], kbw = a.kbw[j];
+  const TBLayout o = tb_layout(kbw, L, a.Tp);
+  for (int i = threadIdx.x; i < kbw * L; i += blockDim.x) s_tw[i] = a.tb[j][o.tws + i];
+  __syncthreads();
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.Tp) return;
+  const double *TB = a.tb[j] + o.tb;
+  for (int k = 0; k < kbw; ++k) {
+    double h = 0.0;
+    for (int l = 0; l < L; ++l) h += s_tw[k * L + l] * TB[(size_t)l * a.Tp + t];
+    a.TW[((size_t)j * a.KP + a.kb0[j] + k) * a.Tp + t] = t < a.T ? h : 0.0;
+  }
+}
+
+// renormalize_parameters for a component with time blobs (:2019-2033), after
+// k_renorm_final: TWs *= w (the FW column means, as the block's H rows got in
+// k_renorm_apply), the restart test on sum(TWs), then TB /= m, TWs *= m with
+// m = TB.mean(axis=1).  A dead component is left to the host (redraw, then
+// the TB step of the renormalisation), one block per (component, source).
+struct TBRArgs {
+  double *tb[kMaxJ][kMaxBlk];
+  int L[kMaxJ][kMaxBlk], kb0[kMaxJ][kMaxBlk], kbw[kMaxJ][kMaxBlk], slot[kMaxJ][kMaxBlk];
+  const double *scal;   // RArgs::scal: w2 = FW column means at [j][2 + KP + k]
+  int *flags;
+  const int *halt;
+  int T, Tp, KP, iter;
+};
+__global__ __launch_bounds__(256) void k_tb_renorm(const TBRArgs a) {
+  if (tb_halted(a.halt, a.flags, a.iter)) return;
+  __shared__ double s_red[256];
+  __shared__ double s_m[kMaxTB];
+  const int b = blockIdx.x, j = blockIdx.y;
+  double *p = a.tb[j][b];
+  if (!p) return;
+  const int L = a.L[j][b], kbw = a.kbw[j][b], n = kbw * L;
+  const TBLayout o = tb_layout(kbw, L, a.Tp);
+  const double *w2 = a.scal + (size_t)j * (2 + 2 * a.KP) + 2 + a.KP + a.kb0[j][b];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double y = p[o.tws + i] * w2[i / L];
+    p[o.tws + i] = y;
+    s += y;
+  }
+  s = block_sum(s, s_red);
+  const int dead = s < kEps ? 1 : 0;
+  if (threadIdx.x == 0) {
+    a.flags[1 + a.slot[j][b]] = dead;
+    if (dead) {
+      a.flags[kFlagHalt] = 1;
+      a.flags[kFlagIter] = a.iter;
+    }
+  }
+  if (dead) return;
+  double *TB = p + o.tb;
+  for (int l = 0; l < L; ++l) {
+    double m = 0.0;
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x) m += TB[(size_t)l * a.Tp + t];
+    m = block_sum(m, s_red) / (double)a.T;
+    if (m == 0.0) m = 1.0;
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x) TB[(size_t)l * a.Tp + t] /= m;
+    if (threadIdx.x == 0) s_m[l] = m;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) p[o.tws + i] *= s_m[i % L];
 }
 
 // ---------------------------------------------------------------- host side
@@ -1991,6 +2211,12 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   c->soff[J] = c->nslot = J;
   c->maxblk = 1;
   c->multi = 0;
+  for (int j = 0; j < kMaxJ; ++j)
+    for (int b = 0; b < kMaxBlk; ++b) {
+      c->tb[j][b].release();
+      c->tbl[j][b] = c->btb[j][b] = 0;
+    }
+  c->anytb = 0;
   c->nsrc = 0;
   c->lambda = 0.0;
   c->nseq = 0;
@@ -2092,6 +2318,62 @@ int launch_w_old(fasst_ctx *c) {
   return FASST_OK;
 }
 
+static void update_multi(fasst_ctx *c) {
+  c->anytb = 0;
+  for (int j = 0; j < c->J; ++j)
+    for (int b = 0; b < c->nblk[j]; ++b) c->anytb |= c->tbl[j][b] > 0;
+  c->multi = c->maxblk > 1 || c->lambda > 0.0 || c->anytb;
+}
+
+// Time-blob arguments of step b (only_j as multi_step); which = 0: every
+// block with time blobs, 1: those whose TW is free, 2: those whose TB is free
+static TBArgs tb_args(const fasst_ctx *c, int b, int only_j, int which, double omega) {
+  TBArgs a;
+  for (int j = 0; j < kMaxJ; ++j) {
+    bool on = j < c->J && b < c->nblk[j] && c->tbl[j][b] > 0 && (only_j < 0 || j == only_j);
+    if (on && which == 1) on = c->btw[j][b] != 0;
+    if (on && which == 2) on = c->btb[j][b] != 0;
+    a.tb[j] = on ? c->tb[j][b].p : nullptr;
+    a.L[j] = on ? c->tbl[j][b] : 0;
+    a.kb0[j] = on ? c->kb[j][b] : 0;
+    a.kbw[j] = on ? c->kb[j][b + 1] - c->kb[j][b] : 0;
+  }
+  a.TW = c->TW.p;
+  a.tnum = c->tnum.p;
+  a.tden = c->tden.p;
+  a.T = c->T;
+  a.Tp = c->Tp;
+  a.KP = c->KP;
+  a.J = c->J;
+  a.nsplit = c->nsplit_t;
+  a.omega = omega;
+  a.flags = nullptr;
+  a.iter = -1;
+  a.halt = c->halt;
+  return a;
+}
+
+static bool tb_any(const TBArgs &a, int *lmax, int *kwmax) {
+  bool any = false;
+  *lmax = *kwmax = 0;
+  for (int j = 0; j < kMaxJ; ++j)
+    if (a.tb[j]) {
+      any = true;
+      *lmax = std::max(*lmax, a.L[j]);
+      *kwmax = std::max(*kwmax, a.kbw[j]);
+    }
+  return any;
+}
+
+static int launch_tb_h(fasst_ctx *c, const TBArgs &a) {
+  int lmax, kwmax;
+  if (!tb_any(a, &lmax, &kwmax)) return FASST_OK;
+  k_tb_h<<<dim3((c->Tp + 255) / 256, c->J), 256, (size_t)kwmax * lmax * sizeof(double),
+           c->stream>>>(a);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
 static int launch_renorm(fasst_ctx *c, int iter) {
   RArgs r;
   r.A = c->A.p;
@@ -2115,6 +2397,10 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   r.tpc = (c->T + c->nchunk_r - 1) / c->nchunk_r;
   r.fpc = (c->F + c->nchunk_r - 1) / c->nchunk_r;
   r.nslot = c->nslot;
+  r.tbmask = 0;
+  for (int j = 0; j < c->J; ++j)
+    for (int b = 0; b < c->nblk[j]; ++b)
+      if (c->tbl[j][b] > 0) r.tbmask |= 1u << (c->soff[j] + b);
   for (int j = 0; j < kMaxJ; ++j) {
     r.K[j] = j < c->J ? c->K[j] : 0;
     r.nblk[j] = j < c->J ? c->nblk[j] : 0;
@@ -2128,8 +2414,35 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   k_renorm_stats<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
   k_renorm_apply<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
   k_renorm_final<<<1, 256, 0, c->stream>>>(r, c->J, iter);
-  prof_end(c, KREN);
   FASST_LAUNCH_CHECK();
+  if (c->anytb) {
+    TBRArgs tr;
+    tr.scal = c->rscal.p;
+    tr.flags = c->flags.p;
+    tr.halt = c->halt;
+    tr.T = c->T;
+    tr.Tp = c->Tp;
+    tr.KP = c->KP;
+    tr.iter = iter;
+    for (int j = 0; j < kMaxJ; ++j)
+      for (int b = 0; b < kMaxBlk; ++b) {
+        const bool on = j < c->J && b < c->nblk[j] && c->tbl[j][b] > 0;
+        tr.tb[j][b] = on ? c->tb[j][b].p : nullptr;
+        tr.L[j][b] = on ? c->tbl[j][b] : 0;
+        tr.kb0[j][b] = on ? c->kb[j][b] : 0;
+        tr.kbw[j][b] = on ? c->kb[j][b + 1] - c->kb[j][b] : 0;
+        tr.slot[j][b] = on ? c->soff[j] + b : 0;
+      }
+    k_tb_renorm<<<dim3(kMaxBlk, c->J), 256, 0, c->stream>>>(tr);
+    FASST_LAUNCH_CHECK();
+    for (int b = 0; b < c->maxblk; ++b) {
+      TBArgs ta = tb_args(c, b, -1, 0, 1.0);
+      ta.flags = c->flags.p;
+      ta.iter = iter;
+      if (int st = launch_tb_h(c, ta)) return st;
+    }
+  }
+  prof_end(c, KREN);
   return FASST_OK;
 }
 
@@ -2303,6 +2616,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     mp.rtw = c->mplanes.p + 2 * plane;
     mp.rcp = c->mplanes.p + 3 * plane;
     mp.rpow = c->mplanes.p + 4 * plane;
+    mp.roth = nullptr;
     mp.lambda = c->lambda;
     mp.F = c->F;
     mp.T = c->T;
@@ -2379,6 +2693,11 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     tu.omega = omega;
     t.cp = mp.rcp;
     t.pw = mp.rpow;
+    t.oth = nullptr;
+    const TBArgs tbw = tb_args(c, b, only_j, 1, omega), tbb = tb_args(c, b, only_j, 2, omega);
+    int lmax, kwmax;
+    const bool any_tbb = tb_any(tbb, &lmax, &kwmax);
+    if (any_tbb) mp.roth = c->mplanes.p + 5 * plane;
     for (int j = 0; j < kMaxJ; ++j) {
       const bool has = j < J && b < c->nblk[j] && (only_j < 0 || j == only_j);
       mp.on[j] = has;
@@ -2386,7 +2705,8 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
       mp.kb0[j] = u.kb0[j] = t.kb0[j] = tu.kb0[j] = k0;
       mp.kb1[j] = u.kb1[j] = t.kb1[j] = tu.kb1[j] = k1;
       bb.fb_free[j] = u.fb_free[j] = has && c->bfb[j][b];
-      t.tw_free[j] = tu.tw_free[j] = has && c->btw[j][b];
+      t.tw_free[j] = has && c->btw[j][b];
+      tu.tw_free[j] = t.tw_free[j] && !tbw.tb[j];   // time blobs: k_tb_tw_red / apply
     }
     const dim3 gp(c->nft, J, c->nchunk_b);
     const dim3 gb((c->nft + kFPW - 1) / kFPW, J, c->nchunk_b);
@@ -2491,6 +2811,36 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     FASST_LAUNCH_CHECK();
     k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
     FASST_LAUNCH_CHECK();
+    if (tb_any(tbw, &lmax, &kwmax)) {   // TW with time blobs (:1665-1691)
+      k_tb_tw_red<<<dim3(lmax, (kwmax + 15) / 16, J), 256, 0, c->stream>>>(tbw);
+      k_tb_tw_apply<<<J, 256, 0, c->stream>>>(tbw);
+      FASST_LAUNCH_CHECK();
+      if (int st = launch_tb_h(c, tbw)) return st;
+    }
+    if (tb_any(tbb, &lmax, &kwmax)) {   // TB (:1931-1978) with the updated H
+      TArgs t2 = t;
+      t2.hatW = c->hatW.p;
+      t2.oth = mp.roth;
+      for (int j = 0; j < kMaxJ; ++j) t2.tw_free[j] = tbb.tb[j] != nullptr;
+      switch (nkc) {
+        case 1:
+          if (lam) k_tw_contract<1, kTPW, true, true, true><<<gt, 64, 0, c->stream>>>(t2);
+          else k_tw_contract<1, kTPW, true, false, true><<<gt, 64, 0, c->stream>>>(t2);
+          break;
+        case 2:
+          if (lam) k_tw_contract<2, kTPW, true, true, true><<<gt, 64, 0, c->stream>>>(t2);
+          else k_tw_contract<2, kTPW, true, false, true><<<gt, 64, 0, c->stream>>>(t2);
+          break;
+        default:
+          if (lam) k_tw_contract<4, kTPW, true, true, true><<<gt, 64, 0, c->stream>>>(t2);
+          else k_tw_contract<4, kTPW, true, false, true><<<gt, 64, 0, c->stream>>>(t2);
+          break;
+      }
+      k_tb_tb_upd<<<dim3((c->T + 63) / 64, J), 64,
+                    (size_t)(kwmax * lmax + 2 * 64 * lmax) * sizeof(double), c->stream>>>(tbb);
+      FASST_LAUNCH_CHECK();
+      if (int st = launch_tb_h(c, tbb)) return st;
+    }
     // the step's W = FB FW is the current W of the next step
     FASST_HIP(hipMemcpyAsync(c->Wkf.p, c->Wkf_new.p, (size_t)J * c->KP * c->Fp * sizeof(double),
                              hipMemcpyDeviceToDevice, c->stream));
@@ -3051,7 +3401,11 @@ int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb
   for (int i = 0; i < c->J; ++i) c->soff[i + 1] = c->soff[i] + c->nblk[i];
   c->nslot = nslot;
   c->maxblk = maxblk;
-  c->multi = maxblk > 1 || c->lambda > 0.0;
+  for (int b = 0; b < kMaxBlk; ++b) {   // the blocks moved: their time blobs go
+    c->tb[j][b].release();
+    c->tbl[j][b] = c->btb[j][b] = 0;
+  }
+  update_multi(c);
   return FASST_OK;
 }
 
@@ -3085,7 +3439,65 @@ int fasst_set_corr(fasst_ctx *c, double lambda, int nseq, const int *seq_j, cons
   }
   c->lambda = lambda;
   c->nseq = lambda > 0.0 ? nseq : 0;
-  c->multi = c->maxblk > 1 || lambda > 0.0;
+  update_multi(c);
+  return FASST_OK;
+}
+
+int fasst_set_tb(fasst_ctx *c, int j, int b, int L, const double *TW, const double *TB,
+                 int tb_free) {
+  int st = need_model(c, j);
+  if (st) return st;
+  if (b < 0 || b >= c->nblk[j] || L < 0 || L > kMaxTB || (L > 0 && (!TW || !TB))) {
+    set_error("fasst_set_tb: source %d component %d with %d time blobs (1..%d)", j, b, L, kMaxTB);
+    return L > kMaxTB ? FASST_ERR_UNSUPPORTED : FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(c->device);
+  if (L == 0) {
+    c->tb[j][b].release();
+    c->tbl[j][b] = c->btb[j][b] = 0;
+    update_multi(c);
+    return FASST_OK;
+  }
+  const int kbw = c->kb[j][b + 1] - c->kb[j][b];
+  const TBLayout o = tb_layout(kbw, L, c->Tp);
+  const size_t plane = (size_t)c->J * c->Tp * c->Fp;
+  if (c->mplanes.n < 6 * plane && (st = c->mplanes.alloc(6 * plane))) return st;
+  const size_t nb = (size_t)c->nchunk_b * c->J * c->Fp * c->KP;
+  if (c->bden.n < nb && (st = c->bden.alloc(nb))) return st;
+  if ((st = c->tb[j][b].alloc(o.n))) return st;   // zero-filled: TB's padding frames stay 0
+  FASST_HIP(hipMemcpyAsync(c->tb[j][b].p + o.tws, TW, (size_t)kbw * L * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemcpy2DAsync(c->tb[j][b].p + o.tb, c->Tp * sizeof(double), TB,
+                             c->T * sizeof(double), c->T * sizeof(double), L,
+                             hipMemcpyHostToDevice, c->stream));
+  c->tbl[j][b] = L;
+  c->btb[j][b] = tb_free ? 1 : 0;
+  update_multi(c);
+  c->halt = nullptr;
+  TBArgs a = tb_args(c, b, j, 0, 1.0);   // H = TW TB into the block's rows
+  if ((st = launch_tb_h(c, a))) return st;
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_get_tb(fasst_ctx *c, int j, int b, double *TW, double *TB) {
+  int st = need_model(c, j);
+  if (st) return st;
+  if (b < 0 || b >= c->nblk[j] || c->tbl[j][b] == 0) {
+    set_error("fasst_get_tb: source %d component %d has no time blobs", j, b);
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(c->device);
+  const int kbw = c->kb[j][b + 1] - c->kb[j][b], L = c->tbl[j][b];
+  const TBLayout o = tb_layout(kbw, L, c->Tp);
+  if (TW)
+    FASST_HIP(hipMemcpyAsync(TW, c->tb[j][b].p + o.tws, (size_t)kbw * L * sizeof(double),
+                             hipMemcpyDeviceToHost, c->stream));
+  if (TB)
+    FASST_HIP(hipMemcpy2DAsync(TB, c->T * sizeof(double), c->tb[j][b].p + o.tb,
+                               c->Tp * sizeof(double), c->T * sizeof(double), L,
+                               hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
 }
 

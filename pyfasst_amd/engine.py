@@ -108,6 +108,25 @@ class Engine(object):
         check(lib.fasst_set_corr(self._h, float(lam), len(seq_j), iptr(sj), iptr(sb)),
               "fasst_set_corr")
 
+    def set_tb(self, j, b, TW=None, TB=None, tb_free=True):
+        """Time blobs of component b of source j (fasst_set_tb): TW = the
+        component's factor TW (rows x L), TB = L x T; TB None removes them."""
+        if TB is None:
+            check(lib.fasst_set_tb(self._h, int(j), int(b), 0, None, None, 0), "fasst_set_tb")
+            return
+        TW = np.ascontiguousarray(TW, dtype=np.float64)
+        TB = np.ascontiguousarray(TB, dtype=np.float64)
+        if TB.ndim != 2 or TB.shape[1] != self.T or TW.ndim != 2 or TW.shape[1] != TB.shape[0]:
+            raise ValueError("time blobs: TW %s, TB %s (T = %d)" % (TW.shape, TB.shape, self.T))
+        check(lib.fasst_set_tb(self._h, int(j), int(b), TB.shape[0], dptr(TW), dptr(TB),
+                               int(bool(tb_free))), "fasst_set_tb")
+
+    def get_tb(self, j, b, rows, L):
+        TW = np.empty((rows, L))
+        TB = np.empty((L, self.T))
+        check(lib.fasst_get_tb(self._h, int(j), int(b), dptr(TW), dptr(TB)), "fasst_get_tb")
+        return TW, TB
+
     def get_spectral(self, j, K):
         FB = np.empty((self.F, K))
         FW = np.empty((K, K))
