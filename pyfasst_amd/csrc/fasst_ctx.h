@@ -72,6 +72,8 @@ struct fasst_ctx {
   int nsplit_t = 1, fpc_t = 1;  // TW contraction bin chunks
   int eb_split = 1;             // E-step / FB numerator interleaved over frame ranges
   int nce_run = 1, ncb_run = 1; // partial-sum chunks the current iteration wrote
+  int tw_fused = 1;             // TW update applied in the TW contraction's last arrivers
+  fasst::DBuf<int> tcnt;        // their arrival counters [J][TW contraction x blocks]
   fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rpmax, rpe, rtpart;
   fasst::DBuf<double> gden, TWt, pnum, pden;  // FW update (free FW)
   int nchunk_r = 1;

@@ -877,19 +877,44 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   __shared__ double2 s_H[kMaxR][kMaxR];
   __shared__ double2 s_mult[kMaxR];
   __shared__ double s_sv[kMaxJ];
+  __shared__ double s_wh[2][kMaxJ * kMaxKP];   // W_j(f, k), sum_t TW_j(k, t)
   const int f = blockIdx.x, lane = threadIdx.x;
   const int J = a.J, R = a.R, NACC = a.nacc;
   const int NP = J * (J + 1) / 2;
-  for (int u = lane; u < NACC; u += 64) {  // NACC = 72 > 64 lanes for J = 4
-    double x = 0.0;
-    x = chunk_sum(a.part + (size_t)f * NACC + u, (size_t)a.Fp * NACC, a.nchunk);
-    s_acc[u] = x;
+  {  // NACC = 72 > 64 lanes for J = 4: a lane sums up to 4 statistics, the
+     // loads of all of them for 8 chunks in flight together (chunk order kept)
+    constexpr int kQ = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64;
+    double x[kQ] = {};
+    const size_t cs = (size_t)a.Fp * NACC;
+    const double *p0 = a.part + (size_t)f * NACC + lane;
+    for (int c = 0; c < a.nchunk; c += 8) {
+      double v[kQ][8];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[q][u] = (lane + 64 * q < NACC && c + u < a.nchunk) ? p0[(size_t)(c + u) * cs + 64 * q] : 0.0;
+#pragma unroll
+      for (int q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[q] += v[q][u];
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+      if (lane + 64 * q < NACC) s_acc[lane + 64 * q] = x[q];
   }
   if (lane < 2 * R) s_A[lane >> 1][lane & 1] = a.A[(size_t)lane * a.Fp + f];
-  if (lane < J) {  // sum_t V_j(f, t) = sum_k W_j(f, k) sum_t TW_j(k, t)
+  // sum_t V_j(f, t) = sum_k W_j(f, k) sum_t TW_j(k, t): the operands are
+  // loaded by all lanes at once (a per-source loop over k was a chain of
+  // global-latency round trips), then summed in k order
+  for (int i = lane; i < J * a.KP; i += 64) {
+    s_wh[0][i] = a.Wkf[(size_t)i * a.Fp + f];
+    s_wh[1][i] = a.hsum[i];
+  }
+  __syncthreads();
+  if (lane < J) {
     double sv = 0.0;
-    for (int k = 0; k < a.KP; ++k)
-      sv += a.Wkf[((size_t)lane * a.KP + k) * a.Fp + f] * a.hsum[lane * a.KP + k];
+    for (int k = 0; k < a.KP; ++k) sv += s_wh[0][lane * a.KP + k] * s_wh[1][lane * a.KP + k];
     s_sv[lane] = sv;
   }
   __syncthreads();
@@ -1199,13 +1224,13 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   double *s_wn = s_den + KP;
   for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
     s_fw[idx] = a.FW[(size_t)j * KP * KP + idx];
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) s_den[k] = a.hsum[(size_t)j * KP + k];
   __syncthreads();
-  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
-    const double *hs = a.hsum + (size_t)j * KP;
-    double d = 0.0;
-    for (int q = 0; q < KP; ++q) d += s_fw[k * KP + q] * hs[q];
-    s_den[k] = d;
-  }
+  double dk = 0.0;
+  if (threadIdx.x < KP)
+    for (int q = 0; q < KP; ++q) dk += s_fw[threadIdx.x * KP + q] * s_den[q];
+  __syncthreads();
+  if (threadIdx.x < KP) s_den[threadIdx.x] = dk;
   __syncthreads();
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int fl = idx / KP, k = idx % KP, f = f0 + fl;
@@ -1410,8 +1435,75 @@ struct TArgs {
   int kb0[kMaxJ], kb1[kMaxJ];  // BLK: the V tiles sum the columns [kb0, kb1) only
   const double *cp, *pw;       // LAM: corrPen / powers planes of k_multi_prep
   const double *oth;           // TBQ: max(V_c, eps) plane of k_multi_prep
+  // !BLK with cnt set: the last of a frame tile's gridDim.z bin-chunk blocks
+  // sums their partials and applies the TW update itself (k_tw_update's work,
+  // in launch); cnt[j][blockIdx.x] are its arrival counters (zero between
+  // launches: the last arriver resets them)
+  int *cnt;
+  double omega;
   const int *halt;
 };
+
+// write-through (sc1) 8-byte buffer accesses: a hand-off that needs no
+// agent-scope release / acquire fence (cdna_hip_programming.md split-K recipe)
+typedef unsigned tw_u2 __attribute__((ext_vector_type(2)));
+constexpr int kSc1 = 16;
+__device__ __forceinline__ void sc1_store(__amdgpu_buffer_rsrc_t r, size_t i, double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  tw_u2 x;
+  x.x = (unsigned)b;
+  x.y = (unsigned)(b >> 32);
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)(i * sizeof(double)), 0, kSc1);
+}
+__device__ __forceinline__ double sc1_load(__amdgpu_buffer_rsrc_t r, size_t i) {
+  const tw_u2 x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * sizeof(double)), 0, kSc1);
+  return __longlong_as_double((long long)(((unsigned long long)x.y << 32) | x.x));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const double *p, size_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, (int)(n * sizeof(double)),
+                                           0x00020000);
+}
+
+// TW *= (sum_chunks num / max(sum_chunks den, eps))^omega for the frames of
+// the TPW tiles at tt0 of source j (k_tw_update's arithmetic, chunk order
+// kept): one wave, loads coalesced over k
+template <int TPW>
+__device__ void tw_apply_tiles(const TArgs &a, int j, int tt0, int lane) {
+  const int n = 16 * a.KP;
+  const size_t cs = (size_t)a.J * a.Tp * a.KP;
+  const __amdgpu_buffer_rsrc_t rn = buf_rsrc(a.tnum, cs * gridDim.z);
+  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(a.tden, cs * gridDim.z);
+  for (int p = 0; p < TPW; ++p) {
+    if (tt0 + p >= a.ntt) break;
+    const int t0 = (tt0 + p) * 16;
+    for (int base = 0; base < n; base += 4 * 64) {
+      double num[4], den[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) num[u] = den[u] = 0.0;
+      for (int c = 0; c < (int)gridDim.z; ++c) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = base + u * 64 + lane;
+          if (idx < n) {
+            const size_t o = c * cs + ((size_t)j * a.Tp + t0 + idx / a.KP) * a.KP + idx % a.KP;
+            num[u] += sc1_load(rn, o);
+            den[u] += sc1_load(rd, o);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = base + u * 64 + lane;
+        const int t = t0 + idx / a.KP, k = idx % a.KP;
+        if (idx < n && t < a.T && k >= a.kb0[j] && k < a.kb1[j]) {
+          const double ratio = num[u] / fmax(den[u], kEps);
+          const_cast<double *>(a.TW)[((size_t)j * a.KP + k) * a.Tp + t] *=
+              a.omega == 1.0 ? ratio : pow(ratio, a.omega);
+        }
+      }
+    }
+  }
+}
 
 // TW numerator / denominator over f (:1694-1726), one wave per (TPW frame
 // tiles, source, bin chunk):
@@ -1523,6 +1615,37 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
     }
   }
   const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Tp;
+  bool fused = false;
+  if constexpr (!BLK && !TBQ) fused = a.cnt != nullptr;
+  if (fused) {
+    // in-launch split-K reduction: the partials go out write-through (sc1),
+    // drained before the ticket; the last arriver reads them with sc1 loads
+    // (no agent fences: cdna_hip_programming.md split-K recipe, sc1 form)
+    const size_t nall = (size_t)gridDim.z * a.J * a.Tp * a.KP;
+    const __amdgpu_buffer_rsrc_t rn = buf_rsrc(a.tnum, nall), rd = buf_rsrc(a.tden, nall);
+#pragma unroll
+    for (int p = 0; p < TPW; ++p) {
+      if (tt0 + p >= a.ntt) break;
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const size_t o = (base + (tt0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl;
+          sc1_store(rn, o, num[p][kc][m]);
+          sc1_store(rd, o, den[p][kc][m]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) {
+      int *ct = a.cnt + (size_t)j * gridDim.x + blockIdx.x;
+      const int old = __hip_atomic_fetch_add(ct, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == (int)gridDim.z - 1;
+      if (last) __hip_atomic_store(ct, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (__builtin_amdgcn_readfirstlane(last)) tw_apply_tiles<TPW>(a, j, tt0, lane);
+    return;
+  }
 #pragma unroll
   for (int p = 0; p < TPW; ++p) {
     if (tt0 + p >= a.ntt) break;
@@ -1769,31 +1892,40 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   __shared__ double s_red[256];
   __shared__ double s_w[kMaxKP], s_w2[kMaxKP];
   __shared__ double s_e;
+  __shared__ double s_big[kMaxKP * kMaxKP];   // chunk maxima, then FW_j
   const int j = blockIdx.y, c = blockIdx.x;
   const int K = a.K[j], KP = a.KP;
   const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+  // the cross-chunk statistics are loaded by all threads at once and folded
+  // in LDS (a per-thread loop over the chunks was a chain of dependent
+  // global-latency round trips), in the same order as before
+  const int ne = a.conv ? a.nchunk : nr * 2;
+  for (int q = threadIdx.x; q < ne; q += blockDim.x) {
+    if (a.conv) {
+      s_red[q] = a.pe[(size_t)j * a.nchunk + q];
+    } else {
+      const double2 x = a.Pinst[2 * r0 + q];
+      s_red[q] = x.x * x.x + x.y * x.y;
+    }
+  }
+  for (int i = threadIdx.x; i < a.nchunk * KP; i += blockDim.x)
+    s_big[i] = a.pmax[(size_t)j * a.nchunk * KP + i];
+  __syncthreads();
   if (threadIdx.x == 0) {
     double e = 0.0;
-    if (a.conv) {
-      for (int q = 0; q < a.nchunk; ++q) e += a.pe[(size_t)j * a.nchunk + q];
-      e /= (double)(nr * 2 * a.F);
-    } else {
-      for (int q = 0; q < nr * 2; ++q) {
-        const double2 x = a.Pinst[2 * r0 + q];
-        e += x.x * x.x + x.y * x.y;
-      }
-      e /= (double)(nr * 2);
-    }
-    s_e = e;
+    for (int q = 0; q < ne; ++q) e += s_red[q];
+    s_e = e / (double)(a.conv ? nr * 2 * a.F : nr * 2);
   }
   __syncthreads();
   const double e = s_e;
   if (threadIdx.x < KP) {
     double m = -INFINITY;
-    for (int q = 0; q < a.nchunk; ++q) m = fmax(m, a.pmax[((size_t)j * a.nchunk + q) * KP + threadIdx.x]);
+    for (int q = 0; q < a.nchunk; ++q) m = fmax(m, s_big[q * KP + threadIdx.x]);
     const double w = m * e;
     s_w[threadIdx.x] = w == 0.0 ? 1.0 : w;
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KP * KP; i += blockDim.x) s_big[i] = a.FW[(size_t)j * KP * KP + i];
   __syncthreads();
   if (threadIdx.x < K) {
     // FW.mean(axis=0) of the column's own spectral component (block)
@@ -1801,9 +1933,8 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
     int b = 0;
     while (b + 1 < a.nblk[j] && cc >= a.kb[j][b + 1]) ++b;
     const int r0b = a.kb[j][b], r1b = a.kb[j][b + 1];
-    const double *FW = a.FW + (size_t)j * KP * KP;
     double s = 0.0;
-    for (int r = r0b; r < r1b; ++r) s += FW[r * KP + cc] * s_w[r];
+    for (int r = r0b; r < r1b; ++r) s += s_big[r * KP + cc] * s_w[r];
     s /= (double)(r1b - r0b);
     s_w2[cc] = s == 0.0 ? 1.0 : s;
   }
@@ -1895,11 +2026,13 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
       *p = make_double2(p->x / se, p->y / se);
     }
   }
+  __shared__ double s_t[kMaxSlot * 64];   // the per-chunk TW sums, loaded at once
+  for (int i = threadIdx.x; i < a.nslot * a.nchunk; i += blockDim.x) s_t[i] = a.tpart[i];
   __syncthreads();
   const int sl = threadIdx.x;   // one TW restart test per spectral component
   if (sl >= a.nslot || (a.tbmask >> sl & 1u)) return;
   double s = 0.0;
-  for (int c = 0; c < a.nchunk; ++c) s += a.tpart[(size_t)sl * a.nchunk + c];
+  for (int c = 0; c < a.nchunk; ++c) s += s_t[sl * a.nchunk + c];
   const int dead = s < kEps ? 1 : 0;
   a.flags[1 + sl] = dead;
   if (dead) {
@@ -2252,6 +2385,14 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
   c->eb_split = 1;
   if (const char *v = getenv("FASST_EB_SPLIT")) c->eb_split = std::max(1, std::min(atoi(v), 8));
+  // FASST_TW_FUSED=1: the TW update in the TW contraction's last arrivers
+  // (A/B knob, default off: C3 1.144 ms per iteration fused with the sc1
+  // hand-off vs 1.139 separate; 1.358 with agent release / acquire fences);
+  // the fused form addresses the partials with 32-bit buffer offsets
+  c->tw_fused = 0;
+  if (const char *v = getenv("FASST_TW_FUSED"))
+    c->tw_fused = atoi(v) != 0 &&
+                  (size_t)c->nsplit_t * J * c->Tp * c->KP * sizeof(double) < (1ull << 31);
   if (getenv("FASST_VERBOSE"))
     fprintf(stderr,
             "fasst: %d CUs; estep %d chunks (cap %ld blocks); fb %d chunks (cap %ld); tw %d "
@@ -2282,6 +2423,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   ALLOC(pnum, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(pden, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(tnum, (size_t)c->nsplit_t * J * Tp * KP);
+  if ((st = c->tcnt.alloc((size_t)J * ((c->ntt + kTPW - 1) / kTPW)))) return st;
   ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
@@ -2694,6 +2836,8 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     t.cp = mp.rcp;
     t.pw = mp.rpow;
     t.oth = nullptr;
+    t.cnt = nullptr;
+    t.omega = omega;
     const TBArgs tbw = tb_args(c, b, only_j, 1, omega), tbb = tb_args(c, b, only_j, 2, omega);
     int lmax, kwmax;
     const bool any_tbb = tb_any(tbb, &lmax, &kwmax);
@@ -3059,6 +3203,9 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   t.nft = c->nft;
   t.ntt = c->ntt;
   t.fpc = c->fpc_t;
+  t.cp = t.pw = t.oth = nullptr;
+  t.cnt = c->tw_fused ? c->tcnt.p : nullptr;
+  t.omega = omega;
   TUArgs tu;
   tu.TW = c->TW.p;
   tu.tnum = c->tnum.p;
@@ -3161,10 +3308,12 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     default: launch_contract<4>(c, b, t, false); break;
   }
   FASST_LAUNCH_CHECK();
-  prof_begin(c, KTWU);
-  k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
-  prof_end(c, KTWU);
-  FASST_LAUNCH_CHECK();
+  if (!c->tw_fused) {   // else applied by the contraction's last arrivers
+    prof_begin(c, KTWU);
+    k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
+    prof_end(c, KTWU);
+    FASST_LAUNCH_CHECK();
+  }
   return launch_renorm(c, iter);
 }
 

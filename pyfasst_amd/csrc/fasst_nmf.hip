@@ -174,17 +174,26 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
   };
   auto compute = [&](int tt, int cs) {
     const int t0 = tt * 16;
+    // the hat tiles of all FPW bin tiles first, four accumulation chains each
+    // (one wave per SIMD: the MFMA latency is hidden by independent chains)
+    d4 hv[FPW];
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      d4 v0 = d4{0.0, 0.0, 0.0, 0.0}, v1 = v0, v2 = v0, v3 = v0;
+#pragma unroll
+      for (int s = 0; s < NKS; s += 4) {
+        v0 = nmfma(th[cs][s], wk[p][s], v0);
+        v1 = nmfma(th[cs][s + 1], wk[p][s + 1], v1);
+        v2 = nmfma(th[cs][s + 2], wk[p][s + 2], v2);
+        v3 = nmfma(th[cs][s + 3], wk[p][s + 3], v3);
+      }
+      hv[p] = (v0 + v1) + (v2 + v3);
+    }
 #pragma unroll
     for (int p = 0; p < FPW; ++p) {
       if (ft0 + p >= nft) break;  // wave-uniform
       const int f = (ft0 + p) * 16 + fl;
-      d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;  // hat at (frame t0+tq+4i, bin f)
-#pragma unroll
-      for (int s = 0; s < NKS; s += 2) {
-        v = nmfma(th[cs][s], wk[p][s], v);
-        v2 = nmfma(th[cs][s + 1], wk[p][s + 1], v2);
-      }
-      v += v2;
+      const d4 v = hv[p];  // hat at (frame t0+tq+4i, bin f)
       double x[4], y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -269,17 +278,24 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
   };
   auto compute = [&](int ft, int cs) {
     const int f0 = ft * 16;
+    d4 hv[TPW];   // as k_nmf_wnum: all hat tiles first, four chains each
+#pragma unroll
+    for (int p = 0; p < TPW; ++p) {
+      d4 v0 = d4{0.0, 0.0, 0.0, 0.0}, v1 = v0, v2 = v0, v3 = v0;
+#pragma unroll
+      for (int s = 0; s < NKS; s += 4) {
+        v0 = nmfma(ao[cs][s], bt[p][s], v0);
+        v1 = nmfma(ao[cs][s + 1], bt[p][s + 1], v1);
+        v2 = nmfma(ao[cs][s + 2], bt[p][s + 2], v2);
+        v3 = nmfma(ao[cs][s + 3], bt[p][s + 3], v3);
+      }
+      hv[p] = (v0 + v1) + (v2 + v3);
+    }
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
       if (tt0 + p >= ntt) break;  // wave-uniform
       const int t = (tt0 + p) * 16 + fl;
-      d4 v = d4{0.0, 0.0, 0.0, 0.0}, v2 = v;  // hat at (bin f0+tq+4i, frame t)
-#pragma unroll
-      for (int s = 0; s < NKS; s += 2) {
-        v = nmfma(ao[cs][s], bt[p][s], v);
-        v2 = nmfma(ao[cs][s + 1], bt[p][s + 1], v2);
-      }
-      v += v2;
+      const d4 v = hv[p];  // hat at (bin f0+tq+4i, frame t)
       double x[4], y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -313,19 +329,30 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
 }
 
 // k_nmf_w over the fused path's group partials ([g][num / den][K][F])
-__global__ __launch_bounds__(256) void k_nmf_w_part(double *__restrict__ W,
+__global__ __launch_bounds__(1024) void k_nmf_w_part(double *__restrict__ W,
                                                     const double *__restrict__ part, int ng,
                                                     double *__restrict__ s_out, int F, int K) {
-  __shared__ double s_red[256];
+  // 1024 threads: one or two bins each, the ng group partials of a bin
+  // loaded 8 at a time (a per-group loop was a chain of global round trips)
+  __shared__ double s_red[1024];
   const int k = blockIdx.x;
   const size_t slab = (size_t)K * F;
   double acc = 0.0;
-  for (int f = threadIdx.x; f < F; f += 256) {
+  for (int f = threadIdx.x; f < F; f += blockDim.x) {
     const double *q = part + (size_t)k * F + f;
-    double n = q[0], d = q[slab];
-    for (int g = 1; g < ng; ++g) {
-      n += q[(size_t)g * 2 * slab];
-      d += q[(size_t)g * 2 * slab + slab];
+    double n = 0.0, d = 0.0;
+    for (int g = 0; g < ng; g += 8) {
+      double vn[8], vd[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        vn[u] = g + u < ng ? q[(size_t)(g + u) * 2 * slab] : 0.0;
+        vd[u] = g + u < ng ? q[(size_t)(g + u) * 2 * slab + slab] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        n += vn[u];
+        d += vd[u];
+      }
     }
     const double w = W[(size_t)f * K + k] * (n / fmax(d, kNmfEps));
     W[(size_t)f * K + k] = w;
@@ -333,13 +360,13 @@ __global__ __launch_bounds__(256) void k_nmf_w_part(double *__restrict__ W,
   }
   s_red[threadIdx.x] = acc;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
     if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
     __syncthreads();
   }
   double s = s_red[0];
   if (s == 0) s = 1.0;  // sumW[sumW==0] = 1. (nmf.py:46)
-  for (int f = threadIdx.x; f < F; f += 256) W[(size_t)f * K + k] /= s;
+  for (int f = threadIdx.x; f < F; f += blockDim.x) W[(size_t)f * K + k] /= s;
   if (threadIdx.x == 0) s_out[k] = s;
 }
 
@@ -549,7 +576,7 @@ static void nmf_fused_pw(nmf_ctx *c, int update_w, int update_h) {
   if (update_w) {
     k_nmf_wnum<NKC, PW><<<dim3((nft + PW - 1) / PW, c->ng_w), 256, 0, c->stream>>>(
         c->W.p, c->H.p, c->SXt.p, c->part.p, F, N, c->tpc_w);
-    k_nmf_w_part<<<K, 256, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
+    k_nmf_w_part<<<K, 1024, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
   }
   const double *hs = update_w ? c->s.p : nullptr;
   if (update_h) {
