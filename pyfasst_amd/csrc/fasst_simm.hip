@@ -14,6 +14,7 @@
 #include "fasst_gemm.h"
 
 #include <cmath>
+#include <type_traits>
 
 #include "../../include/fasst_simm.h"
 
@@ -37,29 +38,84 @@ __device__ __forceinline__ double powo(double x, double omega) {
   return omega == 1.0 ? x : pow(x, omega);
 }
 
-// HF0 / HPHI / HGAMMA ratios, stereo (SIMM.py:623-630, :688-694):
-//   com = aR2*Z/max(hR), den = aL2*Z/max(hL), num = com*SXR/max(hR) + den*SXL/max(hL), den += com
-// mono (SIMM.py:282-283): den = Z/max(hat), num = (den*SX)/max(hat)
-__global__ void k_simm_numden(const double *__restrict__ Z, const double *__restrict__ hR,
-                              const double *__restrict__ hL, const double *__restrict__ SXR,
-                              const double *__restrict__ SXL, const double *__restrict__ alpha,
-                              double *__restrict__ num, double *__restrict__ den, size_t n,
-                              int stereo) {
-  if (stereo) {
-    const double aR2 = alpha[0] * alpha[0], aL2 = alpha[1] * alpha[1];
-    GRID_STRIDE(i, n) {
-      const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
-      const double com = aR2 * CLD(Z[i]) / mr;
-      const double d = aL2 * CLD(Z[i]) / ml;
-      num[i] = com * CLD(SXR[i]) / mr + d * CLD(SXL[i]) / ml;
-      den[i] = d + com;
-    }
+constexpr int kSimmKmax = 8;  // simm_create: K <= 8 filters
+constexpr int kHgRowChunks = 4;  // frame chunks of k_hgamma_rows (>= 4 waves per SIMD at C5)
+
+// ---------------------------------------------------------------------------
+// The model spectrograms are not stored between updates.  Every update of the
+// reference ends with a refresh of hatSX_R / hatSX_L (SIMM.py:661-674,
+// :715-728, :760-773, :812-823, :856-869, :894-906, :925-941); here each
+// consumer recomputes, per point, from the resident planes SF0, SMR, SML:
+//   SPHI = WPHI HPHI (K <= 8 filters: the column of HPHI in registers, the
+//          row of WPHI wave-uniform), summed in k order as k_simm_refresh does
+//   l = SF0 SPHI, hR = max(SMR + aR^2 l, eps), hL = max(aL^2 l + SML, eps)
+//   (mono: hat = max(l + SM, eps))
+// i.e. exactly the values the refresh pass would have stored.  That removes
+// the four hat-refresh passes (6-7 streamed F x N planes each) and shrinks the
+// three accompaniment refreshes to their two SMR / SML writes: ~45 plane
+// passes per Stereo_SIMM iteration instead of ~79.  The column scale that
+// HPHI / HGAMMA apply to HF0 (and so to SF0 = WF0 HF0) is left pending and
+// applied (and written back) by the next kernel that streams SF0.
+template <bool ST>
+__device__ __forceinline__ void hat_of(double sf, double sp, double smr, double sml, double aR2,
+                                       double aL2, double &hr, double &hl) {
+  const double l = sf * sp;
+  if constexpr (ST) {
+    hr = fmax(smr + aR2 * l, kSimmEps);
+    hl = fmax(l * aL2 + sml, kSimmEps);
   } else {
-    GRID_STRIDE(i, n) {
-      const double m = fmax(CLD(hR[i]), kSimmEps);
-      const double d = CLD(Z[i]) / m;
-      den[i] = d;
-      num[i] = (d * CLD(SXR[i])) / m;
+    hr = fmax(l + smr, kSimmEps);
+    hl = 0.0;
+  }
+}
+
+template <int KM>
+__device__ __forceinline__ double sphi_of(const double *__restrict__ w, const double *h, int K) {
+  double sp = 0.0;
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+    if (k < K) sp += w[k] * h[k];
+  return sp;
+}
+
+// the resident planes a consumer reads
+struct SPl {
+  const double *SF0, *SMR, *SML, *SXR, *SXL, *WPHI, *HPHI, *alpha;
+  const double *pend;  // pending column scale of SF0 (null: none)
+  double *SF0w;        // where the scaled SF0 is written back (null: not written)
+  int F, N, K, fchunk;
+};
+
+// HF0 ratios, stereo (SIMM.py:623-630): com = aR2*SPHI/max(hR),
+// d = aL2*SPHI/max(hL), num = com*SXR/max(hR) + d*SXL/max(hL), den = d + com;
+// mono (:282-283): den = SPHI/max(hat), num = (den*SX)/max(hat).  Thread per
+// frame n walking a chunk of bins (grid: N/256 x F chunks).
+template <bool ST, int KM>
+__global__ __launch_bounds__(256) void k_simm_numden(const SPl p, double *__restrict__ num,
+                                                     double *__restrict__ den) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= p.N) return;
+  const int fb = blockIdx.y * p.fchunk, fe = min(p.F, fb + p.fchunk);
+  double h[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) h[k] = k < p.K ? p.HPHI[(size_t)k * p.N + n] : 0.0;
+  const double aR2 = ST ? p.alpha[0] * p.alpha[0] : 1.0;
+  const double aL2 = ST ? p.alpha[1] * p.alpha[1] : 1.0;
+#pragma unroll 2
+  for (int f = fb; f < fe; ++f) {
+    const size_t i = (size_t)f * p.N + n;
+    const double sp = sphi_of<KM>(p.WPHI + (size_t)f * p.K, h, p.K);
+    double hr, hl;
+    hat_of<ST>(CLD(p.SF0[i]), sp, CLD(p.SMR[i]), ST ? CLD(p.SML[i]) : 0.0, aR2, aL2, hr, hl);
+    if constexpr (ST) {
+      const double com = aR2 * sp / hr;
+      const double d = aL2 * sp / hl;
+      SST(num[i], com * CLD(p.SXR[i]) / hr + d * CLD(p.SXL[i]) / hl);
+      SST(den[i], d + com);
+    } else {
+      const double d = sp / hr;
+      SST(den[i], d);
+      SST(num[i], (d * CLD(p.SXR[i])) / hr);
     }
   }
 }
@@ -126,20 +182,18 @@ __global__ void k_simm_refresh(double *__restrict__ SF0, double *__restrict__ SP
   }
 }
 
-// Accompaniment refresh fused with the hat refresh (the step after every HM,
-// WM and beta update, SIMM.py:747-773, :826-869, :909-941): stereo
-// SMR = (WM bR^2) HM, SML = (WM bL^2) HM, mono SM = WM HM (R <= RMAX), then
-// hR / hL exactly as k_simm_refresh.  One thread per frame n keeps the HM
-// column in registers for FB bins; the FB rows of WM (times beta^2) sit in
-// LDS.  Replaces two K = R products (which wrote SMR / SML only for the
-// refresh to read them back) and the refresh pass: 6 streamed planes
-// instead of 8, one launch instead of five.
+// Accompaniment refresh (the step after every HM, WM and beta update,
+// SIMM.py:747-773, :826-869, :909-941): stereo SMR = (WM bR^2) HM,
+// SML = (WM bL^2) HM, mono SM = WM HM (R <= RMAX).  One thread per frame n
+// keeps the HM column in registers for FB bins; the FB rows of WM (times
+// beta^2) are wave-uniform.  Only the two planes are written: the hat is
+// recomputed by its consumers (hat_of).
 template <int RMAX>
-__global__ __launch_bounds__(256) void k_simm_sm_refresh(
-    const double *__restrict__ WbR, const double *__restrict__ WbL, const double *__restrict__ HM,
-    const double *__restrict__ SF0, const double *__restrict__ SPHI,
-    const double *__restrict__ alpha, double *__restrict__ SMR, double *__restrict__ SML,
-    double *__restrict__ hR, double *__restrict__ hL, int F, int N, int R, int stereo) {
+__global__ __launch_bounds__(256) void k_simm_sm(const double *__restrict__ WbR,
+                                                 const double *__restrict__ WbL,
+                                                 const double *__restrict__ HM,
+                                                 double *__restrict__ SMR, double *__restrict__ SML,
+                                                 int F, int N, int R, int stereo) {
   constexpr int FB = 16;
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int f0 = blockIdx.y * FB;
@@ -147,8 +201,6 @@ __global__ __launch_bounds__(256) void k_simm_sm_refresh(
   double hm[RMAX];
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) hm[r] = r < R ? HM[(size_t)r * N + n] : 0.0;
-  const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
-  const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
   for (int fl = 0; fl < FB; ++fl) {
     const int f = f0 + fl;
     if (f >= F) break;
@@ -158,19 +210,12 @@ __global__ __launch_bounds__(256) void k_simm_sm_refresh(
     double sr = 0.0, sl = 0.0;
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) sr += wr[r] * hm[r];
+    const size_t i = (size_t)f * N + n;
+    SST(SMR[i], sr);
     if (stereo) {
 #pragma unroll
       for (int r = 0; r < RMAX; ++r) sl += wl[r] * hm[r];
-    }
-    const size_t i = (size_t)f * N + n;
-    const double l = SLD(SF0[i]) * SLD(SPHI[i]);
-    SST(SMR[i], sr);
-    if (stereo) {
       SST(SML[i], sl);
-      SST(hR[i], fmax(sr + aR2 * l, kSimmEps));
-      SST(hL[i], fmax(l * aL2 + sl, kSimmEps));
-    } else {
-      SST(hR[i], fmax(l + sr, kSimmEps));
     }
   }
 }
@@ -187,11 +232,19 @@ __global__ void k_simm_xy(const double *__restrict__ h, const double *__restrict
   }
 }
 
-// k_simm_xy's operands for one element (both channels' formulas in one place)
+// k_simm_xy's operands for one element (both channels' formulas in one
+// place) in the fused skinny products: reciprocals by v_rcp_f64 + two Newton
+// steps (<= 1 ulp) instead of the IEEE division sequences (hv >= eps: it
+// comes from hat_of)
+__device__ __forceinline__ double simm_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
 template <bool ST>
 __device__ __forceinline__ void xy_of(double hv, double sx, double &x, double &y) {
-  y = 1.0 / fmax(hv, kSimmEps);
-  x = ST ? sx / fmax(hv * hv, kSimmEps) : (y * sx) / fmax(hv, kSimmEps);
+  y = simm_rcp(hv);
+  x = ST ? sx * simm_rcp(fmax(hv * hv, kSimmEps)) : (y * sx) * y;
 }
 
 // Skinny accompaniment products with k_simm_xy fused into the operand loads
@@ -203,72 +256,78 @@ __device__ __forceinline__ void xy_of(double hv, double sx, double &x, double &y
 //   lane (fl, tq) streams T at (f = k0 + 4s + tq, n = n0 + fl): every load
 //   instruction reads four 128-byte row segments.  Split-K over f along
 //   gridDim.z into out + z*slab, [q][R][N] per slab.
-template <bool ST>
-__global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(
-    const double *__restrict__ WM, const double *__restrict__ hR, const double *__restrict__ SXR,
-    const double *__restrict__ hL, const double *__restrict__ SXL, double *__restrict__ out,
-    size_t slab, int F, int N, int R, int kchunk) {
+//   The hat is formed in the loads (hat_of: SF0, SMR, SML, SPHI from this
+//   lane's HPHI column and WPHI rows), and a pending SF0 column scale is
+//   applied and written back here (every (f, n) is loaded by one lane once).
+template <bool ST, int KM>
+__global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(const SPl p, const double *__restrict__ WM,
+                                                        double *__restrict__ out, size_t slab,
+                                                        int R, int kchunk) {
   constexpr int NC = ST ? 2 : 1, NO = 2 * NC;
+  const int F = p.F, N = p.N, K = p.K;
   const int lane = threadIdx.x & 63, fl = lane & 15, tq = lane >> 4;
   const int n = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + fl;
   const int kb = blockIdx.z * kchunk, ke = min(F, kb + kchunk);
   const bool nin = n < N;
-  const double *hs[2] = {hR, hL}, *ss[2] = {SXR, SXL};
+  const double *ss[2] = {p.SXR, p.SXL}, *sm[2] = {p.SMR, p.SML};
+  double h[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) h[k] = (nin && k < K) ? p.HPHI[(size_t)k * N + n] : 0.0;
+  const double cs = (nin && p.pend) ? p.pend[n] : 1.0;
+  const double aR2 = ST ? p.alpha[0] * p.alpha[0] : 1.0;
+  const double aL2 = ST ? p.alpha[1] * p.alpha[1] : 1.0;
+  // the WPHI rows of this block's bin chunk, staged in LDS (lanes of one tq
+  // read the same row: broadcast reads instead of K vector loads per point)
+  extern __shared__ double sW[];
+  for (int e = threadIdx.x; e < (ke - kb) * K; e += 256) sW[e] = p.WPHI[(size_t)kb * K + e];
+  __syncthreads();
   d4 acc[NO][3];
 #pragma unroll
   for (int q = 0; q < NO; ++q)
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
-  double hv[ST ? 1 : 2][NC][4], sv[ST ? 1 : 2][NC][4];
-  auto load = [&](int buf, int k0) {
+  for (int k0 = kb; k0 < ke; k0 += 16) {
+    double sfv[4], smv[NC][4], sv[NC][4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int f = k0 + 4 * s + tq;
       const bool ok = nin && f < ke;
       const size_t idx = (size_t)f * N + n;
+      sfv[s] = ok ? CLD(p.SF0[idx]) : 0.0;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        hv[buf][c][s] = ok ? hs[c][idx] : 0.0;
-        sv[buf][c][s] = ok ? ss[c][idx] : 0.0;
+        smv[c][s] = ok ? CLD(sm[c][idx]) : 0.0;
+        sv[c][s] = ok ? CLD(ss[c][idx]) : 0.0;
       }
     }
-  };
-  auto compute = [&](int buf, int k0) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int f = k0 + 4 * s + tq;
+      const bool fok = f < ke;
+      if (p.SF0w) {   // pending column scale (HPHI's renormalisation of HF0)
+        sfv[s] *= cs;
+        if (nin && fok) SST(p.SF0w[(size_t)f * N + n], sfv[s]);
+      }
+      const double sp = fok ? sphi_of<KM>(sW + (size_t)(f - kb) * K, h, K) : 0.0;
+      double hv[2];
+      hat_of<ST>(sfv[s], sp, smv[0][s], ST ? smv[NC - 1][s] : 0.0, aR2, aL2, hv[0], hv[1]);
       double a[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int r = i * 16 + fl;
-        a[i] = (f < ke && r < R) ? WM[(size_t)f * R + r] : 0.0;  // zero rows outside [kb, ke)
+        a[i] = (fok && r < R) ? WM[(size_t)f * R + r] : 0.0;  // zero rows outside [kb, ke)
       }
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double x, y;
-        xy_of<ST>(hv[buf][c][s], sv[buf][c][s], x, y);
+        xy_of<ST>(hv[c], sv[c][s], x, y);
+        if (!(nin && fok)) x = y = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           acc[2 * c][i] = gmfma(a[i], x, acc[2 * c][i]);
           acc[2 * c + 1][i] = gmfma(a[i], y, acc[2 * c + 1][i]);
         }
       }
-    }
-  };
-  if constexpr (ST) {  // 48 accumulators: no room for a second load buffer
-    for (int k0 = kb; k0 < ke; k0 += 16) {
-      load(0, k0);
-      compute(0, k0);
-    }
-  } else {  // next chunk's loads in flight under the current chunk's MFMAs
-    int k0 = kb;
-    if (k0 < ke) load(0, k0);
-    for (; k0 < ke; k0 += 32) {
-      if (k0 + 16 < ke) load(1, k0 + 16);
-      compute(0, k0);
-      if (k0 + 16 >= ke) break;
-      if (k0 + 32 < ke) load(0, k0 + 32);
-      compute(1, k0 + 16);
     }
   }
   if (!nin) return;
@@ -291,57 +350,89 @@ __global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(
 //   contiguous bytes of 16 rows); HM's chunk [48][32] is shared by the
 //   block's 4 waves through LDS (pitch 34: the half-wave's (fl, tq) pairs hit
 //   32 distinct bank pairs).  Split-K over frames along gridDim.z, [q][F][R] per slab.
-template <bool ST>
-__global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(
-    const double *__restrict__ HM, const double *__restrict__ hR, const double *__restrict__ SXR,
-    const double *__restrict__ hL, const double *__restrict__ SXL, double *__restrict__ out,
-    size_t slab, int F, int N, int R, int kchunk) {
+//   The hat is formed from SF0, SMR, SML and SPHI (this lane's WPHI row in
+//   registers, HPHI's chunk columns staged in LDS next to HM's), and a pending
+//   SF0 column scale (HGAMMA's renormalisation of HF0) is applied and written
+//   back here.
+template <bool ST, int KM>
+__global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const double *__restrict__ HM,
+                                                        double *__restrict__ out, size_t slab,
+                                                        int R, int kchunk) {
   constexpr int NC = ST ? 2 : 1, NO = 2 * NC, KC = 32, PH = KC + 2;
-  __shared__ double sH[48 * PH];
+  constexpr int NR = 48 + KM + 1;   // HM rows, HPHI rows, the pending scale
+  __shared__ double sH[NR * PH];
+  const int F = p.F, N = p.N, K = p.K;
   const int tid = threadIdx.x, lane = tid & 63, fl = lane & 15, tq = lane >> 4;
   const int f = blockIdx.y * 64 + (tid >> 6) * 16 + fl;
   const int kb = blockIdx.z * kchunk, ke = min(N, kb + kchunk);
   const bool fin = f < F;
-  const double *hs[2] = {hR, hL}, *ss[2] = {SXR, SXL};
+  const double *ss[2] = {p.SXR, p.SXL}, *sm[2] = {p.SMR, p.SML};
+  double w[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) w[k] = (fin && k < K) ? p.WPHI[(size_t)f * K + k] : 0.0;
+  const double aR2 = ST ? p.alpha[0] * p.alpha[0] : 1.0;
+  const double aL2 = ST ? p.alpha[1] * p.alpha[1] : 1.0;
   d4 acc[NO][3];
 #pragma unroll
   for (int q = 0; q < NO; ++q)
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
   for (int kc = kb; kc < ke; kc += KC) {
-    double hv[NC][8], sv[NC][8];
     const size_t base = (size_t)f * N + kc + tq;
+    double sfv[8], smv[NC][8], sv[NC][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool ok = fin && kc + tq + 4 * j < ke;
+      // plain (cached) loads: a lane group reads 32 bytes of a row per
+      // instruction, the rest of the line arrives with the next j's
+      sfv[j] = ok ? p.SF0[base + 4 * j] : 0.0;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        hv[c][j] = ok ? hs[c][base + 4 * j] : 0.0;
+        smv[c][j] = ok ? sm[c][base + 4 * j] : 0.0;
         sv[c][j] = ok ? ss[c][base + 4 * j] : 0.0;
       }
     }
-    double hm[6];  // 48 x 32 chunk of HM, zero outside [0, R) x [kc, ke)
+    double hm[(NR * KC + 255) / 256];  // chunk of HM (48 rows), HPHI (8 rows), pend
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
-      const int e = tid + 256 * t, r = e / KC, k = e % KC;
-      hm[t] = (r < R && kc + k < ke) ? HM[(size_t)r * N + kc + k] : 0.0;
+    for (int t = 0; t < (NR * KC + 255) / 256; ++t) {
+      const int e = tid + 256 * t, r = e / KC, k = e % KC, col = kc + k;
+      double v = 0.0;
+      if (col < ke) {
+        if (r < 48) v = r < R ? HM[(size_t)r * N + col] : 0.0;
+        else if (r < 48 + KM) v = r - 48 < K ? p.HPHI[(size_t)(r - 48) * N + col] : 0.0;
+        else if (r == NR - 1) v = p.pend ? p.pend[col] : 1.0;
+      }
+      hm[t] = v;
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
+    for (int t = 0; t < (NR * KC + 255) / 256; ++t) {
       const int e = tid + 256 * t;
-      sH[(e / KC) * PH + e % KC] = hm[t];
+      if (e < NR * KC) sH[(e / KC) * PH + e % KC] = hm[t];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
+      const int kk = tq + 4 * j;
+      const bool ok = fin && kc + kk < ke;
+      if (p.SF0w) {   // (plain store: the line's four 32-byte pieces merge in L2)
+        sfv[j] *= sH[(NR - 1) * PH + kk];
+        if (ok) p.SF0w[base + 4 * j] = sfv[j];
+      }
+      double h[KM];
+#pragma unroll
+      for (int k = 0; k < KM; ++k) h[k] = sH[(48 + k) * PH + kk];
+      const double sp = sphi_of<KM>(w, h, K);
+      double hv[2];
+      hat_of<ST>(sfv[j], sp, smv[0][j], ST ? smv[NC - 1][j] : 0.0, aR2, aL2, hv[0], hv[1]);
       double b[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) b[i] = sH[(i * 16 + fl) * PH + tq + 4 * j];
+      for (int i = 0; i < 3; ++i) b[i] = sH[(i * 16 + fl) * PH + kk];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double x, y;
-        xy_of<ST>(hv[c][j], sv[c][j], x, y);
+        xy_of<ST>(hv[c], sv[c][j], x, y);
+        if (!ok) x = y = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           acc[2 * c][i] = gmfma(x, b[i], acc[2 * c][i]);
@@ -364,48 +455,53 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(
 }
 
 // HPHI numerator/denominator: out[m][n] = sum_f WPHI[f][m] * {num,den}(f, n),
-// num/den built on the fly from Z = SF0 (:688-694).  Block: 256 frames x one
-// f-chunk; partials [chunk][2][K][N].
-__global__ __launch_bounds__(256) void k_hphi_partial(
-    const double *__restrict__ Z, const double *__restrict__ hR, const double *__restrict__ hL,
-    const double *__restrict__ SXR, const double *__restrict__ SXL,
-    const double *__restrict__ alpha, const double *__restrict__ WPHI, double *__restrict__ part,
-    int F, int N, int K, int fchunk, int stereo) {
+// num/den built on the fly from Z = SF0 and the hat (hat_of) (:688-694).
+// Block: 256 frames x one f-chunk; partials [chunk][2][K][N].
+template <bool ST, int KM>
+__global__ __launch_bounds__(256) void k_hphi_partial(const SPl p, double *__restrict__ part) {
   const int n = blockIdx.x * 256 + threadIdx.x;
-  const int c = blockIdx.y;
-  const int fb = c * fchunk, fe = min(F, fb + fchunk);
-  double sn[8], sd[8];
-  for (int k = 0; k < 8; ++k) sn[k] = sd[k] = 0.0;
-  if (n < N) {
-    const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
-    const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
-    for (int f = fb; f < fe; ++f) {
-      const size_t i = (size_t)f * N + n;
-      double num, den;
-      if (stereo) {
-        const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
-        const double com = aR2 * CLD(Z[i]) / mr;
-        const double d = aL2 * CLD(Z[i]) / ml;
-        num = com * CLD(SXR[i]);
-        num /= mr;
-        num += d * CLD(SXL[i]) / ml;
-        den = d + com;
-      } else {
-        const double m = fmax(CLD(hR[i]), kSimmEps);
-        den = CLD(Z[i]) / m;
-        num = (den * CLD(SXR[i])) / m;
-      }
-      for (int k = 0; k < K; ++k) {
-        const double w = WPHI[f * K + k];
-        sn[k] += w * num;
-        sd[k] += w * den;
-      }
+  const int c = blockIdx.y, K = p.K, N = p.N;
+  const int fb = c * p.fchunk, fe = min(p.F, fb + p.fchunk);
+  if (n >= N) return;
+  double sn[KM], sd[KM], h[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    sn[k] = sd[k] = 0.0;
+    h[k] = k < K ? p.HPHI[(size_t)k * N + n] : 0.0;
+  }
+  const double aR2 = ST ? p.alpha[0] * p.alpha[0] : 1.0;
+  const double aL2 = ST ? p.alpha[1] * p.alpha[1] : 1.0;
+  for (int f = fb; f < fe; ++f) {
+    const size_t i = (size_t)f * N + n;
+    const double *w = p.WPHI + (size_t)f * K;
+    const double z = CLD(p.SF0[i]);
+    double mr, ml;
+    hat_of<ST>(z, sphi_of<KM>(w, h, K), CLD(p.SMR[i]), ST ? CLD(p.SML[i]) : 0.0, aR2, aL2, mr, ml);
+    double num, den;
+    if constexpr (ST) {
+      const double com = aR2 * z / mr;
+      const double d = aL2 * z / ml;
+      num = com * CLD(p.SXR[i]);
+      num /= mr;
+      num += d * CLD(p.SXL[i]) / ml;
+      den = d + com;
+    } else {
+      den = z / mr;
+      num = (den * CLD(p.SXR[i])) / mr;
     }
-    for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (k < K) {
+        sn[k] += w[k] * num;
+        sd[k] += w[k] * den;
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+    if (k < K) {
       part[(((size_t)c * 2 + 0) * K + k) * N + n] = sn[k];
       part[(((size_t)c * 2 + 1) * K + k) * N + n] = sd[k];
     }
-  }
 }
 
 // HPHI *= (num/max(den,eps))^omega; s = column sums; HPHI[:, s>0] /= s
@@ -436,46 +532,50 @@ __global__ void k_colscale(double *__restrict__ X, const double *__restrict__ s,
 }
 
 // HGAMMA numerator/denominator rows: out[f][k] = sum_n {num,den}(f, n) HPHI[k][n]
-// (np.dot(tempNumFbyN, HPHI.T), :802); one block per bin f.
-__global__ __launch_bounds__(256) void k_hgamma_rows(
-    const double *__restrict__ Z, const double *__restrict__ hR, const double *__restrict__ hL,
-    const double *__restrict__ SXR, const double *__restrict__ SXL,
-    const double *__restrict__ alpha, const double *__restrict__ HPHI, double *__restrict__ out,
-    int F, int N, int K, int stereo) {
+// (np.dot(tempNumFbyN, HPHI.T), :802), the hat formed on the fly (hat_of);
+// one block per FB bins and frame chunk (gridDim.y chunks: partial rows
+// [chunk][F][2K], summed in chunk order by k_hgamma_numden).
+template <bool ST, int KM>
+__global__ __launch_bounds__(256) void k_hgamma_rows(const SPl p, double *__restrict__ out) {
   constexpr int FB = 4;  // frequency rows per block: each HPHI load serves FB rows
-  __shared__ double s_red[FB * 16][4];
+  __shared__ double s_red[FB * 2 * KM][4];
+  const int F = p.F, N = p.N, K = p.K;
   const int f0 = blockIdx.x * FB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  double sn[FB][8], sd[FB][8];
+  double sn[FB][KM], sd[FB][KM];
 #pragma unroll
   for (int r = 0; r < FB; ++r)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) sn[r][k] = sd[r][k] = 0.0;
-  const double aR2 = stereo ? alpha[0] * alpha[0] : 1.0;
-  const double aL2 = stereo ? alpha[1] * alpha[1] : 1.0;
-  for (int n = threadIdx.x; n < N; n += 256) {
-    double h[8];
+    for (int k = 0; k < KM; ++k) sn[r][k] = sd[r][k] = 0.0;
+  const double aR2 = ST ? p.alpha[0] * p.alpha[0] : 1.0;
+  const double aL2 = ST ? p.alpha[1] * p.alpha[1] : 1.0;
+  const int nb = blockIdx.y * ((N + gridDim.y - 1) / gridDim.y);
+  const int ne = min(N, nb + (N + gridDim.y - 1) / gridDim.y);
+  for (int n = nb + threadIdx.x; n < ne; n += 256) {
+    double h[KM];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) h[k] = k < K ? HPHI[(size_t)k * N + n] : 0.0;
+    for (int k = 0; k < KM; ++k) h[k] = k < K ? p.HPHI[(size_t)k * N + n] : 0.0;
 #pragma unroll
     for (int r = 0; r < FB; ++r) {
       if (f0 + r >= F) break;
       const size_t i = (size_t)(f0 + r) * N + n;
+      const double z = CLD(p.SF0[i]);
+      double mr, ml;
+      hat_of<ST>(z, sphi_of<KM>(p.WPHI + (size_t)(f0 + r) * K, h, K), CLD(p.SMR[i]),
+                 ST ? CLD(p.SML[i]) : 0.0, aR2, aL2, mr, ml);
       double num, den;
-      if (stereo) {
-        const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
-        const double com = aR2 * CLD(Z[i]) / mr;
-        const double d = aL2 * CLD(Z[i]) / ml;
-        num = com * CLD(SXR[i]);
+      if constexpr (ST) {
+        const double com = aR2 * z / mr;
+        const double d = aL2 * z / ml;
+        num = com * CLD(p.SXR[i]);
         num /= mr;
-        num += d * CLD(SXL[i]) / ml;
+        num += d * CLD(p.SXL[i]) / ml;
         den = d + com;
       } else {
-        const double m = fmax(CLD(hR[i]), kSimmEps);
-        den = CLD(Z[i]) / m;
-        num = (den * CLD(SXR[i])) / m;
+        den = z / mr;
+        num = (den * CLD(p.SXR[i])) / mr;
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {  // fixed trip count: sn / sd stay in registers
+      for (int k = 0; k < KM; ++k) {  // fixed trip count: sn / sd stay in registers
         sn[r][k] += num * h[k];
         sd[r][k] += den * h[k];
       }
@@ -485,18 +585,18 @@ __global__ __launch_bounds__(256) void k_hgamma_rows(
 #pragma unroll
   for (int r = 0; r < FB; ++r)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      if (q % 8 >= K) continue;
-      double v = q < 8 ? sn[r][q] : sd[r][q - 8];
+    for (int q = 0; q < 2 * KM; ++q) {
+      if (q % KM >= K) continue;
+      double v = q < KM ? sn[r][q] : sd[r][q - KM];
       for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == 0) s_red[r * 16 + q][wv] = v;
+      if (lane == 0) s_red[r * 2 * KM + q][wv] = v;
     }
   __syncthreads();
   for (int t = threadIdx.x; t < FB * 2 * K; t += 256) {
     const int r = t / (2 * K), q = t % (2 * K);
-    const int slot = r * 16 + (q < K ? q : 8 + q - K);
+    const int slot = r * 2 * KM + (q < K ? q : KM + q - K);
     if (f0 + r < F)
-      out[(size_t)(f0 + r) * 2 * K + q] =
+      out[((size_t)blockIdx.y * F + f0 + r) * 2 * K + q] =
           (s_red[slot][0] + s_red[slot][1]) + (s_red[slot][2] + s_red[slot][3]);
   }
 }
@@ -510,7 +610,7 @@ __global__ __launch_bounds__(256) void k_hgamma_rows(
 __global__ __launch_bounds__(256) void k_hgamma_numden(const double *__restrict__ WGAMMA,
                                                        const double *__restrict__ rows,
                                                        double *__restrict__ nd, int F, int P,
-                                                       int K) {
+                                                       int K, int nrc) {
   __shared__ double s_red[16][8];
   const int p = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double acc[16];
@@ -520,7 +620,11 @@ __global__ __launch_bounds__(256) void k_hgamma_numden(const double *__restrict_
     const double w = WGAMMA[(size_t)f * P + p];
 #pragma unroll
     for (int q = 0; q < 16; ++q)
-      if (q < 2 * K) acc[q] += w * rows[(size_t)f * 2 * K + q];
+      if (q < 2 * K) {
+        double r = rows[(size_t)f * 2 * K + q];
+        for (int c = 1; c < nrc; ++c) r += rows[((size_t)c * F + f) * 2 * K + q];
+        acc[q] += w * r;
+      }
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -646,21 +750,32 @@ __global__ void k_wm_beta(const double *__restrict__ WM, const double *__restric
   }
 }
 
-// alpha sums (:875-885): [sum numR, sum denR, sum numL, sum denL] partials
-__global__ __launch_bounds__(256) void k_alpha_partial(
-    const double *__restrict__ SF0, const double *__restrict__ SPHI, const double *__restrict__ hR,
-    const double *__restrict__ hL, const double *__restrict__ SXR, const double *__restrict__ SXL,
-    double *__restrict__ part, size_t n) {
+// alpha sums (:875-885): [sum numR, sum denR, sum numL, sum denL] partials,
+// one per block of the (N/256 x F chunks) walker grid, the hat on the fly
+template <int KM>
+__global__ __launch_bounds__(256) void k_alpha_partial(const SPl p, double *__restrict__ part) {
   __shared__ double s_red[4][256];
+  const int n = blockIdx.x * 256 + threadIdx.x, N = p.N, K = p.K;
+  const int fb = blockIdx.y * p.fchunk, fe = min(p.F, fb + p.fchunk);
   double a[4] = {0, 0, 0, 0};
-  GRID_STRIDE(i, n) {
-    const double l = CLD(SF0[i]) * CLD(SPHI[i]);
-    const double mr = fmax(CLD(hR[i]), kSimmEps), ml = fmax(CLD(hL[i]), kSimmEps);
-    const double dR = l / mr, dL = l / ml;
-    a[0] += dR * CLD(SXR[i]) / mr;
-    a[1] += dR;
-    a[2] += dL * CLD(SXL[i]) / ml;
-    a[3] += dL;
+  if (n < N) {
+    double h[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) h[k] = k < K ? p.HPHI[(size_t)k * N + n] : 0.0;
+    const double aR2 = p.alpha[0] * p.alpha[0], aL2 = p.alpha[1] * p.alpha[1];
+    for (int f = fb; f < fe; ++f) {
+      const size_t i = (size_t)f * N + n;
+      const double sp = sphi_of<KM>(p.WPHI + (size_t)f * K, h, K);
+      const double sf = CLD(p.SF0[i]);
+      double mr, ml;
+      hat_of<true>(sf, sp, CLD(p.SMR[i]), CLD(p.SML[i]), aR2, aL2, mr, ml);
+      const double l = sf * sp;
+      const double dR = l / mr, dL = l / ml;
+      a[0] += dR * CLD(p.SXR[i]) / mr;
+      a[1] += dR;
+      a[2] += dL * CLD(p.SXL[i]) / ml;
+      a[3] += dL;
+    }
   }
   for (int q = 0; q < 4; ++q) s_red[q][threadIdx.x] = a[q];
   __syncthreads();
@@ -669,7 +784,8 @@ __global__ __launch_bounds__(256) void k_alpha_partial(
       for (int q = 0; q < 4; ++q) s_red[q][threadIdx.x] += s_red[q][threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x < 4) part[(size_t)blockIdx.x * 4 + threadIdx.x] = s_red[threadIdx.x][0];
+  if (threadIdx.x < 4)
+    part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = s_red[threadIdx.x][0];
 }
 
 __global__ void k_alpha_update(const double *__restrict__ part, int nb, double *__restrict__ alpha,
@@ -719,21 +835,34 @@ __global__ void k_beta_update(const double *__restrict__ d, double *__restrict__
 }
 
 // Itakura-Saito divergence partials (ISDistortion, SIMM.py:34-44) of
-// SXR vs hR (+ SXL vs hL): sum(-log(r) + r - 1), r = SX/hat
-__global__ __launch_bounds__(256) void k_is_partial(const double *__restrict__ SXR,
-                                                    const double *__restrict__ hR,
-                                                    const double *__restrict__ SXL,
-                                                    const double *__restrict__ hL,
-                                                    double *__restrict__ part, size_t n,
-                                                    int stereo) {
+// SXR vs hR (+ SXL vs hL): sum(-log(r) + r - 1), r = SX/hat; the hat on the
+// fly, with a pending SF0 column scale applied (not written back)
+template <bool ST, int KM>
+__global__ __launch_bounds__(256) void k_is_partial(const SPl p, double *__restrict__ part) {
   __shared__ double s_red[256];
+  const int n = blockIdx.x * 256 + threadIdx.x, N = p.N, K = p.K;
+  const int fb = blockIdx.y * p.fchunk, fe = min(p.F, fb + p.fchunk);
   double a = 0.0;
-  GRID_STRIDE(i, n) {
-    double r = SXR[i] / hR[i];
-    a += (-log(r) + r) - 1;
-    if (stereo) {
-      r = SXL[i] / hL[i];
+  if (n < N) {
+    double h[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) h[k] = k < K ? p.HPHI[(size_t)k * N + n] : 0.0;
+    const double cs = p.pend ? p.pend[n] : 1.0;
+    const double aR2 = ST ? p.alpha[0] * p.alpha[0] : 1.0;
+    const double aL2 = ST ? p.alpha[1] * p.alpha[1] : 1.0;
+    for (int f = fb; f < fe; ++f) {
+      const size_t i = (size_t)f * N + n;
+      double sf = CLD(p.SF0[i]);
+      if (p.pend) sf *= cs;
+      double hr, hl;
+      hat_of<ST>(sf, sphi_of<KM>(p.WPHI + (size_t)f * K, h, K), CLD(p.SMR[i]),
+                 ST ? CLD(p.SML[i]) : 0.0, aR2, aL2, hr, hl);
+      double r = CLD(p.SXR[i]) / hr;
       a += (-log(r) + r) - 1;
+      if constexpr (ST) {
+        r = CLD(p.SXL[i]) / hl;
+        a += (-log(r) + r) - 1;
+      }
     }
   }
   s_red[threadIdx.x] = a;
@@ -742,7 +871,7 @@ __global__ __launch_bounds__(256) void k_is_partial(const double *__restrict__ S
     if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[blockIdx.x] = s_red[0];
+  if (threadIdx.x == 0) part[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = s_red[0];
 }
 
 __global__ void k_is_final(const double *__restrict__ part, int nb, double *__restrict__ out) {
@@ -787,9 +916,13 @@ struct simm_ctx {
   hipStream_t stream = nullptr;
   rocblas_handle blas = nullptr;  // bound to `stream`: the NF0-sized plain GEMMs
   int use_blas = 1;               // FASST_SIMM_BLAS=0: k_gemm instead (A/B only)
-  int fuse_sm = 1;                // FASST_SIMM_FUSE_SM=0: unfused SM refresh (A/B only)
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
+  int nchunk_w = 1, fchunk_w = 1;  // the frame-walker grid (N/256 x bin chunks)
+  // SF0's pending column scale (s_col after HPHI / HGAMMA), applied by the
+  // next kernel that streams SF0; SPHI / hR / hL hold the model only after
+  // refresh_hat (rebuild_model, the R > 48 path)
+  const double *pend = nullptr;
   DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
   DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, NP0, NP1, WMb, WMb2, s_col, sg, sw;
   DBuf<double> hpart, hrows, apart, bd, gwork, P0, P1, P2, P3, RN0, RN1, reco;
@@ -812,6 +945,7 @@ int sf0_gemm(simm_ctx *c) {
   return gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, c->N, c->SF0.p, c->N, c->F, c->N, c->NF0);
 }
 
+constexpr int kWmtMaxChunk = 512;   // bins per k_simm_wmt_xy block (its LDS WPHI rows)
 // split of the fused skinny products (k_simm_wmt_xy / k_simm_xy_hmt): a
 // grid of >= 1024 (resp. 512) blocks, K chunks of >= 64 (256) rows
 struct SkinnySplit {
@@ -821,6 +955,7 @@ static SkinnySplit wmt_split(int F, int N) {
   const long bx = (N + 63) / 64;
   int nz = 1;
   while (bx * nz < 1024 && F / (2 * nz) >= 64) nz *= 2;
+  nz = std::max(nz, (F + kWmtMaxChunk - 1) / kWmtMaxChunk);   // WPHI rows fit the LDS
   const int kchunk = ((F + nz - 1) / nz + 15) / 16 * 16;
   return {(F + kchunk - 1) / kchunk, kchunk};
 }
@@ -843,10 +978,55 @@ void reduce_slabs(simm_ctx *c, int no, int nz, size_t n, double *const *dst) {
         c->gwork.p + (size_t)q * n, nz, (size_t)no * n, dst[q], n);
 }
 
+// K <= 4 filters (the documented configurations) or <= 8: the per-lane
+// SPHI / HPHI arrays and the HGAMMA accumulators are sized by the bound
+template <class L>
+void kdispatch(int K, L &&launch) {
+  if (K <= 4)
+    launch(std::integral_constant<int, 4>{});
+  else
+    launch(std::integral_constant<int, 8>{});
+}
+
+// the resident planes as the consumers read them; `apply` = the kernel
+// streams every point of SF0 once and writes the pending column scale back
+SPl planes(const simm_ctx *c, bool apply) {
+  SPl p;
+  p.SF0 = c->SF0.p;
+  p.SMR = c->SMR.p;
+  p.SML = c->SML.p;
+  p.SXR = c->SXR.p;
+  p.SXL = c->SXL.p;
+  p.WPHI = c->WPHI.p;
+  p.HPHI = c->HPHI.p;
+  p.alpha = c->alpha.p;
+  p.pend = c->pend;
+  p.SF0w = (apply && c->pend) ? c->SF0.p : nullptr;
+  p.F = c->F;
+  p.N = c->N;
+  p.K = c->K;
+  p.fchunk = c->fchunk_w;
+  return p;
+}
+
+dim3 walker_grid(const simm_ctx *c) { return dim3((c->N + 255) / 256, c->nchunk_w); }
+
+int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi);
+
+// the model spectrograms as planes (SPHI, hR, hL) for the paths that read
+// them (R > 48 products), consuming the pending SF0 scale
+int materialise_hat(simm_ctx *c) {
+  const int st = refresh_hat(c, c->pend, 1);
+  c->pend = nullptr;
+  return st;
+}
+
 // dst[q] (R x N) = WM^T {X_R, Y_R, X_L, Y_L}[q] from the current model
 int wmt_xy(simm_ctx *c, double *const *dst) {
   const int F = c->F, N = c->N, R = c->R, no = c->stereo ? 4 : 2;
   if (R > 48) {  // wide accompaniment dictionaries: materialise X, Y, general GEMM
+    int st = materialise_hat(c);
+    if (st) return st;
     k_simm_xy<<<egrid((size_t)F * N), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p,
                                                            (size_t)F * N, c->stereo);
     if (c->stereo)
@@ -859,13 +1039,17 @@ int wmt_xy(simm_ctx *c, double *const *dst) {
   const SkinnySplit sp = wmt_split(F, N);
   const size_t slab = (size_t)no * R * N;
   dim3 grid((N + 63) / 64, 1, sp.nz);
-  if (c->stereo)
-    k_simm_wmt_xy<true><<<grid, 256, 0, c->stream>>>(c->WM.p, c->hR.p, c->SXR.p, c->hL.p, c->SXL.p,
-                                                      c->gwork.p, slab, F, N, R, sp.kchunk);
-  else
-    k_simm_wmt_xy<false><<<grid, 256, 0, c->stream>>>(c->WM.p, c->hR.p, c->SXR.p, nullptr, nullptr,
-                                                       c->gwork.p, slab, F, N, R, sp.kchunk);
+  const SPl p = planes(c, true);
+  const size_t lds = (size_t)sp.kchunk * c->K * sizeof(double);
+  kdispatch(c->K, [&](auto km) {
+    constexpr int KM = decltype(km)::value;
+    if (c->stereo)
+      k_simm_wmt_xy<true, KM><<<grid, 256, lds, c->stream>>>(p, c->WM.p, c->gwork.p, slab, R, sp.kchunk);
+    else
+      k_simm_wmt_xy<false, KM><<<grid, 256, lds, c->stream>>>(p, c->WM.p, c->gwork.p, slab, R, sp.kchunk);
+  });
   FASST_LAUNCH_CHECK();
+  c->pend = nullptr;
   reduce_slabs(c, no, sp.nz, (size_t)R * N, dst);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
@@ -875,6 +1059,8 @@ int wmt_xy(simm_ctx *c, double *const *dst) {
 int xy_hmt(simm_ctx *c, double *const *dst) {
   const int F = c->F, N = c->N, R = c->R, no = c->stereo ? 4 : 2;
   if (R > 48) {
+    int st = materialise_hat(c);
+    if (st) return st;
     k_simm_xy<<<egrid((size_t)F * N), 256, 0, c->stream>>>(c->hR.p, c->SXR.p, c->T0.p, c->T1.p,
                                                            (size_t)F * N, c->stereo);
     if (c->stereo)
@@ -884,7 +1070,7 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
     for (int q = 0; q < no; ++q) {  // X HM^T : (F x N)(N x R)
       const double *Bs[1] = {c->HM.p};
       double *Cs[1] = {dst[q]};
-      int st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p);
+      st = gemm<false, true, 1>(c->stream, srcs[q], N, Bs, N, Cs, R, F, R, N, c->gwork.p);
       if (st) return st;
     }
     return FASST_OK;
@@ -892,20 +1078,23 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
   const SkinnySplit sp = hmt_split(F, N);
   const size_t slab = (size_t)no * F * R;
   dim3 grid(1, (F + 63) / 64, sp.nz);
-  if (c->stereo)
-    k_simm_xy_hmt<true><<<grid, 256, 0, c->stream>>>(c->HM.p, c->hR.p, c->SXR.p, c->hL.p, c->SXL.p,
-                                                      c->gwork.p, slab, F, N, R, sp.kchunk);
-  else
-    k_simm_xy_hmt<false><<<grid, 256, 0, c->stream>>>(c->HM.p, c->hR.p, c->SXR.p, nullptr, nullptr,
-                                                       c->gwork.p, slab, F, N, R, sp.kchunk);
+  const SPl p = planes(c, true);
+  kdispatch(c->K, [&](auto km) {
+    constexpr int KM = decltype(km)::value;
+    if (c->stereo)
+      k_simm_xy_hmt<true, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+    else
+      k_simm_xy_hmt<false, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+  });
   FASST_LAUNCH_CHECK();
+  c->pend = nullptr;
   reduce_slabs(c, no, sp.nz, (size_t)F * R, dst);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
 }
 
 // SMR = (WM bR^2) HM, SML = (WM bL^2) HM  (stereo); SM = WM HM (mono)
-int refresh_sm(simm_ctx *c) {
+int refresh_sm_gemm(simm_ctx *c) {
   if (c->stereo) {
     k_wm_beta<<<egrid((size_t)c->F * c->R), 256, 0, c->stream>>>(c->WM.p, c->bR.p, c->WMb.p, c->F, c->R);
     int st = gemm_nn(c, c->WMb.p, c->R, c->HM.p, c->N, c->SMR.p, c->N, c->F, c->N, c->R);
@@ -916,27 +1105,22 @@ int refresh_sm(simm_ctx *c) {
   return gemm_nn(c, c->WM.p, c->R, c->HM.p, c->N, c->SMR.p, c->N, c->F, c->N, c->R);
 }
 
-int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi);
-
-// refresh_sm + refresh_hat(c, nullptr, 0) as one fused pass when R is small
+// the accompaniment planes after an HM / WM / beta update (the hat itself is
+// recomputed by its consumers)
 constexpr int kSmRmax = 48;
-int refresh_sm_hat(simm_ctx *c) {
-  if (c->R <= kSmRmax && c->fuse_sm) {
-    const size_t FRP = (size_t)c->F * kSmRmax;
-    k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->stereo ? c->bR.p : nullptr,
-                                                     c->WMb.p, c->F, c->R, kSmRmax);
-    if (c->stereo)
-      k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->bL.p, c->WMb2.p, c->F, c->R,
-                                                       kSmRmax);
-    const dim3 grid((c->N + 255) / 256, (c->F + 15) / 16);
-    k_simm_sm_refresh<kSmRmax><<<grid, 256, 0, c->stream>>>(
-        c->WMb.p, c->WMb2.p, c->HM.p, c->SF0.p, c->SPHI.p, c->alpha.p, c->SMR.p, c->SML.p,
-        c->hR.p, c->hL.p, c->F, c->N, c->R, c->stereo);
-    FASST_LAUNCH_CHECK();
-    return FASST_OK;
-  }
-  int st = refresh_sm(c);
-  return st ? st : refresh_hat(c, nullptr, 0);
+int refresh_sm(simm_ctx *c) {
+  if (c->R > kSmRmax) return refresh_sm_gemm(c);
+  const size_t FRP = (size_t)c->F * kSmRmax;
+  k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->stereo ? c->bR.p : nullptr,
+                                                   c->WMb.p, c->F, c->R, kSmRmax);
+  if (c->stereo)
+    k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->bL.p, c->WMb2.p, c->F, c->R,
+                                                     kSmRmax);
+  const dim3 grid((c->N + 255) / 256, (c->F + 15) / 16);
+  k_simm_sm<kSmRmax><<<grid, 256, 0, c->stream>>>(c->WMb.p, c->WMb2.p, c->HM.p, c->SMR.p,
+                                                  c->SML.p, c->F, c->N, c->R, c->stereo);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
 }
 
 int refresh_hat(simm_ctx *c, const double *colscale, int recompute_sphi) {
@@ -954,7 +1138,8 @@ int rebuild_model(simm_ctx *c) {
   const int F = c->F, K = c->K;
   if ((st = gemm_nn(c, c->WGAMMA.p, c->P, c->HGAMMA.p, K, c->WPHI.p, K, F, K, c->P))) return st;
   if ((st = sf0_gemm(c))) return st;
-  if ((st = refresh_sm(c))) return st;
+  if ((st = refresh_sm_gemm(c))) return st;
+  c->pend = nullptr;
   // the reference's initial hat is not floored by eps (:579-585); every use
   // floors it again with max(., eps), so the floored copy is equivalent
   if ((st = refresh_hat(c, nullptr, 1))) return st;
@@ -963,21 +1148,38 @@ int rebuild_model(simm_ctx *c) {
 }
 
 void reco_error(simm_ctx *c, double *slot) {
-  const size_t FN = (size_t)c->F * c->N;
-  k_is_partial<<<c->nb_alpha, 256, 0, c->stream>>>(c->SXR.p, c->hR.p, c->SXL.p, c->hL.p,
-                                                    c->apart.p, FN, c->stereo);
-  k_is_final<<<1, 64, 0, c->stream>>>(c->apart.p, c->nb_alpha, slot);
+  const dim3 grid = walker_grid(c);
+  const SPl p = planes(c, false);
+  kdispatch(c->K, [&](auto km) {
+    constexpr int KM = decltype(km)::value;
+    if (c->stereo)
+      k_is_partial<true, KM><<<grid, 256, 0, c->stream>>>(p, c->apart.p);
+    else
+      k_is_partial<false, KM><<<grid, 256, 0, c->stream>>>(p, c->apart.p);
+  });
+  k_is_final<<<1, 64, 0, c->stream>>>(c->apart.p, (int)(grid.x * grid.y), slot);
 }
 
 // one loop body; reco (device, may be null) receives the IS divergence
-// after the HF0 and after the HPHI updates (SIMM.py:676-683, :721-728)
+// after the HF0 and after the HPHI updates (SIMM.py:676-683, :721-728).
+// Between updates the resident state is SF0 (times the pending column scale),
+// SMR / SML, WPHI / HPHI and the scalars: the hat is formed by each consumer.
 int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
-  const size_t FN = (size_t)c->F * c->N;
   const int F = c->F, N = c->N, NF0 = c->NF0, K = c->K, R = c->R;
+  const bool ST = c->stereo != 0;
+  const dim3 wg = walker_grid(c);
   int st;
   // ---- HF0 (:623-674 / :281-291)
-  k_simm_numden<<<egrid(FN), 256, 0, c->stream>>>(c->SPHI.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p,
-                                                   c->alpha.p, c->T0.p, c->T1.p, FN, c->stereo);
+  {
+    const SPl p = planes(c, false);   // (no scale is pending at the iteration start)
+    kdispatch(K, [&](auto km) {
+      constexpr int KM = decltype(km)::value;
+      if (ST)
+        k_simm_numden<true, KM><<<wg, 256, 0, c->stream>>>(p, c->T0.p, c->T1.p);
+      else
+        k_simm_numden<false, KM><<<wg, 256, 0, c->stream>>>(p, c->T0.p, c->T1.p);
+    });
+  }
   if (c->use_blas) {  // WF0^T {num, den}: (NF0 x F)(F x N)
     if ((st = blas_gemm(c->blas, true, false, NF0, N, F, c->WF0.p, NF0, c->T0.p, N, c->NP0.p, N)) ||
         (st = blas_gemm(c->blas, true, false, NF0, N, F, c->WF0.p, NF0, c->T1.p, N, c->NP1.p, N)))
@@ -991,19 +1193,27 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   k_mu_apply<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->NP0.p, c->NP1.p,
                                                              (size_t)NF0 * N, omega, 0);
   if ((st = sf0_gemm(c))) return st;
-  if ((st = refresh_hat(c, nullptr, 0))) return st;
   if (reco) reco_error(c, reco);
   // ---- HPHI (:686-729 / :296-313)
-  k_hphi_partial<<<dim3((N + 255) / 256, c->nchunk_h), 256, 0, c->stream>>>(
-      c->SF0.p, c->hR.p, c->hL.p, c->SXR.p, c->SXL.p, c->alpha.p, c->WPHI.p, c->hpart.p, F, N, K,
-      c->fchunk_h, c->stereo);
+  {
+    SPl p = planes(c, false);
+    p.fchunk = c->fchunk_h;
+    const dim3 gh((N + 255) / 256, c->nchunk_h);
+    kdispatch(K, [&](auto km) {
+      constexpr int KM = decltype(km)::value;
+      if (ST)
+        k_hphi_partial<true, KM><<<gh, 256, 0, c->stream>>>(p, c->hpart.p);
+      else
+        k_hphi_partial<false, KM><<<gh, 256, 0, c->stream>>>(p, c->hpart.p);
+    });
+  }
   k_hphi_update<<<(N + 255) / 256, 256, 0, c->stream>>>(c->HPHI.p, c->hpart.p, c->nchunk_h,
                                                          c->s_col.p, K, N, omega);
   k_colscale<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->s_col.p, NF0, N);
-  if ((st = refresh_hat(c, c->s_col.p, 1))) return st;
+  c->pend = c->s_col.p;   // SF0 *= s_col, applied by the HM products below
   if (reco) reco_error(c, reco + 1);
   // ---- HM (:740-773 / :318-331)
-  if (c->stereo) {
+  if (ST) {
     double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
     if ((st = wmt_xy(c, Cs))) return st;
     k_hm_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
@@ -1016,22 +1226,28 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     k_mu_apply<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->RN0.p, c->RN1.p,
                                                             (size_t)R * N, omega, 1);
   }
-  if ((st = refresh_sm_hat(c))) return st;
+  if ((st = refresh_sm(c))) return st;
   // ---- HGAMMA (:776-823 / :335-350)
   if (update_hgamma) {
-    k_hgamma_rows<<<(F + 3) / 4, 256, 0, c->stream>>>(c->SF0.p, c->hR.p, c->hL.p, c->SXR.p,
-                                                       c->SXL.p, c->alpha.p, c->HPHI.p, c->hrows.p,
-                                                       F, N, K, c->stereo);
-    k_hgamma_numden<<<c->P, 256, 0, c->stream>>>(c->WGAMMA.p, c->hrows.p, c->apart.p, F, c->P, K);
+    const SPl p = planes(c, false);
+    kdispatch(K, [&](auto km) {
+      constexpr int KM = decltype(km)::value;
+      if (ST)
+        k_hgamma_rows<true, KM><<<dim3((F + 3) / 4, kHgRowChunks), 256, 0, c->stream>>>(p, c->hrows.p);
+      else
+        k_hgamma_rows<false, KM><<<dim3((F + 3) / 4, kHgRowChunks), 256, 0, c->stream>>>(p, c->hrows.p);
+    });
+    k_hgamma_numden<<<c->P, 256, 0, c->stream>>>(c->WGAMMA.p, c->hrows.p, c->apart.p, F, c->P, K,
+                                                 kHgRowChunks);
     k_hgamma_norm<<<1, 64, 0, c->stream>>>(c->HGAMMA.p, c->apart.p, c->sg.p, c->P, K, omega);
     k_wphi<<<(F * K + 255) / 256, 256, 0, c->stream>>>(c->WGAMMA.p, c->HGAMMA.p, c->WPHI.p, F,
                                                        c->P, K);
     k_hphi_rescale<<<(N + 255) / 256, 256, 0, c->stream>>>(c->HPHI.p, c->sg.p, c->s_col.p, K, N);
     k_colscale<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->s_col.p, NF0, N);
-    if ((st = refresh_hat(c, c->s_col.p, 1))) return st;
+    c->pend = c->s_col.p;   // applied by the WM products below
   }
   // ---- WM (:826-869 / :355-387)
-  if (c->stereo) {
+  if (ST) {
     double *dsts[4] = {c->P0.p, c->P1.p, c->P2.p, c->P3.p};
     if ((st = xy_hmt(c, dsts))) return st;
     k_wm_update<<<R, 256, 0, c->stream>>>(c->WM.p, c->P0.p, c->P1.p, c->P2.p, c->P3.p, c->bR.p,
@@ -1048,13 +1264,13 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     else
       k_colscale<<<egrid((size_t)R * N), 256, 0, c->stream>>>(c->HM.p, c->sw.p, R, N);  // R == N
   }
-  if ((st = refresh_sm_hat(c))) return st;
-  if (!c->stereo) return FASST_OK;
+  if ((st = refresh_sm(c))) return st;
+  if (!ST) return FASST_OK;
   // ---- alpha (:872-906)
-  k_alpha_partial<<<c->nb_alpha, 256, 0, c->stream>>>(c->SF0.p, c->SPHI.p, c->hR.p, c->hL.p,
-                                                       c->SXR.p, c->SXL.p, c->apart.p, FN);
-  k_alpha_update<<<1, 64, 0, c->stream>>>(c->apart.p, c->nb_alpha, c->alpha.p, omega);
-  if ((st = refresh_hat(c, nullptr, 0))) return st;
+  kdispatch(K, [&](auto km) {
+    k_alpha_partial<decltype(km)::value><<<wg, 256, 0, c->stream>>>(planes(c, false), c->apart.p);
+  });
+  k_alpha_update<<<1, 64, 0, c->stream>>>(c->apart.p, (int)(wg.x * wg.y), c->alpha.p, omega);
   // ---- beta (:909-941)
   {
     double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
@@ -1065,7 +1281,7 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p + (size_t)R * N, c->HM.p, c->bd.p + 2 * R, N);
   k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p + (size_t)R * N, c->HM.p, c->bd.p + 3 * R, N);
   k_beta_update<<<1, 64, 0, c->stream>>>(c->bd.p, c->bR.p, c->bL.p, R, omega);
-  return refresh_sm_hat(c);
+  return refresh_sm(c);
 }
 
 }  // namespace
@@ -1093,7 +1309,11 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   c->stereo = stereo ? 1 : 0;
   c->fchunk_h = std::max(1, (F + 15) / 16);
   c->nchunk_h = (F + c->fchunk_h - 1) / c->fchunk_h;
-  c->nb_alpha = 1024;
+  // frame-walker grid: >= ~2048 blocks of 256 frames x a chunk of bins
+  c->nchunk_w = std::max(1, std::min(F, (2048 + (N + 255) / 256 - 1) / ((N + 255) / 256)));
+  c->fchunk_w = (F + c->nchunk_w - 1) / c->nchunk_w;
+  c->nchunk_w = (F + c->fchunk_w - 1) / c->fchunk_w;
+  c->nb_alpha = std::max(1024, ((N + 255) / 256) * c->nchunk_w);
   const size_t FN = (size_t)F * N;
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
@@ -1103,7 +1323,6 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
     st = FASST_ERR_DEVICE;
   }
   if (const char *v = getenv("FASST_SIMM_BLAS")) c->use_blas = atoi(v);
-  if (const char *v = getenv("FASST_SIMM_FUSE_SM")) c->fuse_sm = atoi(v);
   size_t gw = 0;
   gw = std::max(gw, gemm_workspace(NF0, N, F, 2));
   gw = std::max(gw, gemm_workspace(F, N, NF0, 1));
@@ -1144,7 +1363,7 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   SA(sg, K);
   SA(sw, R);
   SA(hpart, (size_t)c->nchunk_h * 2 * K * N);
-  SA(hrows, (size_t)F * 2 * K);
+  SA(hrows, (size_t)kHgRowChunks * F * 2 * K);
   SA(apart, (size_t)c->nb_alpha * 4);
   SA(bd, 4 * (size_t)R);
   SA(gwork, std::max<size_t>(gw, 1));
