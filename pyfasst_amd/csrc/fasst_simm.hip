@@ -182,6 +182,9 @@ __global__ void k_simm_refresh(double *__restrict__ SF0, double *__restrict__ SP
   }
 }
 
+// bins per k_simm_sm block: every block re-reads its frames' HM columns
+// (R x 256 doubles), so 16-bin blocks read 1.25x the two planes they write
+constexpr int kSmRows = 64;
 // Accompaniment refresh (the step after every HM, WM and beta update,
 // SIMM.py:747-773, :826-869, :909-941): stereo SMR = (WM bR^2) HM,
 // SML = (WM bL^2) HM, mono SM = WM HM (R <= RMAX).  One thread per frame n
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void k_simm_sm(const double *__restrict__ WbR,
                                                  const double *__restrict__ HM,
                                                  double *__restrict__ SMR, double *__restrict__ SML,
                                                  int F, int N, int R, int stereo) {
-  constexpr int FB = 16;
+  constexpr int FB = kSmRows;
   const int n = blockIdx.x * 256 + threadIdx.x;
   const int f0 = blockIdx.y * FB;
   if (n >= N) return;
@@ -1110,15 +1113,24 @@ int refresh_sm_gemm(simm_ctx *c) {
 constexpr int kSmRmax = 48;
 int refresh_sm(simm_ctx *c) {
   if (c->R > kSmRmax) return refresh_sm_gemm(c);
-  const size_t FRP = (size_t)c->F * kSmRmax;
+  // WM (x beta^2) rows zero-padded to RP = R rounded up to 8 (the unrolled
+  // FMA count per point)
+  const int RP = (c->R + 7) / 8 * 8;
+  const size_t FRP = (size_t)c->F * RP;
   k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->stereo ? c->bR.p : nullptr,
-                                                   c->WMb.p, c->F, c->R, kSmRmax);
+                                                   c->WMb.p, c->F, c->R, RP);
   if (c->stereo)
-    k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->bL.p, c->WMb2.p, c->F, c->R,
-                                                     kSmRmax);
-  const dim3 grid((c->N + 255) / 256, (c->F + 15) / 16);
-  k_simm_sm<kSmRmax><<<grid, 256, 0, c->stream>>>(c->WMb.p, c->WMb2.p, c->HM.p, c->SMR.p,
-                                                  c->SML.p, c->F, c->N, c->R, c->stereo);
+    k_wm_beta_pad<<<egrid(FRP), 256, 0, c->stream>>>(c->WM.p, c->bL.p, c->WMb2.p, c->F, c->R, RP);
+  const dim3 grid((c->N + 255) / 256, (c->F + kSmRows - 1) / kSmRows);
+#define SM_CASE(RM)                                                                           \
+  case RM:                                                                                    \
+    k_simm_sm<RM><<<grid, 256, 0, c->stream>>>(c->WMb.p, c->WMb2.p, c->HM.p, c->SMR.p, c->SML.p, \
+                                               c->F, c->N, c->R, c->stereo);                  \
+    break;
+  switch (RP) {
+    SM_CASE(8) SM_CASE(16) SM_CASE(24) SM_CASE(32) SM_CASE(40) SM_CASE(48)
+  }
+#undef SM_CASE
   FASST_LAUNCH_CHECK();
   return FASST_OK;
 }
