@@ -1135,6 +1135,9 @@ struct BArgs {
 // DEN (several spectral components on source j, audioModel.py:1525-1571):
 // the numerator plane is (hat_W_j / V_j^2) other and a second plane
 // other / V_j is contracted into the denominator the same way.
+// Without DEN and FPW even the tiles are interleaved (bin f in tile f mod
+// FPW), so each lane's rho values arrive as 16-byte loads (C3: 0.166 ->
+// 0.155 ms at FPW = 2, same-box A/B).
 template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
@@ -1161,6 +1164,32 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int kc = 0; kc < NKC; ++kc) fb[i][kc] = fwh[(size_t)(4 * i) * a.KP + kc * 16];
+    if constexpr (FPW % 2 == 0 && !DEN) {
+      // the wave's FPW bin tiles interleaved: lane fl loads bins
+      // FPW fl .. FPW fl + FPW - 1 of the 16 FPW-bin group with 16-byte loads
+      // (tile p = the bins == p mod FPW): 4 rows x 16 FPW contiguous doubles
+      // per load instruction instead of 4 x 16
+      const int fp = ft0 * 16 + FPW * fl;
+      double r[FPW][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = t0 + tq + 4 * i < a.T && fp < a.Fp;
+        const double *src = rhoj + (size_t)(t0 + tq + 4 * i) * a.Fp + fp;
+#pragma unroll
+        for (int h = 0; h < FPW; h += 2) {
+          const double2 v = ok ? *(const double2 *)(src + h) : make_double2(0.0, 0.0);
+          r[h][i] = v.x;
+          r[h + 1][i] = v.y;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < FPW; ++p)
+#pragma unroll
+          for (int kc = 0; kc < NKC; ++kc) num[p][kc] = mfma4(r[p][i], fb[i][kc], num[p][kc]);
+      continue;
+    }
 #pragma unroll
     for (int p = 0; p < FPW; ++p) {
       if (ft0 + p >= a.nft) break;  // wave-uniform: no bin tile left
@@ -1186,6 +1215,18 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
     }
   }
   const size_t base = ((size_t)(a.zbase + blockIdx.z) * a.J + j) * a.Fp;
+  if constexpr (FPW % 2 == 0 && !DEN) {   // interleaved tiles: tile p holds bins p mod FPW
+#pragma unroll
+    for (int p = 0; p < FPW; ++p)
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int f = ft0 * 16 + FPW * (tq + 4 * m) + p;
+          if (f < a.Fp) a.bnum[(base + f) * a.KP + kc * 16 + fl] = num[p][kc][m];
+        }
+    return;
+  }
 #pragma unroll
   for (int p = 0; p < FPW; ++p) {
     if (ft0 + p >= a.nft) break;
@@ -1540,9 +1581,16 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int fb = blockIdx.z * a.fpc, fe = min(fb + a.fpc, a.nft);
-  const double *wo = a.Wkf_old + ((size_t)j * a.KP + tq) * a.Fp + fl;
-  const double *wn = a.Wkf_new + ((size_t)j * a.KP + tq) * a.Fp + fl;
-  const double *wfk = a.Wfk_new + ((size_t)j * a.Fp + tq) * a.KP + fl;
+  // the V tiles' bin rows are permuted (lane fl's A row is bin
+  // 4 (fl & 3) + (fl >> 2)) so that a lane's four D values are the four
+  // consecutive bins 4 tq .. 4 tq + 3: its rho values arrive as two 16-byte
+  // loads (C3: 0.401 -> 0.381 ms, same-box A/B); the contraction's B rows
+  // (W_new) follow the same order
+  const int fpl = 4 * (fl & 3) + (fl >> 2);
+  const int bq = 4 * tq, bs = 1;   // D value i is bin f0 + bq + bs i
+  const double *wo = a.Wkf_old + ((size_t)j * a.KP + tq) * a.Fp + fpl;
+  const double *wn = a.Wkf_new + ((size_t)j * a.KP + tq) * a.Fp + fpl;
+  const double *wfk = a.Wfk_new + ((size_t)j * a.Fp + bq) * a.KP + fl;
   const double *hwj = a.hatW + (size_t)j * a.Tp * a.Fp;
   for (int ft = fb; ft < fe; ++ft) {
     const int f0 = ft * 16;
@@ -1559,15 +1607,21 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) bw[i][kc] = wfk[(size_t)(f0 + 4 * i) * a.KP + kc * 16];
+      for (int kc = 0; kc < NKC; ++kc) bw[i][kc] = wfk[(size_t)(f0 + bs * i) * a.KP + kc * 16];
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
       if (tt0 + p >= a.ntt) break;  // wave-uniform: no frame tile left
       const int t = (tt0 + p) * 16 + fl;
       double h[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)  // (last use of rho: non-temporal)
-        h[i] = __builtin_nontemporal_load(hwj + (size_t)t * a.Fp + f0 + tq + 4 * i);
+      {  // (last use of rho: non-temporal)
+        typedef double dv2 __attribute__((ext_vector_type(2)));
+        const dv2 *hp = (const dv2 *)(hwj + (size_t)t * a.Fp + f0 + bq);
+        const dv2 h01 = __builtin_nontemporal_load(hp), h23 = __builtin_nontemporal_load(hp + 1);
+        h[0] = h01.x;
+        h[1] = h01.y;
+        h[2] = h23.x;
+        h[3] = h23.y;
+      }
       d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
@@ -1586,8 +1640,8 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       for (int i = 0; i < 4; ++i) {
         const double vm = fmax(vn[i], kEps);
         const double rv = rcp_nr(vm);
-        const bool ok = tok && f0 + tq + 4 * i < a.F;
-        const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + tq + 4 * i;
+        const bool ok = tok && f0 + bq + bs * i < a.F;
+        const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + bq + bs * i;
         double other, q;
         if constexpr (TBQ) {
           other = ok ? a.oth[o] : 0.0;
