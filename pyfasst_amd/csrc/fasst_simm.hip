@@ -1301,7 +1301,7 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
 extern "C" {
 
 int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int stereo, simm_ctx **out) {
-  if (!out || F < 1 || N < 1 || NF0 < 1 || P < 1 || K < 1 || K > 8 || R < 1 || P * K > 512) {
+  if (!out || F < 1 || N < 1 || NF0 < 1 || P < 1 || K < 1 || K > kSimmKmax || R < 1 || P * K > 512) {
     set_error("simm_create: unsupported sizes F=%d N=%d NF0=%d P=%d K=%d R=%d", F, N, NF0, P, K, R);
     return FASST_ERR_SHAPE;
   }
