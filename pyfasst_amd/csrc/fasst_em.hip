@@ -871,15 +871,21 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 // stored for k_mix_inst.
 __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   HALT_GUARD(a.halt);
-  __shared__ double s_acc[4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ];
-  __shared__ double2 s_A[kMaxR][2];
-  __shared__ double2 s_L[kMaxR][kMaxR + 2];   // [M^T | hat_Rxs^T]
-  __shared__ double2 s_H[kMaxR][kMaxR];
-  __shared__ double2 s_mult[kMaxR];
-  __shared__ double s_sv[kMaxJ];
-  __shared__ double s_wh[2][kMaxJ * kMaxKP];   // W_j(f, k), sum_t TW_j(k, t)
+  // LDS sized by this model's J, R, KP (mix_smem): with the kMaxJ / kMaxR /
+  // kMaxKP ceilings a block took 19 KB, so only 8 blocks fit a CU and the
+  // 2049 bins of C3 ran as two rounds of the whole latency chain
+  extern __shared__ __attribute__((aligned(16))) double s_mix[];
   const int f = blockIdx.x, lane = threadIdx.x;
   const int J = a.J, R = a.R, NACC = a.nacc;
+  const int W = R + 2;
+  double2 *s_A = (double2 *)s_mix;           // [R][2]
+  double2 *s_L = s_A + 2 * R;                // [R][R + 2]: [M^T | hat_Rxs^T]
+  double2 *s_H = s_L + R * W;                // [R][R]
+  double2 *s_mult = s_H + R * R;             // [R]
+  double *s_acc = (double *)(s_mult + R);    // [NACC]
+  double *s_sv = s_acc + NACC;               // [J]
+  double *s_wh0 = s_sv + J;                  // [J * KP] W_j(f, k)
+  double *s_wh1 = s_wh0 + J * a.KP;          // [J * KP] sum_t TW_j(k, t)
   const int NP = J * (J + 1) / 2;
   {  // NACC = 72 > 64 lanes for J = 4: a lane sums up to 4 statistics, the
      // loads of all of them for 8 chunks in flight together (chunk order kept)
@@ -903,18 +909,18 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     for (int q = 0; q < kQ; ++q)
       if (lane + 64 * q < NACC) s_acc[lane + 64 * q] = x[q];
   }
-  if (lane < 2 * R) s_A[lane >> 1][lane & 1] = a.A[(size_t)lane * a.Fp + f];
+  if (lane < 2 * R) s_A[(lane >> 1) * 2 + (lane & 1)] = a.A[(size_t)lane * a.Fp + f];
   // sum_t V_j(f, t) = sum_k W_j(f, k) sum_t TW_j(k, t): the operands are
   // loaded by all lanes at once (a per-source loop over k was a chain of
   // global-latency round trips), then summed in k order
   for (int i = lane; i < J * a.KP; i += 64) {
-    s_wh[0][i] = a.Wkf[(size_t)i * a.Fp + f];
-    s_wh[1][i] = a.hsum[i];
+    s_wh0[i] = a.Wkf[(size_t)i * a.Fp + f];
+    s_wh1[i] = a.hsum[i];
   }
   __syncthreads();
   if (lane < J) {
     double sv = 0.0;
-    for (int k = 0; k < a.KP; ++k) sv += s_wh[0][lane * a.KP + k] * s_wh[1][lane * a.KP + k];
+    for (int k = 0; k < a.KP; ++k) sv += s_wh0[lane * a.KP + k] * s_wh1[lane * a.KP + k];
     s_sv[lane] = sv;
   }
   __syncthreads();
@@ -926,14 +932,14 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     const int p = lo * J - lo * (lo - 1) / 2 + (hi - lo);
     const double n00 = s_acc[4 * p], n11 = s_acc[4 * p + 1];
     const double2 n01 = make_double2(s_acc[4 * p + 2], s_acc[4 * p + 3]);
-    const double2 c10 = cconj(s_A[r1][0]), c11 = cconj(s_A[r1][1]);
-    double2 v = cscale(cmul(c10, s_A[r2][0]), n00);               // a_r1^H Nsum a_r2
-    v = cadd(v, cmul(cmul(c10, n01), s_A[r2][1]));
-    v = cadd(v, cmul(cmul(c11, cconj(n01)), s_A[r2][0]));
-    v = cadd(v, cscale(cmul(c11, s_A[r2][1]), n11));
+    const double2 c10 = cconj(s_A[(r1) * 2 + (0)]), c11 = cconj(s_A[(r1) * 2 + (1)]);
+    double2 v = cscale(cmul(c10, s_A[(r2) * 2 + (0)]), n00);               // a_r1^H Nsum a_r2
+    v = cadd(v, cmul(cmul(c10, n01), s_A[(r2) * 2 + (1)]));
+    v = cadd(v, cmul(cmul(c11, cconj(n01)), s_A[(r2) * 2 + (0)]));
+    v = cadd(v, cscale(cmul(c11, s_A[(r2) * 2 + (1)]), n11));
     v = cscale(v, a.invT);
     if (r1 == r2) v.x += s_sv[j1] * a.invT;
-    s_H[r1][r2] = v;
+    s_H[(r1) * R + (r2)] = v;
   }
   __syncthreads();
   double2 hv[4];  // hermitised entries of this lane (e = lane + 64 q)
@@ -943,7 +949,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     hv[q] = make_double2(0.0, 0.0);
     if (e < R * R) {
       const int r1 = e / R, r2 = e % R;
-      const double2 x = s_H[r1][r2], y = s_H[r2][r1];
+      const double2 x = s_H[(r1) * R + (r2)], y = s_H[(r2) * R + (r1)];
       hv[q] = cscale(cadd(x, cconj(y)), 0.5);
     }
   }
@@ -952,7 +958,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     const double *qq = s_acc + 4 * NP + 8 * a.jr[r];
     const double2 q0 = make_double2(qq[4 * c + 0], qq[4 * c + 1]);
     const double2 q1 = make_double2(qq[4 * c + 2], qq[4 * c + 3]);
-    s_L[r][R + c] = cscale(cadd(cmul(q0, s_A[r][0]), cmul(q1, s_A[r][1])), a.invT);
+    s_L[(r) * W + (R + c)] = cscale(cadd(cmul(q0, s_A[(r) * 2 + (0)]), cmul(q1, s_A[(r) * 2 + (1)])), a.invT);
   }
   if (!a.conv_update) {
     __syncthreads();
@@ -964,7 +970,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
       }
       if (lane < 2 * R) {
         const int r = lane >> 1, c = lane & 1;
-        a.rxs[((size_t)f * 2 + c) * R + r] = s_L[r][R + c];
+        a.rxs[((size_t)f * 2 + c) * R + r] = s_L[(r) * W + (R + c)];
       }
     }
     return;
@@ -972,16 +978,15 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {  // L = hermitised(hat_Rss)^T
     const int e = lane + 64 * q;
-    if (e < R * R) s_L[e % R][e / R] = hv[q];
+    if (e < R * R) s_L[(e % R) * W + (e / R)] = hv[q];
   }
   __syncthreads();
-  const int W = R + 2;
   for (int k = 0; k < R; ++k) {
     // pivot: first row i >= k maximising |re|+|im| of L[i][k]
     double m = -1.0;
     int mi = R;
     if (lane >= k && lane < R) {
-      m = fabs(s_L[lane][k].x) + fabs(s_L[lane][k].y);
+      m = fabs(s_L[(lane) * W + (k)].x) + fabs(s_L[(lane) * W + (k)].y);
       mi = lane;
     }
 #pragma unroll
@@ -1001,29 +1006,34 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
       return;
     }
     if (mi != k && lane < W) {
-      const double2 t = s_L[k][lane];
-      s_L[k][lane] = s_L[mi][lane];
-      s_L[mi][lane] = t;
+      const double2 t = s_L[(k) * W + (lane)];
+      s_L[(k) * W + (lane)] = s_L[(mi) * W + (lane)];
+      s_L[(mi) * W + (lane)] = t;
     }
     __syncthreads();
-    if (lane > k && lane < R) s_mult[lane] = cmul(s_L[lane][k], cdiv(make_double2(1.0, 0.0), s_L[k][k]));
+    if (lane > k && lane < R) s_mult[lane] = cmul(s_L[(lane) * W + (k)], cdiv(make_double2(1.0, 0.0), s_L[(k) * W + (k)]));
     __syncthreads();
     const int nr = R - k - 1, nc = W - k - 1;
     for (int e = lane; e < nr * nc; e += 64) {
       const int i = k + 1 + e / nc, c = k + 1 + e % nc;
-      s_L[i][c] = csub(s_L[i][c], cmul(s_mult[i], s_L[k][c]));
+      s_L[(i) * W + (c)] = csub(s_L[(i) * W + (c)], cmul(s_mult[i], s_L[(k) * W + (c)]));
     }
     __syncthreads();
   }
   for (int i = R - 1; i >= 0; --i) {
     if (lane < 2) {
-      double2 x = s_L[i][R + lane];
-      for (int q = i + 1; q < R; ++q) x = csub(x, cmul(s_L[i][q], s_L[q][R + lane]));
-      s_L[i][R + lane] = cdiv(x, s_L[i][i]);
+      double2 x = s_L[(i) * W + (R + lane)];
+      for (int q = i + 1; q < R; ++q) x = csub(x, cmul(s_L[(i) * W + (q)], s_L[(q) * W + (R + lane)]));
+      s_L[(i) * W + (R + lane)] = cdiv(x, s_L[(i) * W + (i)]);
     }
     __syncthreads();
   }
-  if (lane < 2 * R) a.A[(size_t)lane * a.Fp + f] = s_L[lane >> 1][R + (lane & 1)];
+  if (lane < 2 * R) a.A[(size_t)lane * a.Fp + f] = s_L[(lane >> 1) * W + (R + (lane & 1))];
+}
+
+static size_t mix_smem(int J, int R, int KP, int nacc) {
+  return (size_t)(2 * R + R * (R + 2) + R * R + R) * sizeof(double2) +
+         (size_t)(nacc + J + 2 * J * KP) * sizeof(double);
 }
 
 // 'inst' update (:808-839): f-means of the statistics, real R_u x R_u solve.
@@ -3204,7 +3214,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     for (int j = 0; j < J; ++j)
       for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
     prof_begin(c, KMIX);
-    k_mix<<<c->F, 64, 0, c->stream>>>(m);
+    k_mix<<<c->F, 64, mix_smem(J, c->R, c->KP, c->nacc), c->stream>>>(m);
     prof_end(c, KMIX);
     FASST_LAUNCH_CHECK();
     if (!c->conv) {
