@@ -92,7 +92,7 @@ struct SPl {
 // frame n walking a chunk of bins (grid: N/256 x F chunks).
 template <bool ST, int KM>
 __global__ __launch_bounds__(256) void k_simm_numden(const SPl p, double *__restrict__ num,
-                                                     double *__restrict__ den) {
+                                                     double *__restrict__ den, size_t ldo) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= p.N) return;
   const int fb = blockIdx.y * p.fchunk, fe = min(p.F, fb + p.fchunk);
@@ -110,13 +110,24 @@ __global__ __launch_bounds__(256) void k_simm_numden(const SPl p, double *__rest
     if constexpr (ST) {
       const double com = aR2 * sp / hr;
       const double d = aL2 * sp / hl;
-      SST(num[i], com * CLD(p.SXR[i]) / hr + d * CLD(p.SXL[i]) / hl);
-      SST(den[i], d + com);
+      SST(num[(size_t)f * ldo + n], com * CLD(p.SXR[i]) / hr + d * CLD(p.SXL[i]) / hl);
+      SST(den[(size_t)f * ldo + n], d + com);
     } else {
       const double d = sp / hr;
-      SST(den[i], d);
-      SST(num[i], (d * CLD(p.SXR[i])) / hr);
+      SST(den[(size_t)f * ldo + n], d);
+      SST(num[(size_t)f * ldo + n], (d * CLD(p.SXR[i])) / hr);
     }
+  }
+}
+
+// HF0 *= (num / max(den, eps))^omega with num / den the two halves of the
+// rows of NP = WF0^T [num | den] (row stride 2N)
+__global__ void k_mu_apply_nd(double *__restrict__ X, const double *__restrict__ NP, int R, int N,
+                              double omega) {
+  GRID_STRIDE(i, (size_t)R * N) {
+    const size_t r = i / N, n = i % N;
+    const double num = NP[r * 2 * N + n], den = NP[r * 2 * N + N + n];
+    X[i] *= powo(num / fmax(den, kSimmEps), omega);
   }
 }
 
@@ -927,7 +938,7 @@ struct simm_ctx {
   // refresh_hat (rebuild_model, the R > 48 path)
   const double *pend = nullptr;
   DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
-  DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, NP0, NP1, WMb, WMb2, s_col, sg, sw;
+  DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, TND, NPD, WMb, WMb2, s_col, sg, sw;
   DBuf<double> hpart, hrows, apart, bd, gwork, P0, P1, P2, P3, RN0, RN1, reco;
 };
 
@@ -1186,24 +1197,25 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     const SPl p = planes(c, false);   // (no scale is pending at the iteration start)
     kdispatch(K, [&](auto km) {
       constexpr int KM = decltype(km)::value;
+      // num | den side by side in the rows of TND (row stride 2N)
       if (ST)
-        k_simm_numden<true, KM><<<wg, 256, 0, c->stream>>>(p, c->T0.p, c->T1.p);
+        k_simm_numden<true, KM><<<wg, 256, 0, c->stream>>>(p, c->TND.p, c->TND.p + N, 2 * (size_t)N);
       else
-        k_simm_numden<false, KM><<<wg, 256, 0, c->stream>>>(p, c->T0.p, c->T1.p);
+        k_simm_numden<false, KM><<<wg, 256, 0, c->stream>>>(p, c->TND.p, c->TND.p + N, 2 * (size_t)N);
     });
   }
-  if (c->use_blas) {  // WF0^T {num, den}: (NF0 x F)(F x N)
-    if ((st = blas_gemm(c->blas, true, false, NF0, N, F, c->WF0.p, NF0, c->T0.p, N, c->NP0.p, N)) ||
-        (st = blas_gemm(c->blas, true, false, NF0, N, F, c->WF0.p, NF0, c->T1.p, N, c->NP1.p, N)))
+  if (c->use_blas) {  // WF0^T [num | den]: one (NF0 x F)(F x 2N) product
+    if ((st = blas_gemm(c->blas, true, false, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p,
+                        2 * N)))
       return st;
   } else {
-    const double *Bs[2] = {c->T0.p, c->T1.p};
-    double *Cs[2] = {c->NP0.p, c->NP1.p};
-    if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, N, Cs, N, NF0, N, F, c->gwork.p)))
+    const double *Bs[2] = {c->TND.p, c->TND.p + N};
+    double *Cs[2] = {c->NPD.p, c->NPD.p + N};
+    if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, 2 * N, Cs, 2 * N, NF0, N, F,
+                                   c->gwork.p)))
       return st;
   }
-  k_mu_apply<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->NP0.p, c->NP1.p,
-                                                             (size_t)NF0 * N, omega, 0);
+  k_mu_apply_nd<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->NPD.p, NF0, N, omega);
   if ((st = sf0_gemm(c))) return st;
   if (reco) reco_error(c, reco);
   // ---- HPHI (:686-729 / :296-313)
@@ -1336,7 +1348,7 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   }
   if (const char *v = getenv("FASST_SIMM_BLAS")) c->use_blas = atoi(v);
   size_t gw = 0;
-  gw = std::max(gw, gemm_workspace(NF0, N, F, 2));
+  gw = std::max(gw, gemm_workspace(NF0, 2 * N, F, 2));   // (num | den rows: ldc = 2N)
   gw = std::max(gw, gemm_workspace(F, N, NF0, 1));
   gw = std::max(gw, gemm_workspace(F, N, R, 1));
   gw = std::max(gw, gemm_workspace(R, N, F, stereo ? 4 : 2));
@@ -1367,8 +1379,8 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   SA(T1, FN);
   SA(T2, stereo ? FN : 1);
   SA(T3, stereo ? FN : 1);
-  SA(NP0, (size_t)NF0 * N);
-  SA(NP1, (size_t)NF0 * N);
+  SA(TND, 2 * FN);
+  SA(NPD, 2 * (size_t)NF0 * N);
   SA(WMb, (size_t)F * std::max(R, 48));  // (48 = kSmRmax: padded rows of the fused refresh)
   SA(WMb2, (size_t)F * std::max(R, 48));
   SA(s_col, N);
