@@ -270,6 +270,15 @@ def main():
                       "traffic": iter_traffic,
                       "traffic_ratio": round(iter_traffic / itw["B_alg"], 3) if iter_traffic
                       else None}}
+        if rl is not None:
+            # every timed kernel of the iteration on its algorithmic work (the
+            # dominant one above; the TW contraction is the kernel VERDICT names)
+            rl["kernels"] = {
+                k: {"ms": round(times[k][0], 4),
+                    "tflops": round(work[k]["flops"] / (times[k][0] * 1e-3) / 1e12, 3),
+                    "frac": round(work[k]["flops"] / (times[k][0] * 1e-3) / FP64_MFMA_PEAK, 4),
+                    "gbps": round(work[k]["bytes"] / (times[k][0] * 1e-3) / 1e9, 1)}
+                for k in ("k_estep", "k_tw_contract", "k_fb_contract") if k in times and k in work}
         out = {
             "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",
             "value": round(job_value(world, args.steps, dt), 4),
