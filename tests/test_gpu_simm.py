@@ -86,7 +86,9 @@ def _data(F, N, NF0, P, seed):
 # takes the fused skinny kernels (R = 40: the pipeline's numCompAccomp),
 # R = 60 the materialised X, Y + general GEMM
 SHAPES = [(257, 301, 97, 10, 4, 7), (1025, 130, 150, 12, 4, 10), (129, 600, 40, 5, 2, 3),
-          (33, 17, 5, 3, 1, 1), (200, 1300, 30, 6, 2, 40), (97, 150, 20, 4, 2, 60)]
+          (33, 17, 5, 3, 1, 1), (200, 1300, 30, 6, 2, 40), (97, 150, 20, 4, 2, 60),
+          # K in (4, 8]: the 8-filter instantiations of the model-forming kernels
+          (129, 333, 24, 7, 6, 48), (65, 90, 16, 5, 8, 52)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -104,7 +106,7 @@ def test_stereo_simm_vs_oracle(shape):
     _cmp(got, want, ST_NAMES, tol=1e-8)
 
 
-@pytest.mark.parametrize("shape", SHAPES[:2])
+@pytest.mark.parametrize("shape", SHAPES[:2] + SHAPES[6:7])
 def test_mono_simm_vs_oracle(shape):
     F, N, NF0, P, K, _ = shape
     SX, _, WF0, WG = _data(F, N, NF0, P, 6)
