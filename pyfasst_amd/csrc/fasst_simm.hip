@@ -40,6 +40,12 @@ __device__ __forceinline__ double powo(double x, double omega) {
 
 constexpr int kSimmKmax = 8;  // simm_create: K <= 8 filters
 constexpr int kHgRowChunks = 4;  // frame chunks of k_hgamma_rows (>= 4 waves per SIMD at C5)
+// bins per k_hgamma_rows block: 2 halves its accumulators and doubles the
+// blocks (C5 8.92 -> 8.74 ms per iteration vs 4 bins; 1 bin the same as 2)
+#ifndef FASST_HG_ROWS
+#define FASST_HG_ROWS 2
+#endif
+constexpr int kHgRows = FASST_HG_ROWS;
 
 // ---------------------------------------------------------------------------
 // The model spectrograms are not stored between updates.  Every update of the
@@ -551,7 +557,7 @@ __global__ void k_colscale(double *__restrict__ X, const double *__restrict__ s,
 // [chunk][F][2K], summed in chunk order by k_hgamma_numden).
 template <bool ST, int KM>
 __global__ __launch_bounds__(256) void k_hgamma_rows(const SPl p, double *__restrict__ out) {
-  constexpr int FB = 4;  // frequency rows per block: each HPHI load serves FB rows
+  constexpr int FB = kHgRows;  // frequency rows per block: each HPHI load serves FB rows
   __shared__ double s_red[FB * 2 * KM][4];
   const int F = p.F, N = p.N, K = p.K;
   const int f0 = blockIdx.x * FB, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1257,9 +1263,9 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     kdispatch(K, [&](auto km) {
       constexpr int KM = decltype(km)::value;
       if (ST)
-        k_hgamma_rows<true, KM><<<dim3((F + 3) / 4, kHgRowChunks), 256, 0, c->stream>>>(p, c->hrows.p);
+        k_hgamma_rows<true, KM><<<dim3((F + kHgRows - 1) / kHgRows, kHgRowChunks), 256, 0, c->stream>>>(p, c->hrows.p);
       else
-        k_hgamma_rows<false, KM><<<dim3((F + 3) / 4, kHgRowChunks), 256, 0, c->stream>>>(p, c->hrows.p);
+        k_hgamma_rows<false, KM><<<dim3((F + kHgRows - 1) / kHgRows, kHgRowChunks), 256, 0, c->stream>>>(p, c->hrows.p);
     });
     k_hgamma_numden<<<c->P, 256, 0, c->stream>>>(c->WGAMMA.p, c->hrows.p, c->apart.p, F, c->P, K,
                                                  kHgRowChunks);
