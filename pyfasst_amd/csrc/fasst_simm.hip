@@ -943,6 +943,7 @@ struct simm_ctx {
   // next kernel that streams SF0; SPHI / hR / hL hold the model only after
   // refresh_hat (rebuild_model, the R > 48 path)
   const double *pend = nullptr;
+  long slots = 512;   // resident blocks of the skinny products (2 per CU)
   DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
   DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, TND, NPD, WMb, WMb2, s_col, sg, sw;
   DBuf<double> hpart, hrows, apart, bd, gwork, P0, P1, P2, P3, RN0, RN1, reco;
@@ -971,25 +972,49 @@ constexpr int kWmtMaxChunk = 512;   // bins per k_simm_wmt_xy block (its LDS WPH
 struct SkinnySplit {
   int nz, kchunk;
 };
-static SkinnySplit wmt_split(int F, int N) {
+// split count for `units` blocks per split when `slots` blocks (two per CU)
+// are resident: the smallest nz in [lo, hi] whose last round is >= 95% full,
+// else the fullest (C5: k_simm_xy_hmt 33 x 15 blocks, one round instead of
+// 33 x 16 with a 16-block tail; k_simm_wmt_xy 313 x 8: 8.70 -> 8.60 ms)
+static int round_split(long units, int lo, int hi, long slots) {
+  hi = std::max(lo, hi);
+  int best = lo;
+  double beff = 0.0;
+  for (int nz = lo; nz <= hi; ++nz) {
+    const long b = units * nz, rounds = (b + slots - 1) / slots;
+    const double eff = (double)b / (double)(rounds * slots);
+    if (eff >= 0.95) return nz;
+    if (eff > beff) {
+      beff = eff;
+      best = nz;
+    }
+  }
+  return best;
+}
+static SkinnySplit wmt_split(int F, int N, long slots) {
   const long bx = (N + 63) / 64;
-  int nz = 1;
-  while (bx * nz < 1024 && F / (2 * nz) >= 64) nz *= 2;
-  nz = std::max(nz, (F + kWmtMaxChunk - 1) / kWmtMaxChunk);   // WPHI rows fit the LDS
+  // >= 4 blocks per slot ring, chunks of >= 64 bins, WPHI rows in the LDS
+  const int lo = std::max(std::max(1, (F + kWmtMaxChunk - 1) / kWmtMaxChunk),
+                          (int)std::min<long>(16, (2 * slots + bx - 1) / bx));
+  int nz = round_split(bx, lo, std::max(lo, std::min(16, F / 64)), slots);
+  if (const char *v = getenv("FASST_WMT_NZ")) nz = std::max(1, atoi(v));   // A/B knob
+  nz = std::max(nz, (F + kWmtMaxChunk - 1) / kWmtMaxChunk);
   const int kchunk = ((F + nz - 1) / nz + 15) / 16 * 16;
   return {(F + kchunk - 1) / kchunk, kchunk};
 }
-static SkinnySplit hmt_split(int F, int N) {
+static SkinnySplit hmt_split(int F, int N, long slots) {
   const long by = (F + 63) / 64;
-  int nz = 1;
-  while (by * nz < 512 && N / (2 * nz) >= 256) nz *= 2;
+  const int hi = std::max(1, std::min(32, N / 256));
+  int nz = round_split(by, std::min(hi, (int)std::max<long>(1, slots / (2 * by))), hi, slots);
+  if (const char *v = getenv("FASST_HMT_NZ")) nz = std::max(1, atoi(v));   // A/B knob
   const int kchunk = ((N + nz - 1) / nz + 31) / 32 * 32;
   return {(N + kchunk - 1) / kchunk, kchunk};
 }
-static size_t skinny_workspace(int F, int N, int R, int stereo) {
+static size_t skinny_workspace(int F, int N, int R, int stereo, long slots) {
   if (R > 48) return 0;
   const size_t no = stereo ? 4 : 2;
-  return std::max((size_t)wmt_split(F, N).nz * no * R * N, (size_t)hmt_split(F, N).nz * no * F * R);
+  return std::max((size_t)wmt_split(F, N, slots).nz * no * R * N,
+                  (size_t)hmt_split(F, N, slots).nz * no * F * R);
 }
 
 void reduce_slabs(simm_ctx *c, int no, int nz, size_t n, double *const *dst) {
@@ -1056,7 +1081,7 @@ int wmt_xy(simm_ctx *c, double *const *dst) {
     return c->stereo ? gemm<true, false, 4>(c->stream, c->WM.p, R, Bs, N, dst, N, R, N, F, c->gwork.p)
                      : gemm<true, false, 2>(c->stream, c->WM.p, R, Bs, N, dst, N, R, N, F, c->gwork.p);
   }
-  const SkinnySplit sp = wmt_split(F, N);
+  const SkinnySplit sp = wmt_split(F, N, c->slots);
   const size_t slab = (size_t)no * R * N;
   dim3 grid((N + 63) / 64, 1, sp.nz);
   const SPl p = planes(c, true);
@@ -1095,7 +1120,7 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
     }
     return FASST_OK;
   }
-  const SkinnySplit sp = hmt_split(F, N);
+  const SkinnySplit sp = hmt_split(F, N, c->slots);
   const size_t slab = (size_t)no * F * R;
   dim3 grid(1, (F + 63) / 64, sp.nz);
   const SPl p = planes(c, true);
@@ -1359,7 +1384,14 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   gw = std::max(gw, gemm_workspace(F, N, R, 1));
   gw = std::max(gw, gemm_workspace(R, N, F, stereo ? 4 : 2));
   gw = std::max(gw, gemm_workspace(F, R, N, 1));
-  gw = std::max(gw, skinny_workspace(F, N, R, stereo));
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+    c->slots = 2L * ncu;   // resident 256-thread blocks of the skinny products
+  }
+  gw = std::max(gw, skinny_workspace(F, N, R, stereo, c->slots));
 #define SA(buf, n) \
   if (!st) st = c->buf.alloc(n)
   SA(SXR, FN);
