@@ -253,8 +253,19 @@ def main():
             traffic = None
             if pmc and dom in pmc and pmc[dom].get("hbm_bytes_per_launch"):
                 traffic = pmc[dom]["hbm_bytes_per_launch"]
-            rl = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_MFMA_PEAK / 1e12,
-                  "unit": "TFLOP/s", "frac": round(achieved * 1e12 / FP64_MFMA_PEAK, 4),
+            # the binding roofline of the kernel: HBM when its algorithmic
+            # bytes take longer at HBM_PEAK than its flops at the FP64 MFMA peak
+            hbm_bound = work[dom]["bytes"] / HBM_PEAK > work[dom]["flops"] / FP64_MFMA_PEAK
+            if hbm_bound:
+                achieved = work[dom]["bytes"] / sec / 1e9
+                rl = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
+                      "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4),
+                      "tflops": round(work[dom]["flops"] / sec / 1e12, 3)}
+            else:
+                rl = {"bound": "mfma", "achieved": round(achieved, 3),
+                      "peak": FP64_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+                      "frac": round(achieved * 1e12 / FP64_MFMA_PEAK, 4)}
+            rl.update({
                   "traffic": traffic, "kernel": dom, "kernel_ms": round(times[dom][0], 4),
                   "dtype": "f64", "algorithmic_flops": work[dom]["flops"],
                   "executed_flops": work[dom]["exec_flops"],
@@ -269,7 +280,7 @@ def main():
                       "B_alg": itw["B_alg"], "F_mfma": itw["F_mfma"], "F_valu": itw["F_valu"],
                       "traffic": iter_traffic,
                       "traffic_ratio": round(iter_traffic / itw["B_alg"], 3) if iter_traffic
-                      else None}}
+                      else None}})
         if rl is not None:
             # every timed kernel of the iteration on its algorithmic work (the
             # dominant one above; the TW contraction is the kernel VERDICT names)
@@ -277,7 +288,10 @@ def main():
                 k: {"ms": round(times[k][0], 4),
                     "tflops": round(work[k]["flops"] / (times[k][0] * 1e-3) / 1e12, 3),
                     "frac": round(work[k]["flops"] / (times[k][0] * 1e-3) / FP64_MFMA_PEAK, 4),
-                    "gbps": round(work[k]["bytes"] / (times[k][0] * 1e-3) / 1e9, 1)}
+                    "gbps": round(work[k]["bytes"] / (times[k][0] * 1e-3) / 1e9, 1),
+                    "hbm_frac": round(work[k]["bytes"] / (times[k][0] * 1e-3) / HBM_PEAK, 4),
+                    "bound": "hbm" if work[k]["bytes"] / HBM_PEAK
+                    > work[k]["flops"] / FP64_MFMA_PEAK else "mfma"}
                 for k in ("k_estep", "k_tw_contract", "k_fb_contract") if k in times and k in work}
         out = {
             "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",
