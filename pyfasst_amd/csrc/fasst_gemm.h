@@ -376,6 +376,12 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
 // doubles of `work` gemm() needs for these sizes (0: no split)
 size_t gemm_workspace(int M, int N, int K, int NB);
 
+// Large plain products (the Stereo_SIMM NF0-sized ones): row-major
+// C (M x N) = op(A) B on k_dgemm (fasst_dgemm.h).  Returns FASST_ERR_SHAPE
+// without launching when the operands miss its 16-byte alignment.
+int dgemm(hipStream_t s, bool ta, int M, int N, int K, const double *A, int lda, const double *B,
+          int ldb, double *C, int ldc);
+
 // Plain (unfused) large products go to rocBLAS dgemm: row-major
 // C (M x N) = op(A) op(B) with op = transpose when ta / tb, issued on the
 // stream the handle is bound to.  rocBLAS's Tensile kernels (the same

@@ -2,6 +2,7 @@
 // slab reduction.  Explicit instantiations cover the operand forms the NMF
 // and SIMM updates use.
 #include "fasst_gemm.h"
+#include "fasst_dgemm.h"
 
 #include <algorithm>
 
@@ -150,6 +151,52 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
     }
     FASST_LAUNCH_CHECK();
   }
+  return FASST_OK;
+}
+
+// Large plain products on k_dgemm (fasst_dgemm.h).  FASST_ERR_SHAPE (no
+// launch, no error text) when the 16-byte alignment k_dgemm needs does not
+// hold: the caller then takes k_gemm.
+int dgemm(hipStream_t s, bool ta, int M, int N, int K, const double *A, int lda, const double *B,
+          int ldb, double *C, int ldc) {
+  const bool ok = M > 0 && N > 0 && K > 0 && lda % 2 == 0 && ldb % 2 == 0 && N % 2 == 0 &&
+                  (ta ? M % 2 == 0 : K % 2 == 0) && ((uintptr_t)A & 15) == 0 &&
+                  ((uintptr_t)B & 15) == 0;
+  if (!ok) return FASST_ERR_SHAPE;
+  DgemmArgs g;
+  g.A = A;
+  g.B = B;
+  g.C = C;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.mt = (M + kDBM - 1) / kDBM;
+  g.nt = (N + kDBN - 1) / kDBN;
+  g.order = 0;
+  const int nb = (g.mt * g.nt + 7) / 8 * 8;
+  if (ta) {
+    static bool attr = false;
+    if (!attr) {
+      FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)dgemm_smem<true>()));
+      attr = true;
+    }
+    k_dgemm<true><<<nb, 256, dgemm_smem<true>(), s>>>(g);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)dgemm_smem<false>()));
+      attr = true;
+    }
+    k_dgemm<false><<<nb, 256, dgemm_smem<false>(), s>>>(g);
+  }
+  FASST_LAUNCH_CHECK();
   return FASST_OK;
 }
 

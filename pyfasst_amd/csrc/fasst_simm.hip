@@ -935,7 +935,9 @@ struct simm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   rocblas_handle blas = nullptr;  // bound to `stream`: the NF0-sized plain GEMMs
-  int use_blas = 1;               // FASST_SIMM_BLAS=0: k_gemm instead (A/B only)
+  // NF0-sized plain products: 0 = k_dgemm (hand-written, default), 1 =
+  // rocBLAS dgemm, 2 = k_gemm (FASST_SIMM_BLAS, A/B only)
+  int use_blas = 1;
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
   int nchunk_w = 1, fchunk_w = 1;  // the frame-walker grid (N/256 x bin chunks)
@@ -960,9 +962,14 @@ int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, dou
 
 // SF0 = WF0 HF0 (F x NF0)(NF0 x N)
 int sf0_gemm(simm_ctx *c) {
-  if (c->use_blas)
+  if (c->use_blas == 1)
     return blas_gemm(c->blas, false, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
                      c->SF0.p, c->N);
+  if (c->use_blas == 0) {
+    const int st = dgemm(c->stream, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
+                         c->SF0.p, c->N);
+    if (st != FASST_ERR_SHAPE) return st;   // odd extents: k_gemm below
+  }
   return gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, c->N, c->SF0.p, c->N, c->F, c->N, c->NF0);
 }
 
@@ -1235,11 +1242,18 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
         k_simm_numden<false, KM><<<wg, 256, 0, c->stream>>>(p, c->TND.p, c->TND.p + N, 2 * (size_t)N);
     });
   }
-  if (c->use_blas) {  // WF0^T [num | den]: one (NF0 x F)(F x 2N) product
+  // WF0^T [num | den]: one (NF0 x F)(F x 2N) product
+  int gst = FASST_ERR_SHAPE;
+  if (c->use_blas == 1) {
     if ((st = blas_gemm(c->blas, true, false, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p,
                         2 * N)))
       return st;
-  } else {
+    gst = FASST_OK;
+  } else if (c->use_blas == 0) {
+    gst = dgemm(c->stream, true, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p, 2 * N);
+    if (gst != FASST_OK && gst != FASST_ERR_SHAPE) return gst;
+  }
+  if (gst == FASST_ERR_SHAPE) {   // odd extents (or FASST_SIMM_BLAS=2): k_gemm
     const double *Bs[2] = {c->TND.p, c->TND.p + N};
     double *Cs[2] = {c->NPD.p, c->NPD.p + N};
     if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, 2 * N, Cs, 2 * N, NF0, N, F,
