@@ -935,8 +935,10 @@ struct simm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   rocblas_handle blas = nullptr;  // bound to `stream`: the NF0-sized plain GEMMs
-  // NF0-sized plain products: 0 = k_dgemm (hand-written, default), 1 =
-  // rocBLAS dgemm, 2 = k_gemm (FASST_SIMM_BLAS, A/B only)
+  // NF0-sized plain products (FASST_SIMM_BLAS): 1 = rocBLAS dgemm (default:
+  // 8.73 vs 9.38 ms per C5 iteration, same-box A/B), 0 = the hand-written
+  // k_dgemm (rocBLAS when NF0 is odd: its 16-byte loads need even rows),
+  // 2 = k_gemm; all three parity-tested against the oracle
   int use_blas = 1;
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
@@ -962,14 +964,14 @@ int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, dou
 
 // SF0 = WF0 HF0 (F x NF0)(NF0 x N)
 int sf0_gemm(simm_ctx *c) {
-  if (c->use_blas == 1)
-    return blas_gemm(c->blas, false, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
-                     c->SF0.p, c->N);
   if (c->use_blas == 0) {
     const int st = dgemm(c->stream, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
                          c->SF0.p, c->N);
-    if (st != FASST_ERR_SHAPE) return st;   // odd extents: k_gemm below
+    if (st != FASST_ERR_SHAPE) return st;   // odd extents: rocBLAS below
   }
+  if (c->use_blas <= 1)
+    return blas_gemm(c->blas, false, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
+                     c->SF0.p, c->N);
   return gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, c->N, c->SF0.p, c->N, c->F, c->N, c->NF0);
 }
 
@@ -1244,20 +1246,21 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   }
   // WF0^T [num | den]: one (NF0 x F)(F x 2N) product
   int gst = FASST_ERR_SHAPE;
-  if (c->use_blas == 1) {
+  if (c->use_blas == 0) {
+    gst = dgemm(c->stream, true, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p, 2 * N);
+    if (gst != FASST_OK && gst != FASST_ERR_SHAPE) return gst;
+  }
+  if (gst == FASST_ERR_SHAPE && c->use_blas <= 1) {   // odd NF0 (or FASST_SIMM_BLAS=1)
     if ((st = blas_gemm(c->blas, true, false, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p,
                         2 * N)))
       return st;
     gst = FASST_OK;
-  } else if (c->use_blas == 0) {
-    gst = dgemm(c->stream, true, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p, 2 * N);
-    if (gst != FASST_OK && gst != FASST_ERR_SHAPE) return gst;
   }
-  if (gst == FASST_ERR_SHAPE) {   // odd extents (or FASST_SIMM_BLAS=2): k_gemm
+  if (gst == FASST_ERR_SHAPE) {   // FASST_SIMM_BLAS=2: k_gemm (no split-K: its outputs have ldc 2N)
     const double *Bs[2] = {c->TND.p, c->TND.p + N};
     double *Cs[2] = {c->NPD.p, c->NPD.p + N};
     if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, 2 * N, Cs, 2 * N, NF0, N, F,
-                                   c->gwork.p)))
+                                   nullptr)))
       return st;
   }
   k_mu_apply_nd<<<egrid((size_t)NF0 * N), 256, 0, c->stream>>>(c->HF0.p, c->NPD.p, NF0, N, omega);

@@ -114,9 +114,13 @@ def test_config1_shape_50_iterations_drift():
     assert max(d["params"], d["FB"], d["TW"]) < 1e-5
 
 
-def test_config5_full_size_vs_oracle():
+@pytest.mark.parametrize("gemm", ["1", "0"])
+def test_config5_full_size_vs_oracle(monkeypatch, gemm):
     """BASELINE configs[4]: one Stereo_SIMM iteration at F=2049, N=20000,
-    NF0=1092, P=30, K=4, R=40 against oracle/simm_ref.py (SIMM.py:613-941)."""
+    NF0=1092, P=30, K=4, R=40 against oracle/simm_ref.py (SIMM.py:613-941),
+    with the NF0-sized products on rocBLAS (FASST_SIMM_BLAS=1, the default)
+    and on the hand-written k_dgemm (=0)."""
+    monkeypatch.setenv("FASST_SIMM_BLAS", gemm)
     from pyfasst_amd.SeparateLeadStereo.SIMM import SIMM as S
     c = FULL_CASES["c5_full"]
     g = load("c5_full")

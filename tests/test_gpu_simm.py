@@ -106,6 +106,17 @@ def test_stereo_simm_vs_oracle(shape):
     _cmp(got, want, ST_NAMES, tol=1e-8)
 
 
+# The NF0-sized plain products (SF0 = WF0 HF0, WF0^T [num | den]) on the
+# hand-written k_dgemm (FASST_SIMM_BLAS=0; NF0 even, as k_dgemm's 16-byte
+# loads need) and on k_gemm (=2), against the same oracle as the default
+# rocBLAS path.  The variable is read when the SIMM context is created.
+@pytest.mark.parametrize("mode,shape", [("0", sh) for sh in SHAPES if sh[2] % 2 == 0]
+                         + [("2", SHAPES[1]), ("2", SHAPES[2])])
+def test_stereo_simm_gemm_paths_vs_oracle(monkeypatch, mode, shape):
+    monkeypatch.setenv("FASST_SIMM_BLAS", mode)
+    test_stereo_simm_vs_oracle(shape)
+
+
 @pytest.mark.parametrize("shape", SHAPES[:2] + SHAPES[6:7])
 def test_mono_simm_vs_oracle(shape):
     F, N, NF0, P, K, _ = shape
@@ -152,3 +163,9 @@ def test_simm_edge_cases():
     np.random.seed(2)
     want = simm_ref.stereo_simm(SXR, SXL, WF0, WG, 2, 10, numberOfIterations=0)
     _cmp(out, want, ST_NAMES, tol=0.0 + 1e-300)
+
+
+@pytest.mark.parametrize("shape", [SHAPES[1], SHAPES[6]])
+def test_mono_simm_kdgemm_vs_oracle(monkeypatch, shape):
+    monkeypatch.setenv("FASST_SIMM_BLAS", "0")
+    test_mono_simm_vs_oracle(shape)
