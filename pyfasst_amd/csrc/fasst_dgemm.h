@@ -49,7 +49,9 @@ __device__ __forceinline__ fasst::d4 dmfma(double a, double b, fasst::d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <bool TA>
+// IG > 0: __builtin_amdgcn_iglp_opt(IG - 1) scheduling hint in the chunk loop
+// (A/B in tools/ubench_dgemm2.hip only)
+template <bool TA, int IG = 0>
 __global__ __launch_bounds__(256, 2) void k_dgemm(const DgemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int SA = dgemm_sa<TA>(), SB = dgemm_sb();
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(256, 2) void k_dgemm(const DgemmArgs g) {
     const double *sA = odd ? sA1 : sA0;
     const double *sB = odd ? sB1 : sB0;
     if (c + 1 < nch) gload((c + 1) * kDBK);
+    if constexpr (IG > 0) __builtin_amdgcn_iglp_opt(IG - 1);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {   // fragments of two k-steps, then their 32 MFMAs
       double a[2][4], b[2][4];
