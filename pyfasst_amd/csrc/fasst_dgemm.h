@@ -51,7 +51,9 @@ __device__ __forceinline__ fasst::d4 dmfma(double a, double b, fasst::d4 c) {
 
 // IG > 0: __builtin_amdgcn_iglp_opt(IG - 1) scheduling hint in the chunk loop
 // (A/B in tools/ubench_dgemm2.hip only)
-template <bool TA, int IG = 0>
+// SM: the next chunk's LDS store after the first (1) or second (0) half of
+// the chunk's MFMAs (A/B in tools/ubench_dgemm2.hip)
+template <bool TA, int IG = 0, int SM = 0>
 __global__ __launch_bounds__(256, 2) void k_dgemm(const DgemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int SA = dgemm_sa<TA>(), SB = dgemm_sb();
@@ -155,8 +157,9 @@ __global__ __launch_bounds__(256, 2) void k_dgemm(const DgemmArgs g) {
             for (int i = 0; i < 4; ++i)
               if (i < nib) acc[i][j] = dmfma(a[u][i], b[u][j], acc[i][j]);
       }
+      if (SM == 1 && h == 0 && c + 1 < nch) sstore(odd ? sA0 : sA1, odd ? sB0 : sB1);
     }
-    if (c + 1 < nch) sstore(odd ? sA0 : sA1, odd ? sB0 : sB1);
+    if (SM == 0 && c + 1 < nch) sstore(odd ? sA0 : sA1, odd ? sB0 : sB1);
     __syncthreads();
   }
 #pragma unroll

@@ -42,7 +42,7 @@ static double maxrel(const double *a, const double *b, size_t n) {
   return mx / ref;
 }
 
-template <bool TA, int IG = 0>
+template <bool TA, int IG = 0, int SM = 0>
 static void run(const char *tag, const double *A, int lda, const double *B, double *C, int M, int N,
                 int K, const double *Cref, int order = 0) {
   DgemmArgs g{};
@@ -59,13 +59,13 @@ static void run(const char *tag, const double *A, int lda, const double *B, doub
   g.nt = (N + kDBN - 1) / kDBN;
   g.order = order;
   constexpr size_t lds = dgemm_smem<TA>();
-  hipFuncSetAttribute((const void *)k_dgemm<TA, IG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipFuncSetAttribute((const void *)k_dgemm<TA, IG, SM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int nb = ((g.mt * g.nt + 7) / 8) * 8;
   hipMemset(C, 0, sizeof(double) * M * N);
   const double fl = 2.0 * M * (double)N * K;
-  double ms = time_it([&] { k_dgemm<TA, IG><<<nb, 256, lds>>>(g); }, 10);
-  printf("k_dgemm<%s,ig%d> %-3s order %d M=%d N=%d K=%d lds=%zu: %.3f ms  %.1f TFLOP/s  maxrel %.2e\n",
-         TA ? "T" : "N", IG, tag, order, M, N, K, lds, ms, fl / ms / 1e9, maxrel(C, Cref, (size_t)M * N));
+  double ms = time_it([&] { k_dgemm<TA, IG, SM><<<nb, 256, lds>>>(g); }, 10);
+  printf("k_dgemm<%s,ig%d,sm%d> %-3s order %d M=%d N=%d K=%d lds=%zu: %.3f ms  %.1f TFLOP/s  maxrel %.2e\n",
+         TA ? "T" : "N", IG, SM, tag, order, M, N, K, lds, ms, fl / ms / 1e9, maxrel(C, Cref, (size_t)M * N));
 }
 
 int main() {
@@ -103,16 +103,12 @@ int main() {
          2.0 * F * NF0 * (double)N / ms1 / 1e9);
   printf("rocblas TN [NUM|DEN] = WF0^T T M=%d N=%d K=%d: %.3f ms  %.1f TFLOP/s\n", NF0, N2, F, ms2,
          2.0 * F * NF0 * (double)N2 / ms2 / 1e9);
-  run<false>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
-  run<true>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
-  run<false, 1>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
-  run<true, 1>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
-  run<false, 2>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
-  run<true, 2>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
-  run<false, 3>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
-  run<true, 3>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
-  run<false>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
-  run<true>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
+  for (int r = 0; r < 2; ++r) {   // interleaved A/B: default, store mid-chunk
+    run<false>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
+    run<false, 0, 1>("NN", WF0, NF0, HF0, C, F, N, NF0, SF0);
+    run<true>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
+    run<true, 0, 1>("TN", WF0, NF0, T0, C, NF0, N2, F, NUM);
+  }
   rocblas_destroy_handle(h);
   return 0;
 }
