@@ -174,6 +174,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--warm-s", type=float, default=1.0,
+                    help="untimed GEM iterations for at least this long before the W warm-up "
+                         "steps (the GPU clock ramps over the first ~20 iterations)")
     ap.add_argument("--T", type=int, default=T_FRAMES)
     ap.add_argument("--cpu-T", type=int, default=T_FRAMES,
                     help="frames of the CPU-baseline sample (default: the full T)")
@@ -196,8 +199,30 @@ def main():
     eng = m._engine
     order, Ks, conv = m._upload()
     rows_w = psd_schedule(m, max(args.warmup, 1))
+    state = {"upl": (order, Ks, conv)}
+
+    def run_rows(rows):
+        """GEM iterations over the PSD rows; a random TW restart (host RNG)
+        is performed and the run resumed, as the product does"""
+        done = 0
+        while done < len(rows):
+            _, n, mask = eng.run(rows[done:], m.nmfUpdateCoeff)
+            done += n
+            if mask:
+                m._download(*state["upl"])
+                m._restart_tw(mask, state["upl"][0])
+                state["upl"] = m._upload()
+
+    # clock ramp: the first ~20 iterations of a process run while the GPU
+    # clock rises (tools/ramp_probe.py); iterate untimed until it has settled,
+    # so that the K timed steps measure the steady state
+    if args.warm_s > 0:
+        rows_r = psd_schedule(m, 10)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < args.warm_s:
+            run_rows(rows_r)
     if args.warmup:
-        eng.run(rows_w[:args.warmup], m.nmfUpdateCoeff)
+        run_rows(rows_w[:args.warmup])
 
     def barrier_sync():
         if dist is not None:
@@ -209,14 +234,7 @@ def main():
     rows = psd_schedule(m, args.steps)
     barrier_sync()
     t0 = time.perf_counter()
-    done = 0
-    while done < args.steps:
-        _, n, mask = eng.run(rows[done:], m.nmfUpdateCoeff)
-        done += n
-        if mask:   # random TW restart (host RNG) then resume, as the product does
-            m._download(order, Ks, conv)
-            m._restart_tw(mask, order)
-            order, Ks, conv = m._upload()
+    run_rows(rows)
     barrier_sync()
     dt = max_over_ranks(time.perf_counter() - t0, dist,
                         "cuda:%d" % device if backend == "nccl" else "cpu")

@@ -35,8 +35,14 @@ int viterbi_tracking(int device, int n_states, int n_frames, const double *log_d
 
 /* Device time (HIP events) of the last viterbi_tracking call, without the
  * host<->device copies; and which kernel path it used (0: one workgroup
- * holding the whole transition matrix in LDS, 1: one launch per frame).   */
+ * holding the whole transition matrix in LDS, 1: one launch per frame,
+ * 2: one persistent cooperative launch).                                   */
 int viterbi_last_timing(double *device_ms, int *path_kind);
+
+/* Number of persistent launches in this process that aborted (grid not
+ * co-resident) and were rerun on the per-frame path (about 3x slower); the
+ * first one is also reported on stderr.                                    */
+int viterbi_fallback_count(int *aborts);
 
 #ifdef __cplusplus
 }

@@ -110,6 +110,7 @@ SIGNATURES = {
     "viterbi_tracking": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp,
                                         ctypes.c_long, _dp, _dp, ctypes.c_long, _llp]),
     "viterbi_last_timing": (ctypes.c_int, [_dp, _ip]),
+    "viterbi_fallback_count": (ctypes.c_int, [_ip]),
     # include/fasst_dict.h
     "dict_wf0_stft": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _ip, ctypes.c_int, _dp,
                                      ctypes.c_double, ctypes.c_int, _dp, ctypes.c_int,

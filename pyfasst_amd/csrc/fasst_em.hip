@@ -3596,6 +3596,8 @@ int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb
     const size_t nb = (size_t)c->nchunk_b * c->J * c->Fp * c->KP;
     if (c->bden.n < nb && (st = c->bden.alloc(nb))) return st;
   }
+  bool same = c->nblk[j] == nblk;
+  for (int b = 0; same && b <= nblk; ++b) same = c->kb[j][b] == kb[b];
   c->nblk[j] = nblk;
   for (int b = 0; b <= nblk; ++b) c->kb[j][b] = kb[b];
   bool fbf = false, twf = false, fwf = false;
@@ -3614,10 +3616,12 @@ int fasst_set_blocks(fasst_ctx *c, int j, int nblk, const int *kb, const int *fb
   for (int i = 0; i < c->J; ++i) c->soff[i + 1] = c->soff[i] + c->nblk[i];
   c->nslot = nslot;
   c->maxblk = maxblk;
-  for (int b = 0; b < kMaxBlk; ++b) {   // the blocks moved: their time blobs go
-    c->tb[j][b].release();
-    c->tbl[j][b] = c->btb[j][b] = 0;
-  }
+  if (!same)   // the blocks moved: their time blobs go (an unchanged layout,
+               // e.g. the per-iteration re-upload, keeps them and their buffers)
+    for (int b = 0; b < kMaxBlk; ++b) {
+      c->tb[j][b].release();
+      c->tbl[j][b] = c->btb[j][b] = 0;
+    }
   update_multi(c);
   return FASST_OK;
 }
@@ -3677,7 +3681,14 @@ int fasst_set_tb(fasst_ctx *c, int j, int b, int L, const double *TW, const doub
   if (c->mplanes.n < 6 * plane && (st = c->mplanes.alloc(6 * plane))) return st;
   const size_t nb = (size_t)c->nchunk_b * c->J * c->Fp * c->KP;
   if (c->bden.n < nb && (st = c->bden.alloc(nb))) return st;
-  if ((st = c->tb[j][b].alloc(o.n))) return st;   // zero-filled: TB's padding frames stay 0
+  // a buffer large enough is reused (no hipMalloc / device-wide sync on the
+  // per-iteration re-upload); either way it is zero-filled: TB's padding
+  // frames stay 0
+  if (c->tb[j][b].n < o.n) {
+    if ((st = c->tb[j][b].alloc(o.n))) return st;
+  } else {
+    FASST_HIP(hipMemsetAsync(c->tb[j][b].p, 0, o.n * sizeof(double), c->stream));
+  }
   FASST_HIP(hipMemcpyAsync(c->tb[j][b].p + o.tws, TW, (size_t)kbw * L * sizeof(double),
                            hipMemcpyHostToDevice, c->stream));
   FASST_HIP(hipMemcpy2DAsync(c->tb[j][b].p + o.tb, c->Tp * sizeof(double), TB,

@@ -79,13 +79,12 @@ template <bool TA, bool TB, int NB, int WGM, int WTM, int WTN>
 static int launch_gemm(hipStream_t s, const GemmArgs &g, int nz) {
   constexpr int BM = 16 * WGM * WTM, BN = 16 * (4 / WGM) * WTN;
   const size_t smem = 2 * (size_t)kGBK * (gpitch(BM) + NB * gpitch(BN)) * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    if (smem > 64 * 1024)
-      FASST_HIP(hipFuncSetAttribute((const void *)k_gemm<TA, TB, NB, WGM, WTM, WTN>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    attr = true;
-  }
+  // the dynamic-LDS limit is a per-device attribute: set it before every
+  // launch (a host-side call of a few us) so that a second device, or a
+  // concurrent context, never launches before it holds
+  if (smem > 64 * 1024)
+    FASST_HIP(hipFuncSetAttribute((const void *)k_gemm<TA, TB, NB, WGM, WTM, WTN>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, nz);
   k_gemm<TA, TB, NB, WGM, WTM, WTN><<<grid, 256, smem, s>>>(g);
   FASST_LAUNCH_CHECK();
@@ -177,23 +176,16 @@ int dgemm(hipStream_t s, bool ta, int M, int N, int K, const double *A, int lda,
   g.nt = (N + kDBN - 1) / kDBN;
   g.order = 0;
   const int nb = (g.mt * g.nt + 7) / 8 * 8;
+  // per-device attribute, set before every launch (see launch_gemm)
   if (ta) {
-    static bool attr = false;
-    if (!attr) {
-      FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)dgemm_smem<true>()));
-      attr = true;
-    }
+    FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)dgemm_smem<true>()));
     k_dgemm<true><<<nb, 256, dgemm_smem<true>(), s>>>(g);
   } else {
-    static bool attr = false;
-    if (!attr) {
-      FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)dgemm_smem<false>()));
-      attr = true;
-    }
+    FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)dgemm_smem<false>()));
     k_dgemm<false><<<nb, 256, dgemm_smem<false>(), s>>>(g);
   }
   FASST_LAUNCH_CHECK();

@@ -29,6 +29,7 @@
 // the first maximal s' wins, a NaN candidate never wins, and a NaN at s' = 0
 // sticks.  cum[s', n-1] + T[s', s] and "+ logDensity" are the reference's
 // own double additions, so cum and the path are bit-identical.
+#include <atomic>
 #include "fasst_common.h"
 #include "../../include/fasst_viterbi.h"
 
@@ -514,6 +515,9 @@ __global__ __launch_bounds__(256) void k_vt_transpose(const double *__restrict__
 
 static float g_vt_ms = 0.f;
 static int g_vt_kind = -1;
+// persistent launches that aborted and were rerun on the per-frame path
+// (about 3x slower): counted for viterbi_fallback_count and reported once
+static std::atomic<int> g_vt_aborts{0};
 
 }  // namespace fasst
 
@@ -629,6 +633,11 @@ int viterbi_tracking(int device, int n_states, int n_frames, const double *log_d
       if (!aborted) {
         g_vt_kind = 2;
         done = true;
+      } else if (g_vt_aborts.fetch_add(1) == 0) {
+        fprintf(stderr, "viterbi_tracking: the persistent launch aborted (its grid was not "
+                "co-resident, e.g. another process shares the GPU); rerunning on the "
+                "per-frame path (~3x slower). Further aborts are only counted "
+                "(viterbi_fallback_count).\n");
       }
       if (want_probe) {   // per-phase means of workgroup 0 over frames 2..4095, us
         std::vector<long long> h(8 * 4096);
@@ -675,6 +684,12 @@ int viterbi_tracking(int device, int n_states, int n_frames, const double *log_d
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   FASST_HIP(hipMemcpy(path, dpath.p, (size_t)N * sizeof(long long), hipMemcpyDeviceToHost));
+  return FASST_OK;
+}
+
+int viterbi_fallback_count(int *aborts) {
+  if (!aborts) return FASST_ERR_SHAPE;
+  *aborts = g_vt_aborts.load();
   return FASST_OK;
 }
 

@@ -25,6 +25,8 @@ Cases (tests/helpers.py FULL_CASES mirrors the shapes):
   c5_full   BASELINE configs[4]: Stereo_SIMM F=2049 N=20000 NF0=1092 P=30
             K=4 R=40 on gamma spectrograms (RandomState(0)), init seed 1,
             1 iteration
+  c5_10     the same at the pipeline's default 10 iterations
+            (SeparateLeadStereoTF.py:264)
 """
 import os
 import subprocess

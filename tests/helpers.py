@@ -111,6 +111,10 @@ FULL_CASES = {
                   data_rank=1, data_seed=0, init_seed=0),
     "c5_full": dict(F=2049, N=20000, NF0=1092, P=30, K=4, R=40, iters=1, data_seed=0,
                     init_seed=1),
+    # the pipeline's default nbIter=10 (SeparateLeadStereoTF.py:264): multiplicative-
+    # update drift over the iterations the product actually runs
+    "c5_10": dict(F=2049, N=20000, NF0=1092, P=30, K=4, R=40, iters=10, data_seed=0,
+                  init_seed=1),
 }
 
 
@@ -139,6 +143,17 @@ def rel(a, b):
     b = np.asarray(b)
     den = np.max(np.abs(b))
     return float(np.max(np.abs(a - b)) / (den if den > 0 else 1.0))
+
+
+def rel_elem(a, b, floor=1e-6):
+    """Elementwise relative error max |a - b| / max(|b|, floor * max|b|): every
+    point held to its own magnitude, the floor keeping exact-zero / underflowed
+    points out of the quotient."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    den = np.maximum(np.abs(b), floor * np.max(np.abs(b)))
+    den = np.where(den > 0, den, 1.0)
+    return float(np.max(np.abs(a - b) / den))
 
 
 def oracle_model_from_golden(g, case):

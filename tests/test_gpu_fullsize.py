@@ -19,7 +19,7 @@ import threading
 import numpy as np
 import pytest
 
-from helpers import FULL_CASES, load, rel, sub_f, sub_t
+from helpers import FULL_CASES, load, rel, rel_elem, sub_f, sub_t
 
 pytestmark = pytest.mark.gpu
 
@@ -57,6 +57,8 @@ def _drift(m, g, name):
                         abs(fac['TW'].sum() / g["TW_sum_%d" % j] - 1))
     S = np.abs(m.separated_images())
     d["absS"] = rel(S[:, :, fs][:, :, :, ts], g["absS"])
+    # every kept point against its own magnitude (floored at 1e-6 max)
+    d["absS_elem"] = rel_elem(S[:, :, fs][:, :, :, ts], g["absS"])
     d["absS_sum"] = rel(S.sum(axis=(2, 3)), g["absS_sum"])
     return d
 
@@ -74,7 +76,9 @@ def test_config3_full_size_vs_oracle(name):
     d = _drift(m, g, name)
     print(name, "drift", d)
     for k, v in d.items():
-        assert v < 1e-8, (k, v)
+        # elementwise |S|: low-power points carry the reordered sums' rounding
+        # relative to their own (tiny) magnitude
+        assert v < (1e-6 if k == "absS_elem" else 1e-8), (k, v)
 
 
 def test_chunk_overrides_vs_oracle(monkeypatch):
@@ -108,22 +112,26 @@ def test_config1_shape_50_iterations_drift():
     d = _drift(m, g, name)
     d["logliks"] = rel(ll, g["logliks"])
     print("c1_50 drift after 50 iterations:", d)
-    assert d["absS"] < BAR and d["absS_sum"] < BAR
+    # the north-star bar, max-normalised AND elementwise (each kept bin/frame of
+    # |S| against its own magnitude, floored at 1e-6 max: SURVEY.md §7's metric)
+    assert d["absS"] < BAR and d["absS_sum"] < BAR and d["absS_elem"] < BAR
     # the FP64 path holds far tighter than the bar (recorded, asserted loosely)
     assert d["logliks"] < 1e-8
     assert max(d["params"], d["FB"], d["TW"]) < 1e-5
 
 
+@pytest.mark.parametrize("name", ["c5_full", "c5_10"])
 @pytest.mark.parametrize("gemm", ["1", "0"])
-def test_config5_full_size_vs_oracle(monkeypatch, gemm):
-    """BASELINE configs[4]: one Stereo_SIMM iteration at F=2049, N=20000,
-    NF0=1092, P=30, K=4, R=40 against oracle/simm_ref.py (SIMM.py:613-941),
-    with the NF0-sized products on rocBLAS (FASST_SIMM_BLAS=1, the default)
-    and on the hand-written k_dgemm (=0)."""
+def test_config5_full_size_vs_oracle(monkeypatch, gemm, name):
+    """BASELINE configs[4]: Stereo_SIMM at F=2049, N=20000, NF0=1092, P=30,
+    K=4, R=40 against oracle/simm_ref.py (SIMM.py:613-941), one iteration and
+    the pipeline's default 10 (SeparateLeadStereoTF.py:264), with the
+    NF0-sized products on rocBLAS (FASST_SIMM_BLAS=1, the default) and on the
+    hand-written k_dgemm (=0)."""
     monkeypatch.setenv("FASST_SIMM_BLAS", gemm)
     from pyfasst_amd.SeparateLeadStereo.SIMM import SIMM as S
-    c = FULL_CASES["c5_full"]
-    g = load("c5_full")
+    c = FULL_CASES[name]
+    g = load(name)
     F, N, NF0, P, K, Rr = (c[k] for k in ("F", "N", "NF0", "P", "K", "R"))
     rs = np.random.RandomState(c["data_seed"])
     SXR = rs.gamma(0.8, 1.0, size=(F, N))
@@ -149,7 +157,7 @@ def test_config5_full_size_vs_oracle(monkeypatch, gemm):
         elif n == 'WM':
             v = v[fs]
         worst[n] = rel(v, g[n])
-    print("c5_full drift:", worst)
+    print(name, "drift:", worst)
     for k, v in worst.items():
         assert v < 1e-8, (k, v)
 

@@ -228,6 +228,8 @@ def bench_wf0(steps, warmup):
         if i >= warmup:
             ms.append(m.value)
     dm = float(np.median(ms))
+    ab = ctypes.c_int()
+    _lib.lib.viterbi_fallback_count(ctypes.byref(ab))
     # CPU: the oracle (the reference's outer-product synthesis) on 8 of the 1092 F0s
     idx = np.linspace(0, F0Table.size - 1, 8).astype(int)
     t0 = time.perf_counter()
@@ -265,6 +267,8 @@ def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
         if i >= warmup:
             ms.append(m.value)
     dm = float(np.median(ms))
+    ab = ctypes.c_int()
+    _lib.lib.viterbi_fallback_count(ctypes.byref(ab))
     # CPU: the oracle restatement of the pyx recursion on a bounded sample
     n_cpu = 40
     t0 = time.perf_counter()
@@ -276,6 +280,9 @@ def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
             "dtype": "f64", "data": "synthetic log-gamma densities, RandomState(0)",
             "config": {"workload": "viterbiTracking S=%d N=%d (max-plus S^2 per frame)" % (S, N)},
             "maxplus_gops": round(float(S) * S * (N - 1) / (dm * 1e-3) / 1e9, 1),
+            # persistent launches rerun on the per-frame path (results taken
+            # on the slower fallback are identifiable)
+            "path_kind": k.value, "persistent_aborts": ab.value,
             "cpu_baseline": {"value": round(1.0 / cpu_s, 5), "unit": "tracks/s", "cores": 1,
                              "kind": "port", "sample": "oracle/viterbi_ref.py, %d frames, "
                              "scaled to N=%d" % (n_cpu, N)}}
