@@ -15,7 +15,6 @@
 // Split-K along gridDim.z writes partial C slabs (C + z*slab) that
 // k_gemm_reduce sums in fixed order (deterministic).
 #pragma once
-#include <rocblas/rocblas.h>
 
 #include "fasst_common.h"
 
@@ -377,17 +376,10 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
 size_t gemm_workspace(int M, int N, int K, int NB);
 
 // Large plain products (the Stereo_SIMM NF0-sized ones): row-major
-// C (M x N) = op(A) B on k_dgemm (fasst_dgemm.h).  Returns FASST_ERR_SHAPE
-// without launching when the operands miss its 16-byte alignment.
-int dgemm(hipStream_t s, bool ta, int M, int N, int K, const double *A, int lda, const double *B,
-          int ldb, double *C, int ldc);
-
-// Plain (unfused) large products go to rocBLAS dgemm: row-major
-// C (M x N) = op(A) op(B) with op = transpose when ta / tb, issued on the
-// stream the handle is bound to.  rocBLAS's Tensile kernels (the same
-// v_mfma_f64_16x16x4 instruction) sustain ~1.8x the FP64 rate of k_gemm at
-// the Stereo_SIMM sizes (tools/ubench_dgemm.hip).
-int blas_gemm(rocblas_handle h, bool ta, bool tb, int M, int N, int K, const double *A, int lda,
-              const double *B, int ldb, double *C, int ldc);
+// C (M x N) = A^T B with A given k-major [K][lda] and B [K][ldb], on k_dgemm2
+// (fasst_dgemm2.h: global_load_lds stages, 4x4x4_4b MFMA).  Rows that are not
+// 16-byte aligned (odd lda / ldb) are loaded in 4-byte pieces.
+int dgemm2(hipStream_t s, int M, int N, int K, const double *A, int lda, const double *B, int ldb,
+           double *C, int ldc);
 
 }  // namespace fasst

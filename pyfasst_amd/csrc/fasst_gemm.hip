@@ -2,7 +2,7 @@
 // slab reduction.  Explicit instantiations cover the operand forms the NMF
 // and SIMM updates use.
 #include "fasst_gemm.h"
-#include "fasst_dgemm.h"
+#include "fasst_dgemm2.h"
 
 #include <algorithm>
 
@@ -43,22 +43,6 @@ static TileShape tile_shape(int M, int N, int NB) {
 static void tile_dims(const TileShape &t, int &BM, int &BN) {
   BM = 16 * t.wgm * t.wtm;
   BN = 16 * (4 / t.wgm) * t.wtn;
-}
-
-// Row-major C = op(A) op(B) as the column-major product C^T = op(B)^T op(A)^T:
-// a row-major X (r x c, ld) is the column-major X^T (c x r, ld).
-int blas_gemm(rocblas_handle h, bool ta, bool tb, int M, int N, int K, const double *A, int lda,
-              const double *B, int ldb, double *C, int ldc) {
-  const double one = 1.0, zero = 0.0;
-  const rocblas_status s =
-      rocblas_dgemm(h, tb ? rocblas_operation_transpose : rocblas_operation_none,
-                    ta ? rocblas_operation_transpose : rocblas_operation_none, N, M, K, &one, B,
-                    ldb, A, lda, &zero, C, ldc);
-  if (s != rocblas_status_success) {
-    set_error("rocblas_dgemm: %s", rocblas_status_to_string(s));
-    return FASST_ERR_DEVICE;
-  }
-  return FASST_OK;
 }
 
 // split K until the grid holds >= 1024 blocks (4 per CU), chunks >= 64
@@ -153,16 +137,27 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
   return FASST_OK;
 }
 
-// Large plain products on k_dgemm (fasst_dgemm.h).  FASST_ERR_SHAPE (no
-// launch, no error text) when the 16-byte alignment k_dgemm needs does not
-// hold: the caller then takes k_gemm.
-int dgemm(hipStream_t s, bool ta, int M, int N, int K, const double *A, int lda, const double *B,
-          int ldb, double *C, int ldc) {
-  const bool ok = M > 0 && N > 0 && K > 0 && lda % 2 == 0 && ldb % 2 == 0 && N % 2 == 0 &&
-                  (ta ? M % 2 == 0 : K % 2 == 0) && ((uintptr_t)A & 15) == 0 &&
-                  ((uintptr_t)B & 15) == 0;
-  if (!ok) return FASST_ERR_SHAPE;
-  DgemmArgs g;
+// Large plain products on k_dgemm2 (fasst_dgemm2.h) in its product shapes
+// (D2Prod, D2Odd).  The dynamic-LDS limit is a per-device attribute: set
+// before every launch.
+template <class CF, bool A4, bool B4>
+static int launch_dgemm2(hipStream_t s, Dgemm2Args g) {
+  g.mt = (g.M + CF::BM - 1) / CF::BM;
+  g.nt = (g.N + CF::BN - 1) / CF::BN;
+  FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm2<CF, A4, B4>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)CF::smem));
+  k_dgemm2<CF, A4, B4><<<g.mt * g.nt, CF::NT, CF::smem, s>>>(g);
+  FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+int dgemm2(hipStream_t s, int M, int N, int K, const double *A, int lda, const double *B, int ldb,
+           double *C, int ldc) {
+  if (M <= 0 || N <= 0 || K <= 0 || lda < M || ldb < N || ldc < N) {
+    set_error("dgemm2: bad shape M %d N %d K %d (lda %d ldb %d ldc %d)", M, N, K, lda, ldb, ldc);
+    return FASST_ERR_SHAPE;
+  }
+  Dgemm2Args g;
   g.A = A;
   g.B = B;
   g.C = C;
@@ -172,24 +167,12 @@ int dgemm(hipStream_t s, bool ta, int M, int N, int K, const double *A, int lda,
   g.M = M;
   g.N = N;
   g.K = K;
-  g.mt = (M + kDBM - 1) / kDBM;
-  g.nt = (N + kDBN - 1) / kDBN;
-  g.order = 0;
-  const int nb = (g.mt * g.nt + 7) / 8 * 8;
-  // per-device attribute, set before every launch (see launch_gemm)
-  if (ta) {
-    FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)dgemm_smem<true>()));
-    k_dgemm<true><<<nb, 256, dgemm_smem<true>(), s>>>(g);
-  } else {
-    FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)dgemm_smem<false>()));
-    k_dgemm<false><<<nb, 256, dgemm_smem<false>(), s>>>(g);
-  }
-  FASST_LAUNCH_CHECK();
-  return FASST_OK;
+  const bool a16 = lda % 2 == 0 && ((uintptr_t)A & 15) == 0;
+  const bool b16 = ldb % 2 == 0 && ((uintptr_t)B & 15) == 0;
+  if (a16 && b16) return launch_dgemm2<D2Prod, false, false>(s, g);
+  if (a16) return launch_dgemm2<D2Odd, false, true>(s, g);
+  if (b16) return launch_dgemm2<D2Odd, true, false>(s, g);
+  return launch_dgemm2<D2Odd, true, true>(s, g);
 }
 
 size_t gemm_workspace(int M, int N, int K, int NB) {

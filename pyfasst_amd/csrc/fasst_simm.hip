@@ -926,6 +926,18 @@ __global__ void k_lead_masks(const double *__restrict__ SF0, const double *__res
   }
 }
 
+// out[c][r] = in[r][c] (R x C, row pitches ldi / ldo) through a 16 x 16 LDS tile
+__global__ __launch_bounds__(256) void k_simm_transpose(const double *__restrict__ in,
+                                                        double *__restrict__ out, int R, int C,
+                                                        int ldi, int ldo) {
+  __shared__ double t[16][17];
+  const int c0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  if (r0 + ty < R && c0 + tx < C) t[ty][tx] = in[(size_t)(r0 + ty) * ldi + c0 + tx];
+  __syncthreads();
+  if (c0 + ty < C && r0 + tx < R) out[(size_t)(c0 + ty) * ldo + r0 + tx] = t[tx][ty];
+}
+
 }  // namespace fasst
 
 using namespace fasst;
@@ -934,12 +946,11 @@ using namespace fasst;
 struct simm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  rocblas_handle blas = nullptr;  // bound to `stream`: the NF0-sized plain GEMMs
-  // NF0-sized plain products (FASST_SIMM_BLAS): 1 = rocBLAS dgemm (default:
-  // 8.73 vs 9.38 ms per C5 iteration, same-box A/B), 0 = the hand-written
-  // k_dgemm (rocBLAS when NF0 is odd: its 16-byte loads need even rows),
-  // 2 = k_gemm; all three parity-tested against the oracle
-  int use_blas = 1;
+  // NF0-sized plain products (FASST_SIMM_GEMM): 0 = k_dgemm2 (default,
+  // fasst_dgemm2.h), 2 = the generic k_gemm (A/B and parity reference);
+  // both parity-tested against the oracle
+  int gemm_kind = 0;
+  int Fp = 0, NF0p = 0;   // even (16-byte) row pitches of the WF0 copies below
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
   int nchunk_w = 1, fchunk_w = 1;  // the frame-walker grid (N/256 x bin chunks)
@@ -948,7 +959,9 @@ struct simm_ctx {
   // refresh_hat (rebuild_model, the R > 48 path)
   const double *pend = nullptr;
   long slots = 512;   // resident blocks of the skinny products (2 per CU)
-  DBuf<double> SXR, SXL, WF0, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
+  // WF0 [F][NF0] as given (k_gemm), WF0K [F][NF0p] and WF0T [NF0][Fp]: the
+  // k-major operands of WF0^T [num | den] and of SF0 = WF0 HF0 on k_dgemm2
+  DBuf<double> SXR, SXL, WF0, WF0K, WF0T, WGAMMA, HGAMMA, HPHI, HF0, HM, WM, bR, bL, alpha;
   DBuf<double> WPHI, SF0, SPHI, hR, hL, SMR, SML, T0, T1, T2, T3, TND, NPD, WMb, WMb2, s_col, sg, sw;
   DBuf<double> hpart, hrows, apart, bd, gwork, P0, P1, P2, P3, RN0, RN1, reco;
 };
@@ -964,14 +977,8 @@ int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, dou
 
 // SF0 = WF0 HF0 (F x NF0)(NF0 x N)
 int sf0_gemm(simm_ctx *c) {
-  if (c->use_blas == 0) {
-    const int st = dgemm(c->stream, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
-                         c->SF0.p, c->N);
-    if (st != FASST_ERR_SHAPE) return st;   // odd extents: rocBLAS below
-  }
-  if (c->use_blas <= 1)
-    return blas_gemm(c->blas, false, false, c->F, c->N, c->NF0, c->WF0.p, c->NF0, c->HF0.p, c->N,
-                     c->SF0.p, c->N);
+  if (c->gemm_kind == 0)
+    return dgemm2(c->stream, c->F, c->N, c->NF0, c->WF0T.p, c->Fp, c->HF0.p, c->N, c->SF0.p, c->N);
   return gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, c->N, c->SF0.p, c->N, c->F, c->N, c->NF0);
 }
 
@@ -1245,18 +1252,11 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     });
   }
   // WF0^T [num | den]: one (NF0 x F)(F x 2N) product
-  int gst = FASST_ERR_SHAPE;
-  if (c->use_blas == 0) {
-    gst = dgemm(c->stream, true, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p, 2 * N);
-    if (gst != FASST_OK && gst != FASST_ERR_SHAPE) return gst;
-  }
-  if (gst == FASST_ERR_SHAPE && c->use_blas <= 1) {   // odd NF0 (or FASST_SIMM_BLAS=1)
-    if ((st = blas_gemm(c->blas, true, false, NF0, 2 * N, F, c->WF0.p, NF0, c->TND.p, 2 * N, c->NPD.p,
-                        2 * N)))
+  if (c->gemm_kind == 0) {
+    if ((st = dgemm2(c->stream, NF0, 2 * N, F, c->WF0K.p, c->NF0p, c->TND.p, 2 * N, c->NPD.p,
+                     2 * N)))
       return st;
-    gst = FASST_OK;
-  }
-  if (gst == FASST_ERR_SHAPE) {   // FASST_SIMM_BLAS=2: k_gemm (no split-K: its outputs have ldc 2N)
+  } else {   // FASST_SIMM_GEMM=2: k_gemm (no split-K: its outputs have ldc 2N)
     const double *Bs[2] = {c->TND.p, c->TND.p + N};
     double *Cs[2] = {c->NPD.p, c->NPD.p + N};
     if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, 2 * N, Cs, 2 * N, NF0, N, F,
@@ -1389,12 +1389,9 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   const size_t FN = (size_t)F * N;
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
-  if (!st && (rocblas_create_handle(&c->blas) != rocblas_status_success ||
-              rocblas_set_stream(c->blas, c->stream) != rocblas_status_success)) {
-    set_error("rocblas_create_handle / rocblas_set_stream failed");
-    st = FASST_ERR_DEVICE;
-  }
-  if (const char *v = getenv("FASST_SIMM_BLAS")) c->use_blas = atoi(v);
+  if (const char *v = getenv("FASST_SIMM_GEMM")) c->gemm_kind = atoi(v) == 2 ? 2 : 0;
+  c->Fp = (F + 15) / 16 * 16;
+  c->NF0p = (NF0 + 15) / 16 * 16;
   size_t gw = 0;
   gw = std::max(gw, gemm_workspace(NF0, 2 * N, F, 2));   // (num | den rows: ldc = 2N)
   gw = std::max(gw, gemm_workspace(F, N, NF0, 1));
@@ -1414,6 +1411,8 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   SA(SXR, FN);
   SA(SXL, stereo ? FN : 1);
   SA(WF0, (size_t)F * NF0);
+  SA(WF0K, (size_t)F * c->NF0p);   // zero-filled: the padding stays 0
+  SA(WF0T, (size_t)NF0 * c->Fp);
   SA(WGAMMA, (size_t)F * P);
   SA(HGAMMA, (size_t)P * K);
   SA(HPHI, (size_t)K * N);
@@ -1466,7 +1465,6 @@ int simm_destroy(simm_ctx *c) {
   {
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->blas) (void)rocblas_destroy_handle(c->blas);
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
   delete c;  // DBuf destructors free device memory
@@ -1482,6 +1480,12 @@ int simm_set_data(simm_ctx *c, const double *SXR, const double *SXL, const doubl
   if (c->stereo && SXL)
     FASST_HIP(hipMemcpyAsync(c->SXL.p, SXL, FN * 8, hipMemcpyHostToDevice, c->stream));
   FASST_HIP(hipMemcpyAsync(c->WF0.p, WF0, (size_t)c->F * c->NF0 * 8, hipMemcpyHostToDevice, c->stream));
+  // the k-major operands of k_dgemm2: WF0 with an even row pitch, and WF0^T
+  FASST_HIP(hipMemcpy2DAsync(c->WF0K.p, (size_t)c->NF0p * 8, WF0, (size_t)c->NF0 * 8,
+                             (size_t)c->NF0 * 8, c->F, hipMemcpyHostToDevice, c->stream));
+  k_simm_transpose<<<dim3((c->NF0 + 15) / 16, (c->F + 15) / 16), 256, 0, c->stream>>>(
+      c->WF0.p, c->WF0T.p, c->F, c->NF0, c->NF0, c->Fp);
+  FASST_LAUNCH_CHECK();
   FASST_HIP(hipMemcpyAsync(c->WGAMMA.p, WGAMMA, (size_t)c->F * c->P * 8, hipMemcpyHostToDevice,
                            c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));

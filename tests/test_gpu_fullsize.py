@@ -121,14 +121,14 @@ def test_config1_shape_50_iterations_drift():
 
 
 @pytest.mark.parametrize("name", ["c5_full", "c5_10"])
-@pytest.mark.parametrize("gemm", ["1", "0"])
+@pytest.mark.parametrize("gemm", ["0", "2"])
 def test_config5_full_size_vs_oracle(monkeypatch, gemm, name):
     """BASELINE configs[4]: Stereo_SIMM at F=2049, N=20000, NF0=1092, P=30,
     K=4, R=40 against oracle/simm_ref.py (SIMM.py:613-941), one iteration and
     the pipeline's default 10 (SeparateLeadStereoTF.py:264), with the
-    NF0-sized products on rocBLAS (FASST_SIMM_BLAS=1, the default) and on the
-    hand-written k_dgemm (=0)."""
-    monkeypatch.setenv("FASST_SIMM_BLAS", gemm)
+    NF0-sized products on the hand-written k_dgemm2 (FASST_SIMM_GEMM=0, the
+    default) and on the generic k_gemm (=2)."""
+    monkeypatch.setenv("FASST_SIMM_GEMM", gemm)
     from pyfasst_amd.SeparateLeadStereo.SIMM import SIMM as S
     c = FULL_CASES[name]
     g = load(name)

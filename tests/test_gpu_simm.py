@@ -106,14 +106,14 @@ def test_stereo_simm_vs_oracle(shape):
     _cmp(got, want, ST_NAMES, tol=1e-8)
 
 
-# The NF0-sized plain products (SF0 = WF0 HF0, WF0^T [num | den]) on the
-# hand-written k_dgemm (FASST_SIMM_BLAS=0; NF0 even, as k_dgemm's 16-byte
-# loads need) and on k_gemm (=2), against the same oracle as the default
-# rocBLAS path.  The variable is read when the SIMM context is created.
-@pytest.mark.parametrize("mode,shape", [("0", sh) for sh in SHAPES if sh[2] % 2 == 0]
-                         + [("2", SHAPES[1]), ("2", SHAPES[2])])
-def test_stereo_simm_gemm_paths_vs_oracle(monkeypatch, mode, shape):
-    monkeypatch.setenv("FASST_SIMM_BLAS", mode)
+# The NF0-sized plain products (SF0 = WF0 HF0, WF0^T [num | den]) run on the
+# hand-written k_dgemm2 by default (every test above, odd NF0 and odd N
+# included: operands whose rows are not 16-byte aligned take its 4-byte load
+# variant); FASST_SIMM_GEMM=2 selects the generic k_gemm, held to the same
+# oracle.  The variable is read when the SIMM context is created.
+@pytest.mark.parametrize("shape", [SHAPES[1], SHAPES[2]])
+def test_stereo_simm_kgemm_path_vs_oracle(monkeypatch, shape):
+    monkeypatch.setenv("FASST_SIMM_GEMM", "2")
     test_stereo_simm_vs_oracle(shape)
 
 
@@ -166,6 +166,6 @@ def test_simm_edge_cases():
 
 
 @pytest.mark.parametrize("shape", [SHAPES[1], SHAPES[6]])
-def test_mono_simm_kdgemm_vs_oracle(monkeypatch, shape):
-    monkeypatch.setenv("FASST_SIMM_BLAS", "0")
+def test_mono_simm_kgemm_vs_oracle(monkeypatch, shape):
+    monkeypatch.setenv("FASST_SIMM_GEMM", "2")
     test_mono_simm_vs_oracle(shape)
