@@ -81,13 +81,13 @@ ITERATION_KERNELS = ("k_w_from_fb", "k_fwh_t", "k_tw_rowsum", "k_inst_A", "k_est
                      "k_renorm_stats", "k_renorm_apply", "k_renorm_final")
 
 
-def build_model(seed, device, T=T_FRAMES):
+def build_model(seed, device, T=T_FRAMES, J=J_SRC, K=K_NMF):
     import pyfasst_amd.audioModel as am
     from pyfasst_amd import synthetic
     from pyfasst_amd.audioObject import SpectralAudio
-    X = synthetic.stereo_mixture(F_BINS, T, J=J_SRC, K_true=8, rank=RANK, seed=seed)
+    X = synthetic.stereo_mixture(F_BINS, T, J=J, K_true=8, rank=RANK, seed=seed)
     np.random.seed(1)
-    m = am.MultiChanNMFConv(SpectralAudio(X=X), nbComps=J_SRC, nbNMFComps=K_NMF,
+    m = am.MultiChanNMFConv(SpectralAudio(X=X), nbComps=J, nbNMFComps=K,
                             spatial_rank=RANK, iter_num=1, wlen=4096, hopsize=512,
                             device=device)
     m.makeItConvolutive()
@@ -178,6 +178,10 @@ def main():
                     help="untimed GEM iterations for at least this long before the W warm-up "
                          "steps (the GPU clock ramps over the first ~20 iterations)")
     ap.add_argument("--T", type=int, default=T_FRAMES)
+    # structure variants (the headline is J=4, K=32): the J > 4 E-step runs
+    # at one wave per SIMD, K up to 64 per source on the HIP path
+    ap.add_argument("--J", type=int, default=J_SRC)
+    ap.add_argument("--K", type=int, default=K_NMF)
     ap.add_argument("--cpu-T", type=int, default=T_FRAMES,
                     help="frames of the CPU-baseline sample (default: the full T)")
     args = ap.parse_args()
@@ -195,7 +199,7 @@ def main():
         torch.cuda.set_device(device)
         dist.init_process_group(backend)
 
-    m = build_model(seed=seed, device=device, T=args.T)
+    m = build_model(seed=seed, device=device, T=args.T, J=args.J, K=args.K)
     eng = m._engine
     order, Ks, conv = m._upload()
     rows_w = psd_schedule(m, max(args.warmup, 1))
@@ -248,8 +252,8 @@ def main():
     if rank == 0:
         R = sum(m.rank)
         F, T = m.nbFreqsSigRepr, m.nbFramesSigRepr
-        work = kernel_work(F, T, J_SRC, R, K_NMF)
-        itw = iteration_work(F, T, J_SRC, R, K_NMF)
+        work = kernel_work(F, T, args.J, R, args.K)
+        itw = iteration_work(F, T, args.J, R, args.K)
         dom = max(times, key=lambda k: times[k][0])
         rl = None
         pmc = None
@@ -326,7 +330,7 @@ def main():
             "data": "synthetic (STFT-domain stereo NMF mixture, RandomState(rank); init seed 1)",
             "config": {"workload": "C3/C4: MultiChanNMFConv GEM, F=%d T=%d J=%d spatial_rank=%d "
                                    "K=%d, one clip per GPU" % (m.nbFreqsSigRepr, m.nbFramesSigRepr,
-                                                              J_SRC, RANK, K_NMF),
+                                                              args.J, RANK, args.K),
                        "parallelism": "clip-per-GPU x%d" % world},
             "roofline": rl,
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(times.items())},

@@ -247,156 +247,4 @@ void k_dgemm2(const Dgemm2Args g) {
 }
 
 
-// k_dgemm_da: the same product with the A operand read straight from global
-// memory into the MFMA operand registers (no LDS stage for A) and only B
-// staged through LDS by global_load_lds, four stages deep;
-// v_mfma_f64_16x16x4f64, block tile 128 x 128 on 2 x 2 waves of 64 x 64 (4 x 4
-// d4 accumulators), K chunks of 16, two blocks per CU.  A wave's A fragments
-// of one chunk are 16 doubles per lane (A[k0 + 4 kk + tq][m0 + 64 wm + 16 i +
-// fl]: 4 rows x 128 B per load instruction), loaded one chunk ahead into a
-// 2-slot register ring, addressed as a wave-uniform base + 32-bit offset.
-// Loads never branch: an out-of-range element is read from a clamped address
-// and zeroed after the load.  The A loads are hidden from the compiler
-// (inline asm, §5.7 form (ii) of cdna_hip_programming.md): beside
-// global_load_lds it would otherwise wait vmcnt(0) for them and drain the B
-// stages every chunk; their completion is counted by hand.
-constexpr int kDaBM = 128, kDaBN = 128, kDaBK = 16, kDaPB = 144;
-template <int NS>
-constexpr size_t dgemm_da_smem() { return (size_t)NS * kDaBK * kDaPB * sizeof(double); }
-
-template <int NS>
-__global__ __launch_bounds__(256, 2) FASST_NO_LDS_PAIRING void k_dgemm_da(const Dgemm2Args g) {
-  static_assert(NS == 4, "the vmcnt bookkeeping below is written for four B stages");
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int SS = kDaBK * kDaPB;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int fl = lane & 15, tq = lane >> 4, wm = wv >> 1, wn = wv & 1;
-  const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
-  const int m0 = (tile % g.mt) * kDaBM, n0 = (tile / g.mt) * kDaBN;
-  const int nch = (g.K + kDaBK - 1) / kDaBK;
-  // B: rows 4 wv .. 4 wv + 3 of each chunk, one 1 KB glds each
-  const bool bok = n0 + 2 * lane < g.N;
-  auto issue_b = [&](int c) {
-    double *st = smem + (c % NS) * SS;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int kr = 4 * wv + r, k = c * kDaBK + kr;
-      const double *src = (k < g.K && bok) ? g.B + (size_t)k * g.ldb + n0 + 2 * lane : g_d2_zero;
-      __builtin_amdgcn_global_load_lds((d2_gbl_t *)src, (d2_lds_t *)(st + kr * kDaPB), 16, 0, 0);
-    }
-  };
-  // A: this lane's rows m = m0 + 64 wm + 16 i + fl (clamped), byte offsets
-  // from the uniform base (A is at most 4 GB: host check)
-  const int mb = m0 + wm * 64 + fl;
-  const unsigned mlast = (unsigned)(g.M - 1);
-  double ra[2][4][4];   // [slot][kk][i]
-  auto load_a = [&](int c, int slot) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = c * kDaBK + 4 * kk + tq;
-      const unsigned rowoff = (unsigned)(k < g.K ? k : g.K - 1) * (unsigned)g.lda;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const unsigned m = min((unsigned)(mb + 16 * i), mlast);
-        const unsigned off = (rowoff + m) * 8u;
-        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(ra[slot][kk][i]) : "v"(off), "s"(g.A) : "memory");
-      }
-    }
-  };
-  auto mask_a = [&](int c, int slot) {   // after the wait: zero what was clamped
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const bool kok = c * kDaBK + 4 * kk + tq < g.K;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        ra[slot][kk][i] = (kok && mb + 16 * i < g.M) ? ra[slot][kk][i] : 0.0;
-    }
-  };
-  d4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-  const int nib = min(4, max(0, (g.M - m0 - wm * 64 + 15) / 16));
-  // prologue: A(0), then B(0 .. 2)
-  load_a(0, 0);
-#pragma unroll
-  for (int c = 0; c < NS - 1; ++c)
-    if (c < nch) issue_b(c);
-  const int boff = wn * 64 + fl;
-  auto mainloop = [&](auto full_tag) {
-    constexpr bool FULL = decltype(full_tag)::value;
-    for (int c = 0; c < nch; c += 2) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {   // slot = chunk % 2 as a compile-time index
-        const int cc = c + u;
-        if (cc >= nch) break;
-        // A(cc) and B(cc) must have landed.  Issue order: A(0) B(0) B(1) B(2),
-        // then per iteration j: A(j + 1) B(j + 3).  The operations after the
-        // younger of A(cc), B(cc): cc = 0: B(1), B(2); cc >= 1 (A(cc) from
-        // iteration cc - 1): B(cc + 2) -- wait down to that count (the
-        // largest immediate not above it)
-        const int nafter = cc == 0 ? (1 < nch ? 4 : 0) + (2 < nch ? 4 : 0) : (cc + 2 < nch ? 4 : 0);
-#define FASST_DA_WAIT(N)                                                                     \
-  asm volatile("s_waitcnt vmcnt(" #N ")"                                                     \
-               : "+v"(ra[u][0][0]), "+v"(ra[u][0][1]), "+v"(ra[u][0][2]), "+v"(ra[u][0][3]), \
-                 "+v"(ra[u][1][0]), "+v"(ra[u][1][1]), "+v"(ra[u][1][2]), "+v"(ra[u][1][3])  \
-               :                                                                             \
-               : "memory");                                                                  \
-  asm volatile("" : "+v"(ra[u][2][0]), "+v"(ra[u][2][1]), "+v"(ra[u][2][2]), "+v"(ra[u][2][3]), \
-               "+v"(ra[u][3][0]), "+v"(ra[u][3][1]), "+v"(ra[u][3][2]), "+v"(ra[u][3][3]))
-        if (nafter >= 8) {
-          FASST_DA_WAIT(8);
-        } else if (nafter >= 4) {
-          FASST_DA_WAIT(4);
-        } else {
-          FASST_DA_WAIT(0);
-        }
-#undef FASST_DA_WAIT
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        mask_a(cc, u);
-        if (cc + 1 < nch) load_a(cc + 1, u ^ 1);
-        if (cc + NS - 1 < nch) issue_b(cc + NS - 1);
-        const double *st = smem + (cc % NS) * SS + boff;
-        double b[2][4];
-        auto ldb = [&](int kk, int sl) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) b[sl][j] = st[(4 * kk + tq) * kDaPB + 16 * j];
-        };
-        ldb(0, 0);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int sl = kk & 1;
-          if (kk + 1 < 4) ldb(kk + 1, sl ^ 1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (FULL || i < nib)
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[u][kk][i], b[sl][j], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-  };
-  if (nib == 4)
-    mainloop(std::true_type{});
-  else
-    mainloop(std::false_type{});
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm * 64 + 16 * i + tq + 4 * r;
-      if (row < g.M) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = n0 + wn * 64 + 16 * j + fl;
-          if (col < g.N) g.C[(size_t)row * g.ldc + col] = acc[i][j][r];
-        }
-      }
-    }
-}
-
 }  // namespace fasst

@@ -723,6 +723,8 @@ void k_estep_mx(const EArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // all operands of the 4 bin groups in flight at once, then the MFMAs
       // (read -> wait -> MFMA one at a time left the LDS latency exposed)
+      {
+      const int g2 = 0;
       double opd[4][S::NSET];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
@@ -739,6 +741,8 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
         for (int h = 0; h < NPG; ++h)
           pacc[g][h] = mfma44(opd[g][S::SV2 + h], opd[g][S::SN], pacc[g][h]);
+      }
+      (void)g2;
       }
       // the next point's slab writes must not overtake these reads
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

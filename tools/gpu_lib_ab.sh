@@ -17,9 +17,10 @@ PY
   done
 done
 for w in ${AB_AUX:-simm nmf}; do
+  [ "$w" = none ] && continue
   for lib in "$@"; do
     FASST_HIP_LIB=$PWD/$lib timeout -k 10 200 python tools/bench_aux.py --workload $w --steps 20 \
-      --warmup 3 > gpurun_out/ab_aux.log 2>&1
+      --warmup 3 --no-cpu-baseline > gpurun_out/ab_aux.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$lib $w rc=$rc"; tail -5 gpurun_out/ab_aux.log; exit $rc; }
     python - "$lib" "$w" <<'PY'
 import json, sys

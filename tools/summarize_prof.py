@@ -22,6 +22,8 @@ def short(name):
         return "k_estep_part%s" % m.group(1)
     if "fasst::k_estep_mx<" in name:
         return "k_estep"
+    if name.startswith("Cijk"):
+        return "rocblas_" + name[:12]
     m = re.search(r"fasst::(k_\w+)", name)
     return m.group(1) if m else name[:40]
 
@@ -63,6 +65,10 @@ def main(src, dst):
         e["WRITE_SIZE_KiB"] = w
         if f is not None and w is not None:
             e["hbm_bytes_per_launch"] = (2.0 * f + w) * 1024.0
+            t = e.get("avg_us_2nd_half") or e.get("avg_us")
+            if t:
+                e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (t * 1e-6) / 1e9, 1)
+                e["hbm_frac_of_8TBps"] = round(e["hbm_GBps"] / 8000.0, 3)
     out = {"source": src, "kernels": kernels,
            "note": "avg_us from rocprofv3 --kernel-trace --stats; hbm bytes = (2*FETCH_SIZE + "
                    "WRITE_SIZE)*1024 per launch (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md)"}
@@ -70,14 +76,16 @@ def main(src, dst):
         json.dump(out, fh, indent=1)
     with open(dst + ".txt", "w") as fh:
         fh.write("# rocprofv3 summary of %s\n" % src)
-        fh.write("%-16s %7s %12s %12s %14s %14s %16s\n" % (
-            "kernel", "calls", "avg_us", "avg_us_2h", "FETCH_KiB", "WRITE_KiB", "hbm_B/launch"))
+        fh.write("%-16s %7s %12s %12s %14s %14s %16s %9s %6s\n" % (
+            "kernel", "calls", "avg_us", "avg_us_2h", "FETCH_KiB", "WRITE_KiB", "hbm_B/launch",
+            "GB/s", "frac"))
         for k, e in sorted(kernels.items(), key=lambda kv: -kv[1].get("total_ns", 0)):
-            fh.write("%-16s %7s %12s %12s %14s %14s %16s\n" % (
+            fh.write("%-16s %7s %12s %12s %14s %14s %16s %9s %6s\n" % (
                 k, e.get("calls", ""), e.get("avg_us", ""), e.get("avg_us_2nd_half", ""),
                 "%.0f" % e["FETCH_SIZE_KiB"] if e.get("FETCH_SIZE_KiB") is not None else "",
                 "%.0f" % e["WRITE_SIZE_KiB"] if e.get("WRITE_SIZE_KiB") is not None else "",
-                "%.3e" % e["hbm_bytes_per_launch"] if e.get("hbm_bytes_per_launch") else ""))
+                "%.3e" % e["hbm_bytes_per_launch"] if e.get("hbm_bytes_per_launch") else "",
+                e.get("hbm_GBps", ""), e.get("hbm_frac_of_8TBps", "")))
     print(open(dst + ".txt").read())
 
 

@@ -100,30 +100,6 @@ static void sweep(F &&f) {
   f(C7{});
 }
 
-static double run_da(const char *tag, const double *A, int lda, const double *B, int ldb, double *C,
-                     int ldc, int M, int N, int K, const double *Cref, int reps = 10) {
-  Dgemm2Args g{};
-  g.A = A;
-  g.B = B;
-  g.C = C;
-  g.lda = lda;
-  g.ldb = ldb;
-  g.ldc = ldc;
-  g.M = M;
-  g.N = N;
-  g.K = K;
-  g.mt = (M + kDaBM - 1) / kDaBM;
-  g.nt = (N + kDaBN - 1) / kDaBN;
-  constexpr size_t lds = dgemm_da_smem<4>();
-  (void)hipFuncSetAttribute((const void *)k_dgemm_da<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  (void)hipMemset(C, 0, sizeof(double) * M * ldc);
-  const double fl = 2.0 * M * (double)N * K;
-  const double ms = time_it([&] { k_dgemm_da<4><<<g.mt * g.nt, 256, lds>>>(g); }, reps);
-  printf("k_dgemm_da<4> %-7s M=%d N=%d K=%d lda=%d ldb=%d: %.3f ms  %.1f TFLOP/s  maxrel %.2e\n", tag, M,
-         N, K, lda, ldb, ms, fl / ms / 1e9, maxrel(C, Cref, M, N, ldc));
-  return ms;
-}
-
 static void run1(const char *tag, const double *A, int lda, const double *B, double *C, int M, int N,
                  int K, const double *Cref) {
   DgemmArgs g{};
@@ -188,7 +164,6 @@ int main(int argc, char **argv) {
   if (prof) {
     for (int r = 0; r < 5; ++r) blas_ta(h, WF0, NF0, T0, N2, Cref, N2, NF0, N2, F);
     run2<C1>("NPD", WF0, NF0, T0, N2, C, N2, NF0, N2, F, Cref, 5);
-    run_da("NPD", WF0, NF0, T0, N2, C, N2, NF0, N2, F, Cref, 5);
     run2<C2>("NPD", WF0, NF0, T0, N2, C, N2, NF0, N2, F, Cref, 5);
     (void)hipDeviceSynchronize();
     return 0;
@@ -197,12 +172,10 @@ int main(int argc, char **argv) {
   double ms = time_it([&] { blas_ta(h, WF0T, FP, HF0, N, Cref, N, F, N, NF0); }, 10);
   printf("rocblas SF0 = WF0 HF0      M=%d N=%d K=%d: %.3f ms  %.1f TFLOP/s\n", F, N, NF0, ms, fl / ms / 1e9);
   sweep([&](auto cf) { run2<decltype(cf)>("SF0", WF0T, FP, HF0, N, C, N, F, N, NF0, Cref); });
-  run_da("SF0", WF0T, FP, HF0, N, C, N, F, N, NF0, Cref);
   ms = time_it([&] { blas_ta(h, WF0, NF0, T0, N2, Cref, N2, NF0, N2, F); }, 10);
   printf("rocblas NPD = WF0^T T      M=%d N=%d K=%d: %.3f ms  %.1f TFLOP/s\n", NF0, N2, F, ms,
          2.0 * NF0 * (double)N2 * F / ms / 1e9);
   sweep([&](auto cf) { run2<decltype(cf)>("NPD", WF0, NF0, T0, N2, C, N2, NF0, N2, F, Cref); });
-  run_da("NPD", WF0, NF0, T0, N2, C, N2, NF0, N2, F, Cref);
   run1("NPD", WF0, NF0, T0, C, NF0, N2, F, Cref);
   // edges: odd N (ldb even), odd M with even lda, K % 16 != 0, small
   struct E { int M, N, K, lda, ldb; } es[] = {{1091, 1999, 1000, 1092, 2000}, {130, 258, 37, 130, 258},
@@ -210,7 +183,6 @@ int main(int argc, char **argv) {
   for (auto e : es) {
     blas_ta(h, WF0T, e.lda, HF0, e.ldb, Cref, e.N, e.M, e.N, e.K);
     run2<C1>("edge", WF0T, e.lda, HF0, e.ldb, C, e.N, e.M, e.N, e.K, Cref, 2);
-    run_da("edge", WF0T, e.lda, HF0, e.ldb, C, e.N, e.M, e.N, e.K, Cref, 2);
     run2<C2>("edge", WF0T, e.lda, HF0, e.ldb, C, e.N, e.M, e.N, e.K, Cref, 2);
     run2<D2Prod, true, true>("edge4", WF0T, e.lda, HF0, e.ldb, C, e.N, e.M, e.N, e.K, Cref, 2);
   }
