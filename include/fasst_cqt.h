@@ -12,6 +12,7 @@
  *                                                          :794-868 + invertLinearPart)
  *                CQTransfo.invertTransform                 (minqt.py:1013-1055: invertFromCellCQT)
  *                both after `transfo = spCQT`              (minqt.py:648-658, spCQT2CellCQT :949-1011)
+ *   dict_wf0_cqt generate_WF0_TR_chirped on this transform (separateLeadFunctions.py:742-886)
  *   cqt_shape    the frame bookkeeping of computeCQT (nframes per octave, minqt.py:553-556)
  *
  * The one-octave spectral kernel (CQTKernel / MinQTKernel, minqt.py:95-227,
@@ -57,6 +58,19 @@ int cqt_forward(cqt_ctx *ctx, const double *x, long L, double *sp);
  * -> y [L]                                                                */
 int cqt_inverse(cqt_ctx *ctx, const double *sp, long L, double *y);
 
+/* SIMM source dictionary on this transform (generate_WF0_TR_chirped with a
+ * CQT / MinQT transform, SeparateLeadStereo/separateLeadFunctions.py:742-886,
+ * replacing its per-F0 computeTransform loop :829-879): for every column j the
+ * complex KLGLOTT88 comb odgd_j of length_odgd samples (amps, f1, f2 as in
+ * fasst_dict.h: generate_ODGD_spec :888-945 / _chirped :1010-1067) is
+ * transformed, and wf0[k][j] = |transfo(odgd_j)[k, col]|^2, col the
+ * reference's midindex (argmin |datalen_init / 2 - time_stamps|).  The
+ * transform of the complex comb is T(Re) + i T(Im) on the CQT rows and T(Re)
+ * on the MinQT linear rows (the linear part's rfft drops the imaginary part).
+ * wf0 [freqbins][n_cols] row-major.                                        */
+int dict_wf0_cqt(cqt_ctx *ctx, int n_cols, const double *f1, const double *f2,
+                 const int *n_partials, int max_partials, const double *amps, double fs,
+                 long length_odgd, int col, double *wf0);
 /* Device time (HIP events on the context's stream) of the last cqt_forward /
  * cqt_inverse, excluding the host<->device copies of x, sp and y.         */
 int cqt_device_ms(cqt_ctx *ctx, double *forward_ms, double *inverse_ms);

@@ -161,7 +161,9 @@ class RefCQT(object):
         """computeCQT perfRast branch (minqt.py:471-486, 523-646) and, for
         MinQT, computeLinearPart (minqt.py:1410-1450)."""
         k = self.k
-        data = np.asarray(data, dtype=np.float64)
+        data = np.asarray(data)
+        if not np.iscomplexobj(data):
+            data = data.astype(np.float64)
         self.datalen_init = data.shape[0]
         oct_n = int(self.octaveNr)
         self.maxBlock = int(k.FFTLen * (2 ** (self.octaveNr - 1)))
@@ -214,7 +216,9 @@ class RefCQT(object):
         k = self.k
         x = np.concatenate([np.zeros(self.prefixZeros), data, np.zeros(self.suffixZeros)])
         self.offsetSTFT = k.first_center
-        X = stft(x[int(self.offsetSTFT):], k.linWindow, k.atomHOP, k.linFTLen)
+        # a complex signal (the SIMM dictionary's comb, separateLeadFunctions.py
+        # :838-847): the rfft of stft.py:3-69 kept its real part (numpy < 1.13)
+        X = stft(np.real(x[int(self.offsetSTFT):]), k.linWindow, k.atomHOP, k.linFTLen)
         lin = X[k.Kmax:, :int(self.nframes[0] * k.winNr)]
         W = sp.shape[1]
         out = np.vstack([sp, np.zeros([int(k.linBins), W], dtype=complex)])

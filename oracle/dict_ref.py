@@ -99,6 +99,36 @@ def generate_wf0_tr_chirped_stft(ftlen, hop, window, fs, minF0, maxF0, stepNotes
     return F0Table, WF0
 
 
+def generate_wf0_tr_chirped_cqt(t, minF0, maxF0, stepNotes=4, Ot=0.5, perF0=1,
+                                depthChirpInSemiTone=0.5):
+    """generate_WF0_TR_chirped (:696-886) with a CQT-type transform t
+    (cqt_ref.RefCQT): lengthWindow = FFTLen * 2^(octaveNr - 1) (:742-744), the
+    complex comb through the transform, |transfo[:, midindex]|^2 with
+    midindex = argmin((datalen_init / 2 - time_stamps)^2) (:836-843) and the
+    time stamps of minqt.py:676-689."""
+    k = t.k
+    fs = t.fs
+    lengthWindow = int(k.FFTLen * (2 ** (t.octaveNr - 1)))
+    F0Table = f0_table(minF0, maxF0, stepNotes)
+    numberOfF0 = F0Table.size
+    WF0 = np.zeros([int(t.freqbins), int(numberOfF0 * perF0)])
+
+    def mid_power(odgd):
+        sp = t.forward(odgd)
+        time_stamps = (np.arange(t.nframes[0] * k.winNr) * k.atomHOP +
+                       k.first_center * 2 ** (t.octaveNr - 1) - t.prefixZeros)
+        midindex = np.argmin((t.datalen_init / 2. - time_stamps) ** 2)
+        return np.abs(sp[:, midindex]) ** 2
+    for i in range(numberOfF0):
+        WF0[:, i * perF0] = mid_power(generate_odgd(F0Table[i], fs, lengthOdgd=lengthWindow, Ot=Ot))
+        for c in range(perF0 - 1):
+            F2 = F0Table[i] * (2 ** ((c + 1.0) * depthChirpInSemiTone / (12.0 * (perF0 - 1.0))))
+            F1 = 2.0 * F0Table[i] - F2
+            WF0[:, i * perF0 + c + 1] = mid_power(
+                generate_odgd_chirped(F1, F2, fs, lengthOdgd=lengthWindow, Ot=Ot))
+    return F0Table, WF0
+
+
 def generate_hann_basis(numberFrequencyBins, sizeOfFourier, Fs, frequencyScale='linear',
                         numberOfBasis=20, overlap=.75):
     """generateHannBasis (:1074-1146), linear scale."""

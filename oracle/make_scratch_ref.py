@@ -164,6 +164,12 @@ PATCHES = [
      "bigWindow = np.zeros([int(sizeBigWindow * 2), 1])"),
     ("SeparateLeadStereo/separateLeadFunctions.py", r"bigWindow\[\(sizeBigWindow - lengthSineWindow / 2\.0\):\\\n\s+\(sizeBigWindow \+ lengthSineWindow / 2\.0\)\]",
      "bigWindow[int(sizeBigWindow - lengthSineWindow / 2.0):int(sizeBigWindow + lengthSineWindow / 2.0)]"),
+    # generate_WF0_TR_chirped on a CQT / MinQT transform (:742-815): the
+    # window length FFTLen * 2**(octaveNr-1) is a float
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"    if hasattr\(transform, 'octaveNr'\):\n        lengthWindow = \(\n",
+     "    if hasattr(transform, 'octaveNr'):\n        lengthWindow = int(\n"),
+    ("SeparateLeadStereo/separateLeadFunctions.py", r"analysisWindow = transform\.winFunc\(lengthWindow\)",
+     "analysisWindow = transform.winFunc(int(lengthWindow))"),
     # NMF initialisation (audioModel.py:2118-2177): float slice bounds
     ("audioModel.py", r"ind_start = np\.sum\(nbSpecComps\[:spec_ind\]\)",
      "ind_start = int(np.sum(nbSpecComps[:spec_ind]))"),
@@ -188,6 +194,10 @@ PATCHES = [
      "data = np.zeros([int(nuDataLen), 2], np.int16)"),
     ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"start = cumulframe - wlen \+ hopsize\n",
      "start = int(cumulframe - wlen + hopsize)\n"),
+    # CQT-type chunks (:726-735, :810-818, :893-900): sample bounds are float
+    # multiples of atomHOP, which numpy < 1.12 truncated as slice indices
+    ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"            data = data\[start:stop\]\n",
+     "            data = data[int(start):int(stop)]\n"),
     ("SeparateLeadStereo/SeparateLeadStereoTF.py", r"'stft': self\.stftParams\['windowSizeInSamples'\] / 2,",
      "'stft': self.stftParams['windowSizeInSamples'] // 2,"),
 ]

@@ -67,8 +67,10 @@ class SeparateLeadProcess(object):
     of each chunk, overlap-add of the chunk WAVs.  Every SIMM iteration,
     STFT / iSTFT, mask, the dictionary synthesis and the Viterbi recursion
     run on the GPU; chunk bookkeeping and WAV I/O are host-side, as in the
-    reference.  tfrepresentation 'stft' only (the CQT variants feed complex
-    signals into the CQT: NotImplementedError), initHF00 'random' only.
+    reference.  tfrepresentation 'stft' or the CQT-type 'cqt' / 'minqt' /
+    'mqt' (GPU CQT / MinQT transforms and their inverses; the source
+    dictionary of a CQT-type transform transforms the complex KLGLOTT88
+    comb on the GPU, dict_wf0_cqt), initHF00 'random' only.
 
     Addition: with inputAudioFilename=None the state that
     writeSeparatedSignals / runViterbi read can be given directly
@@ -109,9 +111,6 @@ class SeparateLeadProcess(object):
             raise AttributeError("The desired Time-Freq representation " + tfrepresentation +
                                  " is not a recognized one.\nPlease choose from " +
                                  str(knownTransfos))
-        if tfrepresentation != 'stft':
-            raise NotImplementedError("tfrepresentation %r: only 'stft' runs on the GPU path"
-                                      % tfrepresentation)
         if initHF00 != 'random':
             raise NotImplementedError("initHF00=%r (per-frame NNLS) is outside the GPU path"
                                       % initHF00)
@@ -187,12 +186,19 @@ class SeparateLeadProcess(object):
 
     # ---------------------------------------------------------------- setup
     def computeWF0(self):
-        """Source dictionary on the GPU (SeparateLeadStereoTF.py:587-700, the
-        'stft' branch: STFT transform + generate_WF0_TR_chirped)."""
-        from ..tftransforms.stft import STFT
-        self.mqt = STFT(linFTLen=self.stftParams['NFT'],
-                        atomHopFactor=self.stftParams['cqtAtomHopFactor'],
-                        winFunc=self.stftParams['cqtWinFunc'], fs=self.fs, device=self.device)
+        """Source dictionary on the GPU and the transform object
+        (SeparateLeadStereoTF.py:587-700, the transform-registry branch
+        :656-700): the transform named by tfrepresentation ('stft', or the
+        CQT-type 'cqt' / 'minqt' / 'mqt', tftransforms/tft.py:74-80) and
+        generate_WF0_TR_chirped on it.  A CQT-type transform resets the
+        frame geometry: hopsize = atomHOP, NFT = FFTLen, window =
+        FFTLen * 2^(octaveNr - 1) (:689-700)."""
+        from ..tftransforms import tft
+        self.mqt = tft.tftransforms[self.tfrepresentation](
+            fmin=self.stftParams['cqtfmin'], fmax=self.stftParams['cqtfmax'],
+            bins=self.stftParams['cqtbins'], fs=self.fs, linFTLen=self.stftParams['NFT'],
+            atomHopFactor=self.stftParams['cqtAtomHopFactor'],
+            winFunc=self.stftParams['cqtWinFunc'], perfRast=1, verbose=0, device=self.device)
         self.SIMMParams['F0Table'], WF0, self.mqt = slf.generate_WF0_TR_chirped(
             transform=self.mqt, minF0=self.SIMMParams['minF0'], maxF0=self.SIMMParams['maxF0'],
             stepNotes=self.SIMMParams['stepNotes'], Ot=0.5,
@@ -201,6 +207,11 @@ class SeparateLeadProcess(object):
         self.SIMMParams['WF0'] = WF0 / np.sum(WF0, axis=0)
         self.SIMMParams['NF0'] = self.SIMMParams['F0Table'].size
         self.F = WF0.shape[0]
+        if hasattr(self.mqt, 'cqtkernel'):
+            self.stftParams['hopsize'] = self.mqt.cqtkernel.atomHOP
+            self.stftParams['NFT'] = self.mqt.cqtkernel.FFTLen
+            self.stftParams['windowSizeInSamples'] = (self.mqt.cqtkernel.FFTLen *
+                                                      (2 ** (self.mqt.octaveNr - 1)))
 
     def _read(self):
         _, data = wav.read(self.files['inputAudioFilename'])
@@ -212,18 +223,49 @@ class SeparateLeadProcess(object):
                         nfft=self.stftParams['NFT'], start=start, stop=stop,
                         device=self.device)[0]
 
+    def _cqt_span(self, data, start, stop):
+        """Samples of frames start:stop for a CQT-type transform (:726-733):
+        start * atomHOP to (stop - 1) * atomHOP + window (numpy < 1.12
+        truncated the float bounds)."""
+        start = start * self.mqt.cqtkernel.atomHOP
+        if stop is not None:
+            stop = (stop - 1) * self.mqt.cqtkernel.atomHOP
+            stop += self.stftParams['windowSizeInSamples']
+        else:
+            stop = data.shape[0]
+        return data[int(start):int(stop)]
+
+    def _cqt(self, x):
+        """The transform of x on the GPU (transfo), released afterwards."""
+        self.mqt.computeTransform(data=x)
+        X = np.copy(self.mqt.transfo)
+        del self.mqt.transfo
+        return X
+
     def computeMonoX(self, start=0, stop=None):
-        """max(|STFT(mean of channels)|^2, 1e-8) for frames start:stop (:702-739)."""
+        """max(|X(mean of channels)|^2, 1e-8) for frames start:stop, X the
+        STFT or the CQT-type transform (:702-739)."""
         data = self._read()
         if len(data.shape) > 1 and data.shape[1] > 1:
             data = data.mean(axis=1)
-        X = self._stft(data, start, stop)
-        self.F, _ = X.shape
-        return np.maximum(np.abs(X) ** 2, 10 ** -8)
+        if self.tfrepresentation == 'stft':
+            X = self._stft(data, start, stop)
+            self.F, _ = X.shape
+            return np.maximum(np.abs(X) ** 2, 10 ** -8)
+        return np.maximum(np.abs(self._cqt(self._cqt_span(data, start, stop))) ** 2, 10 ** -8)
 
     def computeStereoX(self, start=0, stop=None):
-        """Complex STFTs XR, XL for frames start:stop (:761-841)."""
+        """Complex transforms XR, XL for frames start:stop (:761-841)."""
         data = self._read()
+        if self.tfrepresentation != 'stft':
+            data = self._cqt_span(data, start, stop)
+            self.XR = self._cqt(data[:, 0] if len(data.shape) > 1 else data)
+            if len(data.shape) > 1 and data.shape[1] > 1:
+                self.XL = self._cqt(data[:, 1])
+            else:
+                self.XL = self.XR
+            self.F, _ = self.XR.shape
+            return
         starttime = start * self.stftParams['hopsize']
         stoptime = stop * self.stftParams['hopsize'] if stop is not None else data.shape[0]
         self.originalDataLen = stoptime - starttime
@@ -238,8 +280,18 @@ class SeparateLeadProcess(object):
         self.F, _ = self.XR.shape
 
     def computeStereoSX(self, start=0, stop=None):
-        """max(|STFT|^2, 1e-8) of each channel, frames start:stop (:843-917)."""
+        """max(|X|^2, 1e-8) of each channel, frames start:stop (:843-917)."""
         data = self._read()
+        if self.tfrepresentation != 'stft':
+            data = self._cqt_span(data, start, stop)
+            SXR = np.maximum(np.abs(self._cqt(data[:, 0] if len(data.shape) > 1 else data)) ** 2,
+                             10 ** -8)
+            if len(data.shape) > 1 and data.shape[1] > 1:
+                SXL = np.maximum(np.abs(self._cqt(data[:, 1])) ** 2, 10 ** -8)
+            else:
+                SXL = SXR
+            self.F, _ = SXR.shape
+            return SXR, SXL
         starttime = start * self.stftParams['hopsize']
         stoptime = stop * self.stftParams['hopsize'] if stop is not None else data.shape[0]
         self.originalDataLen = stoptime - starttime
@@ -287,7 +339,12 @@ class SeparateLeadProcess(object):
                 stepNotes=P['stepNotes'], lambdaHF0=0.0 / (1.0 * SX.max()), alphaHF0=0.9,
                 verbose=self.verbose, F0Table=P['F0Table'], chirpPerF0=P['chirpPerF0'],
                 device=self.device)
-            P['HF0'][:, start:stop] = np.copy(HF0)
+            if self.tfrepresentation == 'stft':
+                P['HF0'][:, start:stop] = np.copy(HF0)
+            else:
+                # the first frame of interest of the CQT-type raster (:1025-1032)
+                startincqt = np.sort(np.where(self.mqt.time_stamps > 0)[0])[0]
+                P['HF0'][:, start:stop] = np.copy(HF0[:, startincqt:startincqt + stop - start])
             del SX
 
     def initiateHF0WithIndexBestPath(self):
@@ -325,7 +382,11 @@ class SeparateLeadProcess(object):
             stop = np.minimum((n + 1) * maxFrames, totFrames)
             SXR, SXL = self.computeStereoSX(start=start, stop=stop)
             HF00 = np.zeros([P['NF0'] * P['chirpPerF0'], SXR.shape[1]])
-            startinHF00, stopinHF00 = 0, stop - start
+            if self.tfrepresentation == 'stft':
+                startinHF00, stopinHF00 = 0, stop - start
+            else:                                            # :1400-1402
+                startinHF00 = np.sort(np.where(self.mqt.time_stamps > 0)[0])[0]
+                stopinHF00 = startinHF00 + stop - start
             HF00[:, startinHF00:stopinHF00] = P['HF00'][:, start:stop]
             (alphaR, alphaL, HGAMMA, HPHI, HF0, betaR, betaL, HM, WM,
              recoError2) = SIMM.Stereo_SIMM(
@@ -349,14 +410,20 @@ class SeparateLeadProcess(object):
 
     def overlapAddChunks(self, nChunks, suffixIsSUIMM='.wav'):
         """Concatenate the chunk WAVs with their overlaps (:1469-1583): for the
-        STFT the overlap is rectangular (ones); int16 arithmetic as the
-        reference's."""
+        STFT the overlap is rectangular (ones), for a CQT-type transform a
+        squared sine bell over wlen - atomHOP samples; int16 arithmetic as
+        the reference's."""
         import os
         wlen = self.stftParams['windowSizeInSamples']
         offsetTF = self.stftParams['offsets'][self.tfrepresentation]
-        hopsize = self.stftParams['hopsize']
-        overlapSamp = int(wlen - hopsize)
-        overlapFunc = np.ones(overlapSamp)
+        if self.tfrepresentation == 'stft':
+            hopsize = self.stftParams['hopsize']
+            overlapSamp = int(wlen - hopsize)
+            overlapFunc = np.ones(overlapSamp)
+        else:
+            hopsize = self.mqt.cqtkernel.atomHOP
+            overlapSamp = int(wlen - hopsize)
+            overlapFunc = slf.sinebell(2 * overlapSamp)[overlapSamp:] ** 2
         nuDataLen = int(self.totFrames * hopsize + 2 * wlen)
         for key in ('voc_output_file', 'mus_output_file'):
             data = np.zeros([nuDataLen, 2], np.int16)
@@ -462,14 +529,20 @@ class SeparateLeadProcess(object):
         self.freqMelody = freqMelody
 
     def separated_signals(self, suffix='.wav'):
-        """(vest [2][L], mest [2][L]) float waveforms before int conversion."""
-        if self.tfrepresentation != 'stft':
-            raise NotImplementedError("tfrepresentation %r: only 'stft' runs on the GPU path"
-                                      % self.tfrepresentation)
+        """(vest [2][L], mest [2][L]) float waveforms before int conversion:
+        the masked transforms inverted by the SIMM-pipeline istft, or by the
+        CQT-type transform's invertTransform (:1795-1861)."""
         P = dict(self.SIMMParams)
         if 'VUIMM' in suffix:
             P['WF0'], P['HF0'] = P['WUF0'], P['HUF0']
         vR, vL, mR, mL = separate_lead_stfts(P, self.XR, self.XL, device=self.device)
+        if self.tfrepresentation != 'stft':
+            def inv(X):
+                self.mqt.transfo = X
+                y = self.mqt.invertTransform()
+                del self.mqt.transfo
+                return y
+            return [inv(vR), inv(vL)], [inv(mR), inv(mL)]
         w = slf.sinebell(self.stftParams['windowSizeInSamples'])
         kw = dict(hopsize=self.stftParams['hopsize'], nfft=self.stftParams['NFT'], window=w,
                   originalDataLen=None, device=self.device)

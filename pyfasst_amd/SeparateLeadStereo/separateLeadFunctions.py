@@ -84,40 +84,11 @@ def _odgd_amplitudes(F0, Ot, partialMax):
                            (6 * (1 - np.exp(-temp_array)) / (temp_array ** 2))) / temp_array)
 
 
-def generate_WF0_TR_chirped(transform, minF0, maxF0, stepNotes=4, Ot=0.5, perF0=1,
-                            depthChirpInSemiTone=0.5, loadWF0=True, verbose=False,
-                            device=None):
-    """F0Table, WF0, transform = generate_WF0_TR_chirped(...)
-    (separateLeadFunctions.py:696-886).
-
-    For the STFT transform (SeparateLeadProcess' default tfrepresentation
-    'stft'), WF0[:, j] = |STFT(odgd_j)[:, middle frame]|^2 is synthesised on
-    the GPU (dict_wf0_stft, include/fasst_dict.h).  The cache file holds
-    F0Table and WF0 only (the reference also pickles the transform object).
-    The CQT / MinQT variants feed the complex odgd into those transforms;
-    they are outside the GPU path (NotImplementedError)."""
-    import os
-    if hasattr(transform, 'octaveNr') or hasattr(transform, 'cqtkernel'):
-        raise NotImplementedError("generate_WF0_TR_chirped with a CQT/MinQT transform is "
-                                  "outside the GPU path (the STFT transform is supported)")
-    lengthWindow = (transform.freqbins - 1) * 2 * 2
-    filename = ''.join(['wf0gpu_%s_' % transform.transformname, '_minF0-', str(minF0),
-                        '_maxF0-', str(maxF0), '_stepNotes-', str(int(stepNotes)),
-                        '_Ot-', str(Ot), '_perF0-', str(int(perF0)),
-                        '_depthChirp-', str(depthChirpInSemiTone),
-                        '_lengthWindow-%d' % lengthWindow, '_fs-%s' % str(transform.fs),
-                        '_ftlen-%d' % transform.ftlen, '_hop-%d' % transform.fthop,
-                        '_win-%s' % getattr(transform.winFunc, '__name__', 'w'), '.npz'])
-    if os.path.isfile(filename) and loadWF0:
-        struc = np.load(filename)
-        return struc['F0Table'], struc['WF0'], transform
-    minF0, maxF0 = np.double(minF0), np.double(maxF0)
-    Fs, stepNotes = np.double(transform.fs), np.double(stepNotes)
-    numberOfF0 = np.ceil(12.0 * stepNotes * np.log2(maxF0 / minF0)) + 1
-    F0Table = minF0 * (2 ** (np.arange(numberOfF0, dtype=np.double) / (12 * stepNotes)))
-    # columns: the F0 comb, then perF0 - 1 chirps around it (:829-879)
+def _comb_columns(F0Table, Fs, Ot, perF0, depthChirpInSemiTone):
+    """Columns of WF0 (:829-879): the F0 comb, then perF0 - 1 chirps around
+    it; per column F1, F2 and the KLGLOTT88 partial amplitudes."""
     f1, f2, amps = [], [], []
-    for i in range(int(numberOfF0)):
+    for i in range(F0Table.size):
         F0 = F0Table[i]
         f1.append(F0)
         f2.append(F0)
@@ -135,21 +106,85 @@ def generate_WF0_TR_chirped(transform, minF0, maxF0, stepNotes=4, Ot=0.5, perF0=
     A = np.zeros((ncol, pmax), dtype=np.complex128)
     for j, a in enumerate(amps):
         A[j, :a.size] = a
-    # the middle frame of the transform's STFT of an lengthWindow-sample
-    # signal (STFT.computeTransform, :838-847 with stft.py:3-69, :383-385)
-    hop = int(transform.fthop)
-    nfr = int(np.ceil(lengthWindow / np.double(hop))) + 2
-    time_stamps = np.arange(nfr) * hop / np.double(transform.fs)
-    time_stamps *= transform.fs
-    mid = int(np.argmin((lengthWindow / 2. - time_stamps) ** 2))
-    window = np.ascontiguousarray(transform.window, dtype=np.float64)
-    frame_start = mid * hop - window.size // 2
-    WF0 = np.empty((transform.freqbins, ncol))
-    f1a, f2a = np.ascontiguousarray(f1, dtype=np.float64), np.ascontiguousarray(f2, dtype=np.float64)
-    dev = _dev(device if device is not None else getattr(transform, 'device', None))
-    check(lib.dict_wf0_stft(dev, ncol, dptr(f1a), dptr(f2a), _lib.iptr(npart), pmax, dptr(A),
-                            float(Fs), int(lengthWindow), dptr(window), window.size,
-                            int(transform.ftlen), int(frame_start), dptr(WF0)), "dict_wf0_stft")
+    return (np.ascontiguousarray(f1, dtype=np.float64), np.ascontiguousarray(f2, dtype=np.float64),
+            npart, pmax, A)
+
+
+def generate_WF0_TR_chirped(transform, minF0, maxF0, stepNotes=4, Ot=0.5, perF0=1,
+                            depthChirpInSemiTone=0.5, loadWF0=True, verbose=False,
+                            device=None):
+    """F0Table, WF0, transform = generate_WF0_TR_chirped(...)
+    (separateLeadFunctions.py:696-886).
+
+    WF0[:, j] = |transform(odgd_j)[:, middle frame]|^2, the KLGLOTT88 comb
+    odgd_j synthesised on the GPU.  For the STFT transform
+    (SeparateLeadProcess' default tfrepresentation 'stft') one workgroup per
+    column synthesises and transforms only the middle frame (dict_wf0_stft,
+    include/fasst_dict.h).  For a CQT / MinQT transform (tfrepresentation
+    'cqt' / 'minqt' / 'mqt') the whole comb of FFTLen * 2^(octaveNr-1)
+    samples goes through the GPU transform and the middle column is kept
+    (dict_wf0_cqt, include/fasst_cqt.h).  The cache file holds F0Table and
+    WF0 only (the reference also pickles the transform object)."""
+    import os
+    cqt = hasattr(transform, 'cqtkernel')
+    if cqt:
+        k = transform.cqtkernel
+        if hasattr(transform, 'octaveNr'):                          # :742-744
+            lengthWindow = int(k.FFTLen * (2 ** (transform.octaveNr - 1)))
+        else:
+            lengthWindow = int(k.linFTLen)
+        geo = '_'.join(['atomhopfactor-%s' % str(transform.atomHopFactor),
+                        'bins-%s' % str(transform.bins), 'fmax-%s' % str(transform.fmax),
+                        'fmin-%s' % str(transform.fmin), 'freqbins-%s' % str(transform.freqbins),
+                        'fs-%s' % str(transform.fs),
+                        getattr(transform.winFunc, '__name__', 'w')])
+    else:
+        lengthWindow = (transform.freqbins - 1) * 2 * 2
+        geo = '_'.join(['fs-%s' % str(transform.fs), 'ftlen-%d' % transform.ftlen,
+                        'hop-%d' % transform.fthop,
+                        'win-%s' % getattr(transform.winFunc, '__name__', 'w')])
+    filename = ''.join(['wf0gpu_%s_' % transform.transformname, '_minF0-', str(minF0),
+                        '_maxF0-', str(maxF0), '_stepNotes-', str(int(stepNotes)),
+                        '_Ot-', str(Ot), '_perF0-', str(int(perF0)),
+                        '_depthChirp-', str(depthChirpInSemiTone),
+                        '_lengthWindow-%d' % lengthWindow, '_', geo, '.npz'])
+    if os.path.isfile(filename) and loadWF0:
+        struc = np.load(filename)
+        return struc['F0Table'], struc['WF0'], transform
+    minF0, maxF0 = np.double(minF0), np.double(maxF0)
+    Fs, stepNotes = np.double(transform.fs), np.double(stepNotes)
+    numberOfF0 = np.ceil(12.0 * stepNotes * np.log2(maxF0 / minF0)) + 1
+    F0Table = minF0 * (2 ** (np.arange(numberOfF0, dtype=np.double) / (12 * stepNotes)))
+    f1a, f2a, npart, pmax, A = _comb_columns(F0Table, Fs, Ot, perF0, depthChirpInSemiTone)
+    ncol = f1a.size
+    if cqt:
+        # the transform's geometry for a signal of lengthWindow samples and
+        # the reference's midindex = argmin (datalen_init / 2 - time_stamps)^2
+        F, W, nfr = transform._shape(lengthWindow)
+        maxBlock = int(k.FFTLen * (2 ** (transform.octaveNr - 1)))
+        time_stamps = (np.arange(nfr[0] * k.winNr) * k.atomHOP +
+                       k.first_center * 2 ** (transform.octaveNr - 1) - maxBlock)
+        mid = int(np.argmin((lengthWindow / 2. - time_stamps) ** 2))
+        WF0 = np.empty((F, ncol))
+        check(lib.dict_wf0_cqt(transform._context(), ncol, dptr(f1a), dptr(f2a),
+                               _lib.iptr(npart), pmax, dptr(A), float(Fs), int(lengthWindow), mid,
+                               dptr(WF0)), "dict_wf0_cqt")
+    else:
+        # the middle frame of the transform's STFT of an lengthWindow-sample
+        # signal (STFT.computeTransform, :838-847 with stft.py:3-69, :383-385)
+        hop = int(transform.fthop)
+        nfr = int(np.ceil(lengthWindow / np.double(hop))) + 2
+        time_stamps = np.arange(nfr) * hop / np.double(transform.fs)
+        time_stamps *= transform.fs
+        mid = int(np.argmin((lengthWindow / 2. - time_stamps) ** 2))
+        window = np.ascontiguousarray(transform.window, dtype=np.float64)
+        frame_start = mid * hop - window.size // 2
+        WF0 = np.empty((transform.freqbins, ncol))
+        dev = _dev(device if device is not None else getattr(transform, 'device', None))
+        check(lib.dict_wf0_stft(dev, ncol, dptr(f1a), dptr(f2a), _lib.iptr(npart), pmax, dptr(A),
+                                float(Fs), int(lengthWindow), dptr(window), window.size,
+                                int(transform.ftlen), int(frame_start), dptr(WF0)),
+              "dict_wf0_stft")
     try:
         np.savez(filename, F0Table=F0Table, WF0=WF0)
     except OSError:

@@ -106,6 +106,8 @@ SIGNATURES = {
     "cqt_forward": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
     "cqt_inverse": (ctypes.c_int, [_vp, _dp, ctypes.c_long, _dp]),
     "cqt_device_ms": (ctypes.c_int, [_vp, _dp, _dp]),
+    "dict_wf0_cqt": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _ip, ctypes.c_int, _dp,
+                                    ctypes.c_double, ctypes.c_long, ctypes.c_int, _dp]),
     # include/fasst_viterbi.h
     "viterbi_tracking": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp,
                                         ctypes.c_long, _dp, _dp, ctypes.c_long, _llp]),

@@ -43,6 +43,7 @@
 // Internal spCQT layout: frame-major [W][F] (bins contiguous, the FASST
 // engine's device layout); the C ABI hands out [F][W].
 #include "fasst_fft.h"
+#include "fasst_odgd.h"
 #include "../../include/fasst_cqt.h"
 
 #include <algorithm>
@@ -345,6 +346,44 @@ __global__ void k_icqt_lin_ola(const double *__restrict__ frames, int nfr, int N
   y[p] = y[p] + acc / (nrm == 0.0 ? 1.0 : nrm);
 }
 
+// SIMM source dictionary on a CQT / MinQT (generate_WF0_TR_chirped with a
+// CQT-type transform, separateLeadFunctions.py:742-886): the complex KLGLOTT88
+// comb of L samples, real and imaginary parts, one thread per sample
+__global__ __launch_bounds__(256) void k_odgd_synth(const double2 *__restrict__ amps, int P,
+                                                    double F1, double F2, double fs, long L,
+                                                    double *__restrict__ re,
+                                                    double *__restrict__ im) {
+  extern __shared__ __attribute__((aligned(16))) double2 amp[];
+  for (int h = threadIdx.x; h < P; h += blockDim.x) amp[h] = amps[h];
+  __syncthreads();
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L) return;
+  const double2 z = odgd_sample(amp, P, F1, F2, fs, 2.0 * (double)L / fs, t);
+  re[t] = z.x;
+  im[t] = z.y;
+}
+
+// column `col` of the transform ([W][F] frame-major) -> WF0[:, j]:
+// pass 0 keeps T(Re odgd); pass 1 forms T(odgd) = T(Re) + i T(Im) on the CQT
+// rows (the transform is linear in the signal) and T(Re) on the MinQT linear
+// rows (computeLinearPart's rfft keeps the real part of its frames), then
+// |.|^2 (np.abs(transfo[:, midindex]) ** 2)
+__global__ __launch_bounds__(256) void k_wf0_take(const double2 *__restrict__ sp, int F, int col,
+                                                  int ncq, int pass, double2 *__restrict__ keep,
+                                                  double *__restrict__ wf0, int n_cols, int j) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= F) return;
+  const double2 v = sp[(size_t)col * F + k];
+  if (pass == 0) {
+    keep[k] = v;
+    return;
+  }
+  const double2 r = keep[k];
+  const double2 z = k < ncq ? make_double2(r.x - v.y, r.y + v.x) : r;
+  const double m = hypot(z.x, z.y);
+  wf0[(size_t)k * n_cols + j] = m * m;
+}
+
 }  // namespace fasst
 
 using namespace fasst;
@@ -466,6 +505,56 @@ int filtfilt(cqt_ctx *c, const double *src, long n, int up, double *out, int dec
 int set_smem(const void *fn, size_t bytes) {
   if (bytes > 64 * 1024)
     FASST_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return FASST_OK;
+}
+
+// the transform of the padded signal in c->xp into c->sp ([W][F], frame-major)
+int forward_dev(cqt_ctx *c, const Geo &g, hipStream_t s) {
+  int st;
+  FASST_HIP(hipMemsetAsync(c->sp.p, 0, (size_t)g.W * g.F * sizeof(double2), s));
+  if (c->lin_N && g.W > g.drop0) {   // computeLinearPart on the padded signal
+    const long off = (long)c->first_center - c->lin_N / 2;
+    k_cqt_linear<<<g.W - g.drop0, 256, c->lin_N * sizeof(double2), s>>>(
+        c->xp.p, g.Lp, off, c->lwin.p, c->ltw_f.p, c->lin_N, c->lin_logN, c->atom_hop, g.drop0,
+        c->kmax, c->bins * c->oct, g.F, c->sp.p);
+    FASST_LAUNCH_CHECK();
+  }
+  const double *cur = c->xp.p;
+  double *next = c->sa.p;
+  for (int i = 0; i < c->oct; ++i) {
+    const int nfr = g.nfr[i];
+    if (c->nb > 0) {
+      k_cqt_frames<<<nfr, 256, c->N * sizeof(double2), s>>>(cur, g.len[i], c->fft_hop, c->tw_f.p,
+                                                           c->N, c->logN, c->kb, c->nb, c->nbp,
+                                                           c->XX.p);
+      FASST_LAUNCH_CHECK();
+      BandArgs a;
+      a.K = c->K.p;
+      a.XX = c->XX.p;
+      a.sp = c->sp.p;
+      a.M = c->M;
+      a.nb = c->nb;
+      a.nbp = c->nbp;
+      a.kb = c->kb;
+      a.N = c->N;
+      a.nfr = nfr;
+      a.win_nr = c->win_nr;
+      a.nshifts = 1 << i;
+      a.row0 = c->bins * (c->oct - i - 1);
+      a.W = g.W;
+      a.F = g.F;
+      a.d = g.d[i];
+      a.inc = (double)c->atom_hop / (double)(1L << i);
+      k_cqt_band<<<dim3((nfr + kBandFrames - 1) / kBandFrames, 1 << i), 256,
+                   kBandFrames * c->nbp * sizeof(double2), s>>>(a);
+      FASST_LAUNCH_CHECK();
+    }
+    if (i != c->oct - 1) {
+      if ((st = filtfilt(c, cur, g.len[i], 0, next, 1, 1.0))) return st;
+      cur = next;
+      next = (next == c->sa.p) ? c->sb.p : c->sa.p;
+    }
+  }
   return FASST_OK;
 }
 
@@ -655,50 +744,7 @@ int cqt_forward(cqt_ctx *c, const double *x, long L, double *sp) {
   FASST_HIP(hipMemsetAsync(c->xp.p, 0, g.Lp * sizeof(double), s));
   FASST_HIP(hipMemcpyAsync(c->xp.p + g.maxBlock, x, L * sizeof(double), hipMemcpyHostToDevice, s));
   FASST_HIP(hipEventRecord(c->ev[0], s));
-  FASST_HIP(hipMemsetAsync(c->sp.p, 0, (size_t)g.W * g.F * sizeof(double2), s));
-  if (c->lin_N && g.W > g.drop0) {   // computeLinearPart on the padded signal
-    const long off = (long)c->first_center - c->lin_N / 2;
-    k_cqt_linear<<<g.W - g.drop0, 256, c->lin_N * sizeof(double2), s>>>(
-        c->xp.p, g.Lp, off, c->lwin.p, c->ltw_f.p, c->lin_N, c->lin_logN, c->atom_hop, g.drop0,
-        c->kmax, c->bins * c->oct, g.F, c->sp.p);
-    FASST_LAUNCH_CHECK();
-  }
-  const double *cur = c->xp.p;
-  double *next = c->sa.p;
-  for (int i = 0; i < c->oct; ++i) {
-    const int nfr = g.nfr[i];
-    if (c->nb > 0) {
-      k_cqt_frames<<<nfr, 256, c->N * sizeof(double2), s>>>(cur, g.len[i], c->fft_hop, c->tw_f.p,
-                                                           c->N, c->logN, c->kb, c->nb, c->nbp,
-                                                           c->XX.p);
-      FASST_LAUNCH_CHECK();
-      BandArgs a;
-      a.K = c->K.p;
-      a.XX = c->XX.p;
-      a.sp = c->sp.p;
-      a.M = c->M;
-      a.nb = c->nb;
-      a.nbp = c->nbp;
-      a.kb = c->kb;
-      a.N = c->N;
-      a.nfr = nfr;
-      a.win_nr = c->win_nr;
-      a.nshifts = 1 << i;
-      a.row0 = c->bins * (c->oct - i - 1);
-      a.W = g.W;
-      a.F = g.F;
-      a.d = g.d[i];
-      a.inc = (double)c->atom_hop / (double)(1L << i);
-      k_cqt_band<<<dim3((nfr + kBandFrames - 1) / kBandFrames, 1 << i), 256,
-                   kBandFrames * c->nbp * sizeof(double2), s>>>(a);
-      FASST_LAUNCH_CHECK();
-    }
-    if (i != c->oct - 1) {
-      if ((st = filtfilt(c, cur, g.len[i], 0, next, 1, 1.0))) return st;
-      cur = next;
-      next = (next == c->sa.p) ? c->sb.p : c->sa.p;
-    }
-  }
+  if ((st = forward_dev(c, g, s))) return st;
   k_cqt_transpose<<<dim3((g.F + 15) / 16, (g.W + 15) / 16), 256, 0, s>>>(c->sp.p, c->sph.p, g.W,
                                                                           g.F);
   FASST_LAUNCH_CHECK();
@@ -814,6 +860,67 @@ int cqt_inverse(cqt_ctx *c, const double *sp, long L, double *y) {
   FASST_HIP(hipMemcpyAsync(y, yout, L * sizeof(double), hipMemcpyDeviceToHost, s));
   FASST_HIP(hipStreamSynchronize(s));
   FASST_HIP(hipEventElapsedTime(&c->ms_inv, c->ev[2], c->ev[3]));
+  return FASST_OK;
+}
+
+int dict_wf0_cqt(cqt_ctx *c, int n_cols, const double *f1, const double *f2,
+                 const int *n_partials, int max_partials, const double *amps, double fs,
+                 long length_odgd, int col, double *wf0) {
+  if (!c || n_cols < 1 || max_partials < 1 || !f1 || !f2 || !n_partials || !amps || !wf0 ||
+      fs <= 0) {
+    set_error("dict_wf0_cqt: bad arguments (cols %d, partials %d)", n_cols, max_partials);
+    return FASST_ERR_SHAPE;
+  }
+  for (int j = 0; j < n_cols; ++j)
+    if (n_partials[j] < 0 || n_partials[j] > max_partials) {
+      set_error("dict_wf0_cqt: column %d has %d partials > %d", j, n_partials[j], max_partials);
+      return FASST_ERR_SHAPE;
+    }
+  if ((size_t)max_partials * sizeof(double2) > 64 * 1024) {
+    set_error("dict_wf0_cqt: %d partials exceed the LDS", max_partials);
+    return FASST_ERR_SHAPE;
+  }
+  Geo g;
+  int st = geometry(c, length_odgd, g);
+  if (st) return st;
+  if (col < 0 || col >= g.W) {
+    set_error("dict_wf0_cqt: column %d outside the %d frames", col, g.W);
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard dg(c->device);
+  if ((st = ensure_work(c, g, length_odgd))) return st;
+  const long L = length_odgd;
+  DBuf<double2> damps, keep;
+  DBuf<double> dim, dout;
+  if ((st = damps.alloc((size_t)n_cols * max_partials)) || (st = keep.alloc(g.F)) ||
+      (st = dim.alloc(L)) || (st = dout.alloc((size_t)g.F * n_cols)))
+    return st;
+  FASST_HIP(hipMemcpy(damps.p, amps, (size_t)n_cols * max_partials * sizeof(double2),
+                      hipMemcpyHostToDevice));
+  hipStream_t s = c->stream;
+  FASST_HIP(hipMemsetAsync(c->xp.p, 0, g.Lp * sizeof(double), s));   // the zero padding
+  FASST_HIP(hipEventRecord(c->ev[0], s));
+  const int ncq = c->bins * c->oct;
+  const int gF = (g.F + 255) / 256;
+  for (int j = 0; j < n_cols; ++j) {
+    k_odgd_synth<<<(int)((L + 255) / 256), 256, max_partials * sizeof(double2), s>>>(
+        damps.p + (size_t)j * max_partials, n_partials[j], f1[j], f2[j], fs, L,
+        c->xp.p + g.maxBlock, dim.p);
+    FASST_LAUNCH_CHECK();
+    if ((st = forward_dev(c, g, s))) return st;
+    k_wf0_take<<<gF, 256, 0, s>>>(c->sp.p, g.F, col, ncq, 0, keep.p, dout.p, n_cols, j);
+    FASST_LAUNCH_CHECK();
+    FASST_HIP(hipMemcpyAsync(c->xp.p + g.maxBlock, dim.p, L * sizeof(double),
+                             hipMemcpyDeviceToDevice, s));
+    if ((st = forward_dev(c, g, s))) return st;
+    k_wf0_take<<<gF, 256, 0, s>>>(c->sp.p, g.F, col, ncq, 1, keep.p, dout.p, n_cols, j);
+    FASST_LAUNCH_CHECK();
+  }
+  FASST_HIP(hipEventRecord(c->ev[1], s));
+  FASST_HIP(hipMemcpyAsync(wf0, dout.p, (size_t)g.F * n_cols * sizeof(double),
+                           hipMemcpyDeviceToHost, s));
+  FASST_HIP(hipStreamSynchronize(s));
+  FASST_HIP(hipEventElapsedTime(&c->ms_fwd, c->ev[0], c->ev[1]));
   return FASST_OK;
 }
 

@@ -10,6 +10,7 @@
 // same double operations -- windows them into LDS and runs the radix-2 FFT in
 // LDS; the column of |X|^2 is written straight into WF0.
 #include "fasst_fft.h"
+#include "fasst_odgd.h"
 #include "../../include/fasst_dict.h"
 
 #include <algorithm>
@@ -36,33 +37,14 @@ __global__ __launch_bounds__(256) void k_wf0_column(const DictArgs a) {
   const int j = blockIdx.x;
   const int P = a.np_[j];
   const double F1 = a.f1[j], F2 = a.f2[j];
-  const bool chirp = F1 != F2;
   for (int h = threadIdx.x; h < P; h += blockDim.x) amp[h] = a.amps[(size_t)j * a.max_partials + h];
   __syncthreads();
-  const double two_pi = 2.0 * M_PI;
-  const double w1 = two_pi * F1;                       // (2j pi F0) imaginary part
-  const double dF = F2 - F1, den = 2.0 * (double)a.length_odgd / a.fs;
+  const double den = 2.0 * (double)a.length_odgd / a.fs;
   for (int i = threadIdx.x; i < a.nfft; i += blockDim.x) {
     double v = 0.0;
     const long t = a.frame_start + i;
-    if (i < a.wlen && t >= 0 && t < a.length_odgd) {
-      const double ts = (double)t / a.fs;           // np.arange(L) / Fs (+ t0/F0 = 0)
-      double re = 0.0;
-      for (int h = 0; h < P; ++h) {
-        const double fh = (double)(h + 1);
-        double th;
-        if (!chirp) {
-          th = (w1 * fh) * ts;
-        } else {
-          th = two_pi * ((F1 * fh) * ts + ((dF * fh) * (ts * ts)) / den);
-        }
-        double s, c;
-        sincos(th, &s, &c);
-        const double2 am = amp[h];
-        re += c * am.x - s * am.y;                     // Re(exp(i th) * amp)
-      }
-      v = a.win[i] * re;
-    }
+    if (i < a.wlen && t >= 0 && t < a.length_odgd)
+      v = a.win[i] * odgd_sample(amp, P, F1, F2, a.fs, den, t).x;
     buf[bitrev(i, a.logn)] = make_double2(v, 0.0);
   }
   __syncthreads();

@@ -431,6 +431,41 @@ def run_wf0():
     print("wf0", {k: np.shape(v) for k, v in out.items()})
 
 
+def run_wf0_cqt():
+    """generate_WF0_TR_chirped on CQT-type transforms (separateLeadFunctions.py
+    :742-886 with the tft.py registry's MinQTransfo / CQTransfo, as
+    SeparateLeadProcess.computeWF0 builds them for tfrepresentation 'mqt' /
+    'cqt', SeparateLeadStereoTF.py:656-681): the complex comb goes through
+    the transform; with and without chirps."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import shutil
+    work = "/tmp/golden_wf0_cqt"
+    shutil.rmtree(work, ignore_errors=True)
+    os.makedirs(work)
+    os.chdir(work)          # the reference writes its .npz cache to the cwd
+    import numpy as np
+    from pyfasst.SeparateLeadStereo import separateLeadFunctions as slf
+    from pyfasst.tftransforms import tft
+    from pyfasst.tools.utils import sqrt_blackmanharris
+    out = {}
+    for tag, (kind, fs, nft, fmin, fmax, bins, minF0, maxF0, stepNotes, perF0) in {
+            'm1': ('mqt', 8000, 512, 50, 4000, 12, 100, 800, 4, 1),
+            'm2': ('mqt', 8000, 1024, 60, 4000, 24, 150, 600, 2, 3),
+            'c1': ('cqt', 8000, 512, 100, 1600, 12, 100, 400, 2, 1)}.items():
+        t = tft.tftransforms[kind](fmin=fmin, fmax=fmax, bins=bins, fs=fs, linFTLen=nft,
+                                   atomHopFactor=0.25, winFunc=sqrt_blackmanharris, perfRast=1)
+        F0Table, WF0, _ = slf.generate_WF0_TR_chirped(
+            transform=t, minF0=minF0, maxF0=maxF0, stepNotes=stepNotes, Ot=0.5, perF0=perF0,
+            depthChirpInSemiTone=0.5, loadWF0=False)
+        out['F0Table_' + tag], out['WF0_' + tag] = F0Table, WF0
+        out['cfg_' + tag] = np.array([fs, nft, fmin, fmax, bins, minF0, maxF0, stepNotes, perF0],
+                                     dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "wf0_cqt.npz"), **out)
+    print("wf0_cqt", {k: np.shape(v) for k, v in out.items()})
+
+
 def run_nmfinit(same):
     """initialize_all_spec_comps_with_NMF (audioModel.py:2091-2222) on a
     seeded model, then 2 GEM iterations from that initial state."""
@@ -518,6 +553,68 @@ def run_pipeline():
     print("pipeline", {k: np.shape(v) for k, v in out.items()})
 
 
+def pipeline_signal(fs, n, seed=61):
+    """The stepped-melody stereo test signal of the pipeline fixtures."""
+    import numpy as np
+    rs = np.random.RandomState(seed)
+    t = np.arange(n) / float(fs)
+    f0 = 220 * 2 ** (np.floor(t * 2) / 12.)                 # a stepped melody
+    lead = sum(np.sin(2 * np.pi * h * np.cumsum(f0) / fs) / h for h in range(1, 8))
+    acc = np.convolve(rs.randn(n), np.ones(9) / 9., mode='same') * 0.7
+    x = np.stack([0.7 * lead + 0.4 * acc, 0.5 * lead + 0.6 * np.roll(acc, 5)], axis=1)
+    return (x / np.abs(x).max() * 12000).astype(np.int16)
+
+
+def run_pipeline_mqt():
+    """The lead/accompaniment pipeline on the MinQT, tfrepresentation='mqt'
+    (the reference's own MinQTSLStest, pyfasst_tests/.../
+    test_SeparateLeadStereoTF.py:40-47): WF0 on the MinQT
+    (SeparateLeadStereoTF.py:656-700), chunked mono SIMM with the
+    startincqt realignment (:1023-1032), Viterbi, chunked stereo SIMM, the
+    MinQT inverse of each masked chunk (:1802-1861) and the sine-bell^2
+    overlap-add (:1481-1491); 5 s at 8 kHz, 3 chunks of 140, 140 and 35
+    frames (maxFrames=100 would leave the last 78 frames unestimated: the
+    reference's chunk count 315 // 79 = 3, :1880-1897, whose all-zero HF0
+    makes the Viterbi tail a tie)."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import shutil
+    import numpy as np
+    import scipy.io.wavfile as wf
+    from pyfasst.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    from pyfasst.SeparateLeadStereo.tracking import tracking as TR
+
+    def tracker(S_, N_, logD, prior, logT, verbose=False):
+        return TR.viterbiTrackingArray(logD[:S_, :N_], prior[:S_], logT[:S_, :S_])
+    SL.viterbiTrackingArray = tracker
+    work = "/tmp/golden_pipeline_mqt"
+    shutil.rmtree(work, ignore_errors=True)
+    os.makedirs(work)
+    os.chdir(work)
+    fs = 8000
+    x = pipeline_signal(fs, 40000)
+    wav = os.path.join(work, "mix.wav")
+    wf.write(wav, fs, x)
+    np.random.seed(3)
+    proc = SL.SeparateLeadProcess(wav, windowSize=0.0464, nbIter=3, numCompAccomp=6, minF0=100,
+                                  maxF0=800, stepNotes=4, K_numFilters=3, P_numAtomFilters=10,
+                                  verbose=False, outputDirSuffix='out', tfrepresentation='mqt',
+                                  cqtbins=12, cqtfmin=50)
+    proc.autoMelSepAndWrite(maxFrames=140)
+    out = {'wav': x, 'fs': np.array(fs), 'WF0': proc.SIMMParams['WF0'],
+           'WGAMMA': proc.SIMMParams['WGAMMA'], 'F0Table': proc.SIMMParams['F0Table'],
+           'indexBestPath': np.array(proc.indexBestPath), 'freqMelody': np.array(proc.freqMelody),
+           'HF00': proc.SIMMParams['HF00'], 'totFrames': np.array(proc.totFrames),
+           'hopsize': np.array(proc.stftParams['hopsize']),
+           'window': np.array(proc.stftParams['windowSizeInSamples']),
+           'lead': wf.read(proc.files['voc_output_file'])[1],
+           'acc': wf.read(proc.files['mus_output_file'])[1],
+           'pitches': np.loadtxt(proc.files['pitch_output_file'])}
+    np.savez_compressed(os.path.join(HERE, "pipeline_mqt.npz"), **out)
+    print("pipeline_mqt", {k: np.shape(v) for k, v in out.items()})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -542,13 +639,14 @@ if __name__ == "__main__":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
          "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0, "nmfinit_same": lambda: run_nmfinit(True),
-         "nmfinit_indiv": lambda: run_nmfinit(False), "pipeline": run_pipeline}.get(
+         "nmfinit_indiv": lambda: run_nmfinit(False), "pipeline": run_pipeline,
+         "wf0_cqt": run_wf0_cqt, "pipeline_mqt": run_pipeline_mqt}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
     names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0", "nmfinit_same",
-                              "nmfinit_indiv", "pipeline"] + list(CASES))
+                              "nmfinit_indiv", "pipeline", "wf0_cqt", "pipeline_mqt"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

@@ -74,9 +74,32 @@ def test_hann_basis_exact():
                                                             overlap=ov), g['WGAMMA_' + tag])
 
 
-def test_wf0_cqt_transform_not_on_gpu_path():
+CQT_CASES = ("m1", "m2", "c1")
+
+
+@pytest.mark.parametrize("tag", CQT_CASES)
+def test_wf0_cqt_golden_gpu(tag, tmp_path, monkeypatch):
+    """generate_WF0_TR_chirped on a MinQT / CQT transform (dict_wf0_cqt: the
+    complex comb through the GPU transform by linearity) vs the reference run
+    (tests/golden/wf0_cqt.npz), to 1e-10 of each column's peak."""
     from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
-    from pyfasst_amd.tftransforms.minqt import MinQTransfo
-    t = MinQTransfo(fmin=100, fmax=3000, bins=12, fs=8000, linFTLen=256, perfRast=1)
-    with pytest.raises(NotImplementedError):
-        slf.generate_WF0_TR_chirped(t, 100, 800)
+    from pyfasst_amd.tftransforms import tft
+    from pyfasst_amd.tools.utils import sqrt_blackmanharris
+    monkeypatch.chdir(tmp_path)
+    g = load("wf0_cqt")
+    fs, nft, fmin, fmax, bins, minF0, maxF0, stepNotes, perF0 = g['cfg_' + tag]
+    kind = 'cqt' if tag[0] == 'c' else 'mqt'
+
+    def make():
+        return tft.tftransforms[kind](fmin=fmin, fmax=fmax, bins=int(bins), fs=fs,
+                                      linFTLen=int(nft), atomHopFactor=0.25,
+                                      winFunc=sqrt_blackmanharris, perfRast=1)
+    F0Table, WF0, t = slf.generate_WF0_TR_chirped(make(), minF0, maxF0, stepNotes=stepNotes,
+                                                  perF0=int(perF0), loadWF0=False)
+    np.testing.assert_array_equal(F0Table, g['F0Table_' + tag])
+    assert WF0.shape == g['WF0_' + tag].shape
+    assert _colrel(WF0, g['WF0_' + tag]) < 1e-10
+    # the cache round trip returns the same arrays
+    _, WF0b, _ = slf.generate_WF0_TR_chirped(make(), minF0, maxF0, stepNotes=stepNotes,
+                                             perF0=int(perF0), loadWF0=True)
+    np.testing.assert_array_equal(WF0b, WF0)

@@ -195,6 +195,24 @@ def test_wf0_dictionaries_golden():
                                       g['WGAMMA_' + tag])
 
 
+@pytest.mark.parametrize("tag", ["m1", "m2", "c1"])
+def test_wf0_cqt_dictionaries_golden(tag):
+    """generate_WF0_TR_chirped on a MinQT / CQT transform (the complex comb
+    through the transform, separateLeadFunctions.py:742-886) vs the reference
+    run (tests/golden/wf0_cqt.npz)."""
+    import cqt_ref
+    import dict_ref as D
+    g = load("wf0_cqt")
+    fs, nft, fmin, fmax, bins, minF0, maxF0, stepNotes, perF0 = g['cfg_' + tag]
+    kind = 'cqt' if tag[0] == 'c' else 'mqt'
+    t = cqt_ref.RefCQT(kind, fmin=fmin, fmax=fmax, bins=int(bins), fs=fs, linFTLen=int(nft))
+    F0Table, WF0 = D.generate_wf0_tr_chirped_cqt(t, minF0, maxF0, stepNotes, perF0=int(perF0))
+    np.testing.assert_array_equal(F0Table, g['F0Table_' + tag])
+    ref = g['WF0_' + tag]
+    assert WF0.shape == ref.shape
+    assert float(np.max(np.abs(WF0 - ref) / np.max(ref, axis=0))) < 1e-12
+
+
 @pytest.mark.parametrize("same", [True, False])
 def test_nmf_init_golden(same):
     """initialize_all_spec_comps_with_NMF (audioModel.py:2091-2222), then EM."""
