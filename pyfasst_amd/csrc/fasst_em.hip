@@ -513,6 +513,32 @@ static constexpr size_t estep_mx_smem() {
 // into ds_read2_b64 / ds_read2st64_b64, which take 8 LDS cycles for the 4 of
 // two ds_read_b64 -- MI355X_MICROARCH.md §LDS -- and the LDS is this kernel's
 // busiest unit)
+// raw-buffer forms of the E-step's streaming accesses: wave-uniform
+// resource (SGPRs, formed on the scalar unit) + 32-bit per-lane offset, so
+// no 64-bit VALU address arithmetic per access (aux 2 = non-temporal)
+typedef unsigned es_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t es_rsrc(const double *p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, 0x7fffffff, 0x00020000);
+}
+template <int AUX>
+__device__ __forceinline__ double es_ld(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+  const es_u2 x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, (int)so, AUX);
+  return __builtin_bit_cast(double, x);
+}
+template <int AUX>
+__device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(es_u2, v), r, (int)vo, (int)so, AUX);
+}
+
+#ifndef ESTEP_LL_SELECT
+#define ESTEP_LL_SELECT 0
+#endif
+#ifndef ESTEP_NO_STOREHAT
+#define ESTEP_NO_STOREHAT 1
+#endif
+#ifndef ESTEP_SADDR
+#define ESTEP_SADDR 1
+#endif
 template <int J, int NKS, int RKU>
 __global__ __launch_bounds__(256, J > 4 ? 1 : 2)
 __attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) FASST_NO_LDS_PAIRING
@@ -589,7 +615,16 @@ void k_estep_mx(const EArgs a) {
 
   const int tb = a.tbase + blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
-  for (int tt = tb + wv; tt < te; tt += 4) {
+  // SA: wave-uniform buffer resources (SGPRs, formed on the scalar unit) +
+  // 32-bit per-lane byte offsets instead of one 64-bit VALU address
+  // computation per access (J <= 4: the J = 8, K = 64 instantiation trips a
+  // compiler crash in ROCm 7.2's AGPR-copy rewrite with it)
+  constexpr bool SA = ESTEP_SADDR && J <= 4;
+  int wvu = wv;
+  if constexpr (SA) wvu = __builtin_amdgcn_readfirstlane(wv);
+  const unsigned vo_tw = (unsigned)(tq * a.Tp + fl) * 8u;   // TW[j][k = tq + 4s][t0 + fl]
+  const unsigned vo_cx = (unsigned)(tq * a.Fp + f) * 8u;    // plane[t0 + tq + 4i][f]
+  for (int tt = tb + wvu; tt < te; tt += 4) {
     const int t0 = tt * 16;
     int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
     asm volatile("" : "+v"(lofs));
@@ -603,16 +638,27 @@ void k_estep_mx(const EArgs a) {
     for (int j = 0; j < JA; ++j) {
       const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) twv[j][s] = tw[(size_t)(4 * s) * a.Tp];
+      for (int s = 0; s < NKS; ++s)
+        twv[j][s] = SA ? es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u)
+                       : tw[(size_t)(4 * s) * a.Tp];
     }
     double cxv[4][4];  // this tile's Cx, in flight with the TW operands
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
-      cxv[0][i] = __builtin_nontemporal_load(a.cx00 + off);
-      cxv[1][i] = __builtin_nontemporal_load(a.cx11 + off);
-      cxv[2][i] = __builtin_nontemporal_load(a.cxr + off);
-      cxv[3][i] = __builtin_nontemporal_load(a.cxi + off);
+      if constexpr (SA) {
+        const size_t ro = (size_t)t0 * a.Fp;
+        const unsigned so = (unsigned)(4 * i * a.Fp) * 8u;
+        cxv[0][i] = es_ld<2>(es_rsrc(a.cx00 + ro), vo_cx, so);
+        cxv[1][i] = es_ld<2>(es_rsrc(a.cx11 + ro), vo_cx, so);
+        cxv[2][i] = es_ld<2>(es_rsrc(a.cxr + ro), vo_cx, so);
+        cxv[3][i] = es_ld<2>(es_rsrc(a.cxi + ro), vo_cx, so);
+      } else {
+        const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
+        cxv[0][i] = __builtin_nontemporal_load(a.cx00 + off);
+        cxv[1][i] = __builtin_nontemporal_load(a.cx11 + off);
+        cxv[2][i] = __builtin_nontemporal_load(a.cxr + off);
+        cxv[3][i] = __builtin_nontemporal_load(a.cxi + off);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     d4 v[J];
@@ -651,6 +697,17 @@ void k_estep_mx(const EArgs a) {
       det = sg * fmax(fabs(det), kEps);
       const double rdet = rcp_nr(det);
       const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
+#if ESTEP_LL_SELECT
+      {
+        // (branch-free form: padding points contribute x = 1, i.e. nothing)
+        const bool ok = fvalid && t < a.T;
+        const double x = ok ? det * M_PI : 1.0;
+        lev += (double)__builtin_amdgcn_frexp_exp(x);
+        lm *= __builtin_amdgcn_frexp_mant(x);
+        xmin = fmin(xmin, x);
+        ll += ok ? i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi) : 0.0;
+      }
+#else
       if (fvalid && t < a.T) {
         // log(det pi) as mantissa product x 2^exponent (v_frexp_*: 0, inf and
         // NaN pass through the mantissa, so log(lm) gives -inf / inf / NaN as
@@ -662,6 +719,7 @@ void k_estep_mx(const EArgs a) {
         xmin = fmin(xmin, x);
         ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
       }
+#endif
       // P = Cx S, N = S Cx S - S = P^H S - S
       const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
       const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
@@ -710,11 +768,15 @@ void k_estep_mx(const EArgs a) {
                           2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i);
         const double q = RKU == 1 ? qa : qa * inv_rk[j];
         double val;
-        if (a.store_hat)
+        if (!ESTEP_NO_STOREHAT && a.store_hat)
           val = fabs((Vj * Vj) * q + Vj);
         else
           val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
-        __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
+        if constexpr (SA)
+          es_st<2>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
+                   (unsigned)(4 * i * a.Fp) * 8u);
+        else
+          __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
       }
       // the slab writes above must land before the cross-lane reads below
       // (LDS is in order within a wave; this keeps the compiler in order too)
@@ -1582,6 +1644,12 @@ __device__ void tw_apply_tiles(const TArgs &a, int j, int tt0, int lane) {
 // TBQ (the TB step of a component with time blobs, :1931-1978): H has moved
 // since the step's start, so other = max(V_c_old, eps) comes from a plane,
 // hatW is hat_W_j itself, and num's ratio is hat_W / max(V_new^2, eps).
+#ifndef TW_1CHAIN
+#define TW_1CHAIN 0
+#endif
+#ifndef TW_EDGE_SPLIT
+#define TW_EDGE_SPLIT 0
+#endif
 template <int NKC, int TPW, bool BLK = false, bool LAM = false, bool TBQ = false>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
@@ -1644,7 +1712,17 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
         h[2] = h23.x;
         h[3] = h23.y;
       }
-      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
+      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
+#if TW_1CHAIN
+      // one accumulation chain per product (vo and vn interleaved): no
+      // partial-sum adds
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        if constexpr (!TBQ) vo = mfma4(ao[s], bt[p][s], vo);
+        vn = mfma4(an[s], bt[p][s], vn);
+      }
+#else
+      d4 vo2 = vo, vn2 = vo;
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
         if constexpr (!TBQ) {
@@ -1656,38 +1734,48 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       }
       vo += vo2;
       vn += vn2;
-      const bool tok = t < a.T;
-      double r3[4], r4[4];
+#endif
+      // EDGE = false for interior tiles (every bin < F and frame < T: all but
+      // the last bin and frame tiles): no per-point padding masks there
+      auto form = [&](auto edge_c) {
+        constexpr bool EDGE = decltype(edge_c)::value;
+        const bool tok = !EDGE || t < a.T;
+        double r3[4], r4[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double vm = fmax(vn[i], kEps);
-        const double rv = rcp_nr(vm);
-        const bool ok = tok && f0 + bq + bs * i < a.F;
-        const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + bq + bs * i;
-        double other, q;
-        if constexpr (TBQ) {
-          other = ok ? a.oth[o] : 0.0;
-          q = h[i] / fmax(vm * vm, kEps);   // hat_W / max(V^2, eps) (:1971-1973)
-        } else {
-          other = fmax(vo[i], kEps);
-          q = (h[i] * other) * (rv * rv);   // hat_W from the E-step's rho
+        for (int i = 0; i < 4; ++i) {
+          const double vm = fmax(vn[i], kEps);
+          const double rv = rcp_nr(vm);
+          const bool ok = !EDGE || (tok && f0 + bq + bs * i < a.F);
+          const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + bq + bs * i;
+          double other, q;
+          if constexpr (TBQ) {
+            other = ok ? a.oth[o] : 0.0;
+            q = h[i] / fmax(vm * vm, kEps);   // hat_W / max(V^2, eps) (:1971-1973)
+          } else {
+            other = fmax(vo[i], kEps);
+            q = (h[i] * other) * (rv * rv);   // hat_W from the E-step's rho
+          }
+          if constexpr (LAM) {   // corrPen terms (audioModel.py:1650-1719)
+            const double cp = ok ? a.cp[o] : 0.0, pw = ok ? a.pw[o] : 1.0;
+            r3[i] = ok ? other * (q + cp * (2.0 * (vm / pw))) : 0.0;
+            r4[i] = ok ? other * (rv + cp) : 0.0;
+          } else {
+            r3[i] = ok ? other * q : 0.0;
+            r4[i] = ok ? other * rv : 0.0;
+          }
         }
-        if constexpr (LAM) {   // corrPen terms (audioModel.py:1650-1719)
-          const double cp = ok ? a.cp[o] : 0.0, pw = ok ? a.pw[o] : 1.0;
-          r3[i] = ok ? other * (q + cp * (2.0 * (vm / pw))) : 0.0;
-          r4[i] = ok ? other * (rv + cp) : 0.0;
-        } else {
-          r3[i] = ok ? other * q : 0.0;
-          r4[i] = ok ? other * rv : 0.0;
-        }
-      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int kc = 0; kc < NKC; ++kc) {
-          num[p][kc] = mfma4(r3[i], bw[i][kc], num[p][kc]);
-          den[p][kc] = mfma4(r4[i], bw[i][kc], den[p][kc]);
-        }
+          for (int kc = 0; kc < NKC; ++kc) {
+            num[p][kc] = mfma4(r3[i], bw[i][kc], num[p][kc]);
+            den[p][kc] = mfma4(r4[i], bw[i][kc], den[p][kc]);
+          }
+      };
+      if (TW_EDGE_SPLIT && f0 + 16 <= a.F && (tt0 + p) * 16 + 16 <= a.T)
+        form(std::false_type{});
+      else
+        form(std::true_type{});
     }
   }
   const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Tp;
