@@ -257,7 +257,7 @@ def main():
         dom = max(times, key=lambda k: times[k][0])
         rl = None
         pmc = None
-        pmc_path = os.environ.get("FASST_PMC_JSON", os.path.join(ROOT, "profiles", "r2c_bench.json"))
+        pmc_path = os.environ.get("FASST_PMC_JSON", os.path.join(ROOT, "profiles", "r3_bench.json"))
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))["kernels"]

@@ -49,6 +49,15 @@ int fasst_device_count(int *n);
  * C x r), 1 = 'conv' (params r x C x F).  Reconfiguring keeps Cx / X.       */
 int fasst_create(int device, int F, int T, fasst_ctx **out);
 int fasst_configure(fasst_ctx *ctx, int J, const int *rank, const int *K, int mix_conv);
+/* The same with the mixing type per spatial component (mix_conv[J], the
+ * reference's per-component 'mix_type', retrieve_subsrc_params
+ * audioModel.py:546-576).  In a model with both types, the mixing update
+ * (update_mix_matrix :766-889) runs the 'inst' update over the free 'inst'
+ * components with every other component held fixed; the reference's 'conv'
+ * solve (:854-863) can only run when no other component exists, so its
+ * free 'conv' components in a mixed model are rejected by the host layer. */
+int fasst_configure_types(fasst_ctx *ctx, int J, const int *rank, const int *K,
+                          const int *mix_conv);
 int fasst_destroy(fasst_ctx *ctx);
 
 /* comp_transf_Cx (audioModel.py:250-302) on the device: data[L][2] float64

@@ -41,6 +41,7 @@ SIGNATURES = {
     "fasst_device_count": (ctypes.c_int, [_ip]),
     "fasst_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
     "fasst_configure": (ctypes.c_int, [_vp, ctypes.c_int, _ip, _ip, ctypes.c_int]),
+    "fasst_configure_types": (ctypes.c_int, [_vp, ctypes.c_int, _ip, _ip, _ip]),
     "fasst_destroy": (ctypes.c_int, [_vp]),
     "fasst_set_audio": (ctypes.c_int, [_vp, _dp, ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int]),

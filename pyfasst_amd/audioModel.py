@@ -176,8 +176,10 @@ class FASST(object):
         HIP path: stereo; single-factor NMF spectral components (TW_constr
         'NMF'; FB, FW, TW each free or fixed; time blobs TB, free or fixed, or
         none), one or several per spatial component (comp_spat_comp_power sums
-        them, :469-498); all spatial components 'inst' or all 'conv'; any
-        lambdaCorr >= 0 (the inter-source correlation penalty, :1484-1719).
+        them, :469-498); 'inst' and 'conv' spatial components in any
+        combination the reference's mixing update can run (free 'conv' ones
+        only when every component is free 'conv'); any lambdaCorr >= 0 (the
+        inter-source correlation penalty, :1484-1719).
         """
         if self.audioObject.channels != 2:
             raise AttributeError("Nb channels " + str(self.audioObject.channels) +
@@ -203,20 +205,24 @@ class FASST(object):
                 raise NotImplementedError("TW_constr=%s is outside the HIP path" % fac['TW_constr'])
         if sorted(owner.keys()) != list(range(J)):
             raise NotImplementedError("every spatial component needs a spectral component")
-        types = set(sc['mix_type'] for sc in self.spat_comps.values())
-        if len(types) != 1:
-            raise NotImplementedError("mixed inst/conv spatial components are outside the HIP path")
-        conv = types.pop() == 'conv'
-        if conv:
-            frees = set(sc['frdm_prior'] == 'free' for sc in self.spat_comps.values())
-            if len(frees) != 1:
-                raise NotImplementedError("mixed free/fixed convolutive components")
+        conv = [self.spat_comps[j]['mix_type'] == 'conv' for j in range(J)]
+        free = [self.spat_comps[j]['frdm_prior'] == 'free' for j in range(J)]
+        # update_mix_matrix (:843-863) solves the free 'conv' components with
+        # the FULL hat_Rss[f] against the right-hand side of those components
+        # only, which the reference can evaluate only when no other (fixed or
+        # 'inst') component exists: any other component makes np.linalg.solve
+        # raise at the first M-step.  Raise the same exception type up front.
+        if any(c and f for c, f in zip(conv, free)) and not all(c and f for c, f in zip(conv, free)):
+            raise ValueError("update_mix_matrix: free 'conv' spatial components next to fixed or "
+                             "'inst' ones (audioModel.py:856-857 solves hat_Rss[f].T of all %d "
+                             "components against the free components' right-hand side only)"
+                             % J)
         ranks, Ks = [], []
         for j in range(J):
             p = self.spat_comps[j]['params']
-            ranks.append(p.shape[0] if conv else p.shape[1])
+            ranks.append(p.shape[0] if conv[j] else p.shape[1])
             Ks.append(int(sum(self.spec_comps[k]['factor'][0]['FB'].shape[1] for k in owner[j])))
-        return [owner[j] for j in range(J)], ranks, Ks, conv
+        return [owner[j] for j in range(J)], ranks, Ks, (all(conv) if len(set(conv)) == 1 else conv)
 
     def _upload(self):
         order, ranks, Ks, conv = self._structure()

@@ -35,6 +35,7 @@ struct fasst_ctx {
   bool have_X = false;
   // model
   int J = 0, R = 0, KP = 0, conv = 0, configured = 0;
+  unsigned convm = 0;  // bit j: source j is 'conv' (conv == every source 'conv')
   int rank[fasst::kMaxJ] = {0}, roff[fasst::kMaxJ + 1] = {0}, K[fasst::kMaxJ] = {0};
   int spat_free[fasst::kMaxJ] = {0}, fb_free[fasst::kMaxJ] = {0}, tw_free[fasst::kMaxJ] = {0};
   int fw_free[fasst::kMaxJ] = {0};
@@ -95,7 +96,7 @@ struct fasst_ctx {
 };
 
 namespace fasst {
-int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv);
+int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const int *convj);
 int build_inst_A(fasst_ctx *c);
 int launch_w_old(fasst_ctx *c);  // Wkf = FB.FW
 }  // namespace fasst

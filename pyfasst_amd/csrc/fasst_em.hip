@@ -126,15 +126,17 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
   }
 }
 
-// 'inst' mixing replicated over bins: A[r][c][f] = params[c][r]
+// 'inst' mixing replicated over bins: A[r][c][f] = params[c][r], for the
+// rows of rowm ('inst' sources; a mixed model's 'conv' rows hold their own
+// per-bin filters)
 __global__ void k_inst_A(const double2 *__restrict__ Pinst, double2 *__restrict__ A, int R,
-                         int F, int Fp, const int *halt) {
+                         int F, int Fp, unsigned rowm, const int *halt) {
   HALT_GUARD(halt);
   const int n = R * 2 * Fp;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
     const int f = idx % Fp;
     const int rc = idx / Fp;
-    A[idx] = f < F ? Pinst[rc] : make_double2(0.0, 0.0);
+    if (rowm >> (rc >> 1) & 1u) A[idx] = f < F ? Pinst[rc] : make_double2(0.0, 0.0);
   }
 }
 
@@ -1989,7 +1991,8 @@ struct RArgs {
   double *pe;     // [J][nchunk] partial mixing-filter energy (conv)
   double *tpart;  // [nslot][nchunk] partial sums of the rescaled TW, per block
   int *flags;
-  int F, T, Fp, Tp, KP, conv, nchunk, tpc, fpc, nslot;
+  int F, T, Fp, Tp, KP, nchunk, tpc, fpc, nslot;
+  unsigned convm;    // bit j: spatial component j is 'conv' (per-bin filters in A)
   int K[kMaxJ], roff[kMaxJ + 1];
   // spectral components of source j (column blocks of FB / FW / TW) and the
   // slot of block 0
@@ -2032,7 +2035,7 @@ __global__ __launch_bounds__(256) void k_renorm_stats(const RArgs a) {
     a.pmax[((size_t)j * a.nchunk + c) * KP + threadIdx.x] = x;
   }
   __syncthreads();
-  if (a.conv) {
+  if (a.convm >> j & 1u) {
     const int r0 = a.roff[j], nr = a.roff[j + 1] - r0, w = fe - fb;
     double e = 0.0;
     for (int idx = threadIdx.x; idx < nr * 2 * w; idx += blockDim.x) {
@@ -2063,9 +2066,10 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   // the cross-chunk statistics are loaded by all threads at once and folded
   // in LDS (a per-thread loop over the chunks was a chain of dependent
   // global-latency round trips), in the same order as before
-  const int ne = a.conv ? a.nchunk : nr * 2;
+  const bool cj = a.convm >> j & 1u;
+  const int ne = cj ? a.nchunk : nr * 2;
   for (int q = threadIdx.x; q < ne; q += blockDim.x) {
-    if (a.conv) {
+    if (cj) {
       s_red[q] = a.pe[(size_t)j * a.nchunk + q];
     } else {
       const double2 x = a.Pinst[2 * r0 + q];
@@ -2078,7 +2082,7 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   if (threadIdx.x == 0) {
     double e = 0.0;
     for (int q = 0; q < ne; ++q) e += s_red[q];
-    s_e = e / (double)(a.conv ? nr * 2 * a.F : nr * 2);
+    s_e = e / (double)(cj ? nr * 2 * a.F : nr * 2);
   }
   __syncthreads();
   const double e = s_e;
@@ -2126,7 +2130,7 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
     }
   }
   const double se = sqrt(e);
-  if (a.conv) {
+  if (cj) {
     const int w = fe - fb;
     for (int idx = threadIdx.x; idx < nr * 2 * w; idx += blockDim.x) {
       const int f = fb + idx % w, rc = idx / w;
@@ -2184,7 +2188,7 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
       FW[r * KP + cc] = (FW[r * KP + cc] * sc[2 + r]) / sc[2 + KP + cc];
     }
     const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
-    if (!a.conv && threadIdx.x < nr * 2) {
+    if (!(a.convm >> j & 1u) && threadIdx.x < nr * 2) {
       const double se = sqrt(sc[0]);
       double2 *p = a.Pinst + 2 * r0 + threadIdx.x;
       *p = make_double2(p->x / se, p->y / se);
@@ -2468,7 +2472,7 @@ static int best_split(long unit, long cap, int max_split) {
   return 1;
 }
 
-int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv) {
+int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const int *convj) {
   if (J < 1 || J > kMaxJ) {
     set_error("J=%d outside the HIP path (1..%d sources)", J, kMaxJ);
     return FASST_ERR_UNSUPPORTED;
@@ -2489,6 +2493,12 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
   }
   c->J = J;
   c->R = R;
+  c->convm = 0;
+  for (int j = 0; j < J; ++j)
+    if (convj[j]) c->convm |= 1u << j;
+  // conv: every source 'conv' (per-bin mixing update); otherwise the 'inst'
+  // update runs over the free 'inst' sources with the rest held fixed
+  const int conv = c->convm == (1u << J) - 1u ? 1 : 0;
   c->conv = conv;
   c->KP = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : 64);
   c->roff[0] = 0;
@@ -2607,9 +2617,13 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, int conv
 
 int build_inst_A(fasst_ctx *c) {
   if (c->conv) return FASST_OK;
+  unsigned rowm = 0;
+  for (int j = 0; j < c->J; ++j)
+    if (!(c->convm >> j & 1u))
+      for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) rowm |= 1u << r;
   prof_begin(c, KINSTA);
   k_inst_A<<<launch_grid((size_t)c->R * 2 * c->Fp), 256, 0, c->stream>>>(c->Pinst.p, c->A.p, c->R,
-                                                                        c->F, c->Fp, c->halt);
+                                                                        c->F, c->Fp, rowm, c->halt);
   prof_end(c, KINSTA);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
@@ -2698,7 +2712,7 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   r.Fp = c->Fp;
   r.Tp = c->Tp;
   r.KP = c->KP;
-  r.conv = c->conv;
+  r.convm = c->convm;
   r.nchunk = c->nchunk_r;
   r.tpc = (c->T + c->nchunk_r - 1) / c->nchunk_r;
   r.fpc = (c->F + c->nchunk_r - 1) / c->nchunk_r;
@@ -3538,10 +3552,20 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   return FASST_OK;
 }
 
-int fasst_configure(fasst_ctx *c, int J, const int *rank, const int *K, int mix_conv) {
-  if (!c || !rank || !K) return FASST_ERR_SHAPE;
+int fasst_configure_types(fasst_ctx *c, int J, const int *rank, const int *K,
+                          const int *mix_conv) {
+  if (!c || !rank || !K || !mix_conv) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   return configure_model(c, J, rank, K, mix_conv);
+}
+
+int fasst_configure(fasst_ctx *c, int J, const int *rank, const int *K, int mix_conv) {
+  if (!c || !rank || !K) return FASST_ERR_SHAPE;
+  if (J < 1 || J > kMaxJ) return configure_model(c, J, rank, K, nullptr);
+  int types[kMaxJ];
+  for (int j = 0; j < J; ++j) types[j] = mix_conv ? 1 : 0;
+  DeviceGuard g(c->device);
+  return configure_model(c, J, rank, K, types);
 }
 
 int fasst_destroy(fasst_ctx *c) {
@@ -3613,7 +3637,7 @@ int fasst_set_spatial(fasst_ctx *c, int j, const double *params, int free_) {
   c->spat_free[j] = free_ ? 1 : 0;
   const int r0 = c->roff[j], nr = c->rank[j];
   const double2 *p = reinterpret_cast<const double2 *>(params);
-  if (c->conv) {
+  if (c->convm >> j & 1u) {
     // params [r][C][F] -> A[r][c][f] (row pitch Fp)
     FASST_HIP(hipMemcpy2DAsync(c->A.p + (size_t)2 * r0 * c->Fp, c->Fp * sizeof(double2), p,
                                c->F * sizeof(double2), c->F * sizeof(double2), (size_t)nr * 2,
@@ -3637,7 +3661,7 @@ int fasst_get_spatial(fasst_ctx *c, int j, double *params) {
   DeviceGuard g(c->device);
   const int r0 = c->roff[j], nr = c->rank[j];
   double2 *p = reinterpret_cast<double2 *>(params);
-  if (c->conv) {
+  if (c->convm >> j & 1u) {
     FASST_HIP(hipMemcpy2DAsync(p, c->F * sizeof(double2), c->A.p + (size_t)2 * r0 * c->Fp,
                                c->Fp * sizeof(double2), c->F * sizeof(double2), (size_t)nr * 2,
                                hipMemcpyDeviceToHost, c->stream));

@@ -35,13 +35,18 @@ class Engine(object):
             pass
 
     def configure(self, ranks, Ks, conv):
-        key = (tuple(int(r) for r in ranks), tuple(int(k) for k in Ks), bool(conv))
+        """conv: True / False for every source, or one flag per source (a
+        model with both 'inst' and 'conv' spatial components)."""
+        per = np.broadcast_to(np.asarray(conv, dtype=bool), (len(ranks),))
+        key = (tuple(int(r) for r in ranks), tuple(int(k) for k in Ks),
+               tuple(bool(c) for c in per))
         if key == self.structure:
             return
         r = np.ascontiguousarray(ranks, dtype=np.int32)
         k = np.ascontiguousarray(Ks, dtype=np.int32)
-        check(lib.fasst_configure(self._h, len(r), iptr(r), iptr(k), int(bool(conv))),
-              "fasst_configure")
+        c = np.ascontiguousarray(per, dtype=np.int32)
+        check(lib.fasst_configure_types(self._h, len(r), iptr(r), iptr(k), iptr(c)),
+              "fasst_configure_types")
         self.structure = key
 
     # ------------------------------------------------------------ observation

@@ -67,6 +67,11 @@ CASES = {
     "em_tb": dict(cls="MultiChanNMFConv", nbComps=3, nbNMFComps=8, spatial_rank=2,
                   conv=True, n=5000, fs=8000, kw=dict(iter_num=4, wlen=256, hopsize=64),
                   setup='tb'),
+    # 'inst' (free, fixed) and 'conv' (fixed) spatial components in one model
+    # (tests/helpers.py apply_setup 'mixed')
+    "em_mixed": dict(cls="MultiChanNMFInst_FASST", nbComps=3, nbNMFComps=6, spatial_rank=1,
+                     conv=False, n=5000, fs=8000, kw=dict(iter_num=5, wlen=256, hopsize=64),
+                     setup='mixed'),
 }
 
 

@@ -31,6 +31,10 @@ CASES = {
     # time blobs H = TW.TB (audioModel.py:1665-1691, 1931-1978, 2029-2033): TB
     # free with TW free, TB free with TW fixed, TB fixed
     "em_tb": (3, 8, 2, True, dict(iter_num=4, wlen=256, hopsize=64, _setup='tb')),
+    # 'inst' and 'conv' spatial components in one model (retrieve_subsrc_params
+    # :546-576, update_mix_matrix :807-841 with the others held fixed): a free
+    # and a fixed 'inst' component and a fixed 'conv' one
+    "em_mixed": (3, 6, 1, False, dict(iter_num=5, wlen=256, hopsize=64, _setup='mixed')),
 }
 
 # time blobs of the 'tb' setup: spectral component key -> (L, TB prior, TW prior)
@@ -85,6 +89,22 @@ def apply_setup(m, name):
             TW *= fac['TW'].mean() / np.dot(TW, TB).mean()
             fac['TW'], fac['TB'] = TW, TB
             fac['TB_frdm_prior'], fac['TW_frdm_prior'] = tb_prior, tw_prior
+    elif name == 'mixed':
+        # component 1 'inst' fixed; component 2 'conv' fixed, its filters the
+        # 'inst' gains with a per-channel delay (a genuinely per-bin mixing)
+        F = m.nbFreqsSigRepr
+        m.spat_comps[1]['frdm_prior'] = 'fixed'
+        sc = m.spat_comps[2]
+        inst = np.asarray(sc['params'])          # C x r
+        r = inst.shape[1]
+        delay = np.array([0.0, 1.5])
+        ph = np.exp(-1j * np.pi * np.outer(delay, np.arange(F)) / (F - 1))   # C x F
+        p = np.zeros((r, 2, F), dtype=complex)
+        for c in range(2):
+            p[:, c, :] = np.outer(inst[c], ph[c])
+        sc['params'] = p
+        sc['mix_type'] = 'conv'
+        sc['frdm_prior'] = 'fixed'
     else:
         raise ValueError(name)
 

@@ -132,7 +132,9 @@ def test_em_end_to_end_vs_reference(case, tmp_path):
     assert rel(ll, g['logliks']) < TIGHT
     tight = TIGHT_CASE.get(case, TIGHT)
     for j in range(J):
-        assert np.iscomplexobj(m.spat_comps[j]['params'])
+        # (the reference leaves a fixed 'inst' component's real params real)
+        assert np.iscomplexobj(m.spat_comps[j]['params']) == \
+            np.iscomplexobj(g['final_params_%d' % j])
         assert rel(m.spat_comps[j]['params'], g['final_params_%d' % j]) < tight
     for j in spec_keys(g, J):
         assert rel(m.spec_comps[j]['factor'][0]['FB'], g['final_FB_%d' % j]) < tight
@@ -578,6 +580,23 @@ def test_unsupported_structures_fail_loudly():
     m.spec_comps[0]['factor'][0]['TW_constr'] = 'HMM'
     with pytest.raises(NotImplementedError):
         m.estim_param_a_post_model()
+
+
+def test_mixed_types_free_conv_raises_as_reference(tmp_path):
+    """A free 'conv' component next to any other component: the reference's
+    conv solve (audioModel.py:856-857) passes the full hat_Rss[f].T against
+    the free components' right-hand side and np.linalg.solve raises
+    ValueError at the first M-step (the oracle restates it); the product
+    raises the same exception type before running."""
+    g = load("em_mixed")
+    m = _product_model("em_mixed", g, tmp_path)
+    m.spat_comps[2]['frdm_prior'] = 'free'
+    with pytest.raises(ValueError):
+        m.estim_param_a_post_model()
+    o, _ = oracle_model_from_golden(g, "em_mixed")
+    o.spat_comps[2]['frdm_prior'] = 'free'
+    with pytest.raises(ValueError):
+        o.estim_param_a_post_model()
 
 
 def test_full_size_config3_invariants():
