@@ -191,7 +191,9 @@ def main():
     # RCCL ("nccl") is the product; FASST_BENCH_BACKEND=gloo rehearses the
     # multi-rank path with more ranks than GPUs (ranks share cards round-robin)
     backend = os.environ.get("FASST_BENCH_BACKEND", "nccl")
-    if world > 1:
+    # FASST_BENCH_DIST=1 initialises the process group even for one rank (the
+    # RCCL barrier / max-over-ranks path exercised on a one-GPU box)
+    if world > 1 or os.environ.get("FASST_BENCH_DIST") == "1":
         import torch
         import torch.distributed as dist
         if backend != "nccl":

@@ -24,7 +24,8 @@ namespace fasst {
 constexpr double kEps = 1e-10;  // audioModel.py:61, tools/signalTools.py:11
 constexpr int kMaxJ = 8;        // sources (spatial components)
 constexpr int kMaxR = 16;       // total spatial rank
-constexpr int kMaxKP = 64;      // padded NMF components
+constexpr int kMaxKP = 128;     // padded NMF components (K > 64: one spectral
+                                // component per source, fixed FW, no lambdaCorr / TB)
 constexpr int kFwFpc = 64;      // bins per block of the FW update's f-contraction
 constexpr int kTile = 16;       // MFMA f64 16x16x4 tile edge
 // several spectral components per spatial component: source j's NMF columns

@@ -78,19 +78,22 @@ __global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB
   HALT_GUARD(halt);
   extern __shared__ __attribute__((aligned(16))) double s_m[];
   double *s_fb = s_m;             // [16][KP + 1]
-  double *s_fw = s_m + 16 * (KP + 1);  // [KP][KP]
+  double *s_fw = s_m + 16 * (KP + 1);  // [KP][KP] (KP <= 64; else FW is read from L2)
+  const bool fwg = KP > 64;
   const int j = blockIdx.y, f0 = blockIdx.x * 16;
+  const double *fw = fwg ? FW + (size_t)j * KP * KP : s_fw;
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int fl = idx / KP, q = idx % KP;
     s_fb[fl * (KP + 1) + q] = FB[((size_t)j * Fp + f0 + fl) * KP + q];
   }
-  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
-    s_fw[idx] = FW[(size_t)j * KP * KP + idx];
+  if (!fwg)
+    for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
+      s_fw[idx] = FW[(size_t)j * KP * KP + idx];
   __syncthreads();
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int k = idx / 16, fl = idx % 16;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += s_fb[fl * (KP + 1) + q] * s_fw[q * KP + k];
+    for (int q = 0; q < KP; ++q) s += s_fb[fl * (KP + 1) + q] * fw[q * KP + k];
     Wkf[((size_t)j * KP + k) * Fp + f0 + fl] = s;
     if (Wfk) Wfk[((size_t)j * Fp + f0 + fl) * KP + k] = s;
   }
@@ -104,14 +107,17 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
                                                int J, int Tp, int KP, const int *halt) {
   HALT_GUARD(halt);
   extern __shared__ __attribute__((aligned(16))) double s_f[];
-  double *s_fw = s_f;             // [KP][KP]
-  double *s_tw = s_f + KP * KP;   // [KP][64]
+  const bool fwg = KP > 64;       // FW read from L2 (its [KP][KP] copy would not fit)
+  double *s_fw = s_f;             // [KP][KP] (KP <= 64)
+  double *s_tw = s_f + (fwg ? 0 : KP * KP);   // [KP][64]
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
   const int tn = min(64, Tp - t0);
-  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
-    const int k = idx / KP, q = idx % KP;  // stored transposed: s_fw[q][k]
-    s_fw[q * KP + k] = FW[(size_t)j * KP * KP + idx];
-  }
+  if (!fwg)
+    for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
+      const int k = idx / KP, q = idx % KP;  // stored transposed: s_fw[q][k]
+      s_fw[q * KP + k] = FW[(size_t)j * KP * KP + idx];
+    }
+  const double *fwj = FW + (size_t)j * KP * KP;
   for (int idx = threadIdx.x; idx < KP * 64; idx += blockDim.x) {
     const int q = idx >> 6, tl = idx & 63;
     s_tw[idx] = tl < tn ? TW[((size_t)j * KP + q) * Tp + t0 + tl] : 0.0;
@@ -120,7 +126,10 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
   for (int idx = threadIdx.x; idx < tn * KP; idx += blockDim.x) {
     const int tl = idx / KP, k = idx % KP;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += s_fw[q * KP + k] * s_tw[q * 64 + tl];
+    if (fwg)
+      for (int q = 0; q < KP; ++q) s += fwj[k * KP + q] * s_tw[q * 64 + tl];
+    else
+      for (int q = 0; q < KP; ++q) s += s_fw[q * KP + k] * s_tw[q * 64 + tl];
     FWHt[((size_t)j * Tp + t0 + tl) * KP + k] = s;
     if (TWt) TWt[((size_t)j * Tp + t0 + tl) * KP + k] = s_tw[k * 64 + tl];  // H^T (FW update)
   }
@@ -541,6 +550,9 @@ __device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsign
 #ifndef ESTEP_SADDR
 #define ESTEP_SADDR 1
 #endif
+#ifndef ESTEP_TRIM
+#define ESTEP_TRIM 0
+#endif
 template <int J, int NKS, int RKU>
 __global__ __launch_bounds__(256, J > 4 ? 1 : 2)
 __attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) FASST_NO_LDS_PAIRING
@@ -613,7 +625,13 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
     for (int h = 0; h < NPG; ++h) pacc[g][h] = 0.0;
   }
+#if ESTEP_TRIM
+  // exponent sum in an integer, negative-det flag as the OR of the sign words
+  double ll = 0.0, lm = 1.0;
+  int ilev = 0, sgn = 0;
+#else
   double ll = 0.0, lm = 1.0, lev = 0.0, xmin = 1.0;
+#endif
 
   const int tb = a.tbase + blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
@@ -716,9 +734,15 @@ void k_estep_mx(const EArgs a) {
         // log() would; a negative det, which the guard only lets through for
         // a Sigma_x that is not positive semi-definite, is flagged in xmin)
         const double x = det * M_PI;
+#if ESTEP_TRIM
+        ilev += __builtin_amdgcn_frexp_exp(x);
+        lm *= __builtin_amdgcn_frexp_mant(x);
+        sgn |= (int)(__double_as_longlong(x) >> 32);
+#else
         lev += (double)__builtin_amdgcn_frexp_exp(x);
         lm *= __builtin_amdgcn_frexp_mant(x);
         xmin = fmin(xmin, x);
+#endif
         ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
       }
 #endif
@@ -731,6 +755,10 @@ void k_estep_mx(const EArgs a) {
       const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
       const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
       const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
+#if ESTEP_TRIM
+      constexpr double sr = RKU == 2 ? 0.5 : 1.0;
+      const double m00 = n00 * sr, m11 = n11 * sr, m01r = n01r * (2.0 * sr), m01i = n01i * (2.0 * sr);
+#endif
       // this point's MFMA operands -> the wave's slab (reader layout)
 #pragma unroll
       for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
@@ -766,9 +794,20 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const double Vj = V[j];
+#if ESTEP_TRIM
+        // (the factors 2 and 1 / rank folded into the N components once per
+        // point: exact scalings by powers of two for ranks 1 and 2)
+        const double q = RKU == 1 || RKU == 2
+                              ? (cj[(j * 4 + 0) * 16] * m00 + cj[(j * 4 + 1) * 16] * m11) +
+                                    (cj[(j * 4 + 2) * 16] * m01r + cj[(j * 4 + 3) * 16] * m01i)
+                              : ((cj[(j * 4 + 0) * 16] * n00 + cj[(j * 4 + 1) * 16] * n11) +
+                                 2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i)) *
+                                    inv_rk[j];
+#else
         const double qa = (cj[(j * 4 + 0) * 16] * n00 + cj[(j * 4 + 1) * 16] * n11) +
                           2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i);
         const double q = RKU == 1 ? qa : qa * inv_rk[j];
+#endif
         double val;
         if (!ESTEP_NO_STOREHAT && a.store_hat)
           val = fabs((Vj * Vj) * q + Vj);
@@ -814,10 +853,18 @@ void k_estep_mx(const EArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
+#if ESTEP_TRIM
+    ilev += __builtin_amdgcn_frexp_exp(lm);
+#else
     lev += (double)__builtin_amdgcn_frexp_exp(lm);
+#endif
     lm = __builtin_amdgcn_frexp_mant(lm);
   }
+#if ESTEP_TRIM
+  ll += (log(lm) + (double)ilev * M_LN2) + (sgn < 0 ? NAN : 0.0);
+#else
   ll += (log(lm) + lev * M_LN2) + (xmin < 0.0 ? NAN : 0.0);
+#endif
 
   // epilogue: lane (X = m, b, Y = n) holds, per bin group g, the 4x4 blocks
   // D[m][n] of bin f0 + 4g + b: cross (j = m, c = 4h + n), pairs (p = 4h + m, c = n)
@@ -1346,16 +1393,19 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   extern __shared__ __attribute__((aligned(16))) double s_fw[];
   const int f0 = blockIdx.x * 16, j = blockIdx.y;
   const int KP = a.KP;
-  double *s_fb = s_fw + KP * KP;
+  const bool fwg = KP > 64;   // FW read from L2 (its [KP][KP] copy would not fit)
+  const double *fw = fwg ? a.FW + (size_t)j * KP * KP : s_fw;
+  double *s_fb = s_fw + (fwg ? 0 : KP * KP);
   double *s_den = s_fb + 16 * KP;
   double *s_wn = s_den + KP;
-  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
-    s_fw[idx] = a.FW[(size_t)j * KP * KP + idx];
+  if (!fwg)
+    for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
+      s_fw[idx] = a.FW[(size_t)j * KP * KP + idx];
   for (int k = threadIdx.x; k < KP; k += blockDim.x) s_den[k] = a.hsum[(size_t)j * KP + k];
   __syncthreads();
   double dk = 0.0;
   if (threadIdx.x < KP)
-    for (int q = 0; q < KP; ++q) dk += s_fw[threadIdx.x * KP + q] * s_den[q];
+    for (int q = 0; q < KP; ++q) dk += fw[threadIdx.x * KP + q] * s_den[q];
   __syncthreads();
   if (threadIdx.x < KP) s_den[threadIdx.x] = dk;
   __syncthreads();
@@ -1382,7 +1432,7 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int fl = idx / KP, k = idx % KP, f = f0 + fl;
     double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * s_fw[q * KP + k];
+    for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * fw[q * KP + k];
     a.Wfk_new[((size_t)j * a.Fp + f) * KP + k] = s;
     s_wn[fl * (KP + 1) + k] = s;
   }
@@ -2059,7 +2109,7 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   __shared__ double s_red[256];
   __shared__ double s_w[kMaxKP], s_w2[kMaxKP];
   __shared__ double s_e;
-  __shared__ double s_big[kMaxKP * kMaxKP];   // chunk maxima, then FW_j
+  __shared__ double s_big[64 * 64];   // chunk maxima, then FW_j (KP <= 64; else from L2)
   const int j = blockIdx.y, c = blockIdx.x;
   const int K = a.K[j], KP = a.KP;
   const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
@@ -2076,8 +2126,12 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
       s_red[q] = x.x * x.x + x.y * x.y;
     }
   }
-  for (int i = threadIdx.x; i < a.nchunk * KP; i += blockDim.x)
-    s_big[i] = a.pmax[(size_t)j * a.nchunk * KP + i];
+  const bool big = a.nchunk * KP > 64 * 64 || KP > 64;
+  const double *pmx = big ? a.pmax + (size_t)j * a.nchunk * KP : s_big;
+  const double *fwb = big ? a.FW + (size_t)j * KP * KP : s_big;
+  if (!big)
+    for (int i = threadIdx.x; i < a.nchunk * KP; i += blockDim.x)
+      s_big[i] = a.pmax[(size_t)j * a.nchunk * KP + i];
   __syncthreads();
   if (threadIdx.x == 0) {
     double e = 0.0;
@@ -2088,12 +2142,13 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   const double e = s_e;
   if (threadIdx.x < KP) {
     double m = -INFINITY;
-    for (int q = 0; q < a.nchunk; ++q) m = fmax(m, s_big[q * KP + threadIdx.x]);
+    for (int q = 0; q < a.nchunk; ++q) m = fmax(m, pmx[q * KP + threadIdx.x]);
     const double w = m * e;
     s_w[threadIdx.x] = w == 0.0 ? 1.0 : w;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < KP * KP; i += blockDim.x) s_big[i] = a.FW[(size_t)j * KP * KP + i];
+  if (!big)
+    for (int i = threadIdx.x; i < KP * KP; i += blockDim.x) s_big[i] = a.FW[(size_t)j * KP * KP + i];
   __syncthreads();
   if (threadIdx.x < K) {
     // FW.mean(axis=0) of the column's own spectral component (block)
@@ -2102,7 +2157,7 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
     while (b + 1 < a.nblk[j] && cc >= a.kb[j][b + 1]) ++b;
     const int r0b = a.kb[j][b], r1b = a.kb[j][b + 1];
     double s = 0.0;
-    for (int r = r0b; r < r1b; ++r) s += s_big[r * KP + cc] * s_w[r];
+    for (int r = r0b; r < r1b; ++r) s += fwb[r * KP + cc] * s_w[r];
     s /= (double)(r1b - r0b);
     s_w2[cc] = s == 0.0 ? 1.0 : s;
   }
@@ -2454,6 +2509,12 @@ static int launch_grid(size_t n, int block = 256) {
 
 static int estep_occupancy(const fasst_ctx *c);
 static int contract_occupancy(const fasst_ctx *c, bool fb);
+static int tpw_of(const fasst_ctx *c);
+// dynamic LDS of the kernels that stage FW ([KP][KP] when KP <= 64) next to
+// `rest` doubles
+static size_t fw_lds(const fasst_ctx *c, int rest) {
+  return (size_t)((c->KP > 64 ? 0 : c->KP * c->KP) + rest) * sizeof(double);
+}
 
 // Split count c in [1, max_split] for a launch of unit * c equal blocks on
 // `cap` resident slots: maximises the filled fraction of the last round
@@ -2500,7 +2561,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   // update runs over the free 'inst' sources with the rest held fixed
   const int conv = c->convm == (1u << J) - 1u ? 1 : 0;
   c->conv = conv;
-  c->KP = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : 64);
+  c->KP = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : (kmax <= 64 ? 64 : 128));
   c->roff[0] = 0;
   for (int j = 0; j < J; ++j) {
     c->rank[j] = rank[j];
@@ -2552,8 +2613,9 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   // (the bin split also multiplies k_tw_update's reduction: a fixed, small
   // split measured best at C3)
   c->nsplit_t = std::max(1, std::min(4, c->nft / 32));
-  if ((long)((c->ntt + kTPW - 1) / kTPW) * J * c->nsplit_t < cap_t)
-    c->nsplit_t = best_split((long)((c->ntt + kTPW - 1) / kTPW) * J, cap_t, c->nft / 16);
+  const int tpw = tpw_of(c);
+  if ((long)((c->ntt + tpw - 1) / tpw) * J * c->nsplit_t < cap_t)
+    c->nsplit_t = best_split((long)((c->ntt + tpw - 1) / tpw) * J, cap_t, c->nft / 16);
   if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
   c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
@@ -2597,7 +2659,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(pnum, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(pden, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(tnum, (size_t)c->nsplit_t * J * Tp * KP);
-  if ((st = c->tcnt.alloc((size_t)J * ((c->ntt + kTPW - 1) / kTPW)))) return st;
+  if ((st = c->tcnt.alloc((size_t)J * ((c->ntt + tpw_of(c) - 1) / tpw_of(c))))) return st;
   ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
@@ -2631,7 +2693,7 @@ int build_inst_A(fasst_ctx *c) {
 
 int launch_w_old(fasst_ctx *c) {
   prof_begin(c, KW);
-  k_w_from_fb<<<dim3(c->nft, c->J), 256, (size_t)(16 * (c->KP + 1) + c->KP * c->KP) * sizeof(double),
+  k_w_from_fb<<<dim3(c->nft, c->J), 256, fw_lds(c, 16 * (c->KP + 1)),
                 c->stream>>>(c->FB.p, c->FW.p, c->Wkf.p, nullptr, c->J, c->Fp, c->KP, c->halt);
   prof_end(c, KW);
   FASST_LAUNCH_CHECK();
@@ -2812,7 +2874,11 @@ static void estep_dispatch_j(const fasst_ctx *c, F &&f) {
   switch (c->KP) {
     case 16: estep_dispatch_r<J, 4>(c, f); break;
     case 32: estep_dispatch_r<J, 8>(c, f); break;
-    default: estep_dispatch_r<J, 16>(c, f); break;
+    case 64: estep_dispatch_r<J, 16>(c, f); break;
+    default:   // K up to 128: general ranks only, J <= 4 (gem_iteration refuses more)
+      if constexpr (J <= 4) f(ETag<J, 32, 0, 0>{});
+      else f(ETag<J, 16, 0, 0>{});
+      break;
   }
 }
 
@@ -2841,7 +2907,7 @@ static void launch_estep(fasst_ctx *c, const EArgs &e, int ny) {
       prof_end(c, KESTEP);
       return;
     }
-    if constexpr (T::J <= 4) {  // round-1 two-pass E-step (A/B measurements only)
+    if constexpr (T::J <= 4 && T::NKS <= 16) {  // round-1 two-pass E-step (A/B only)
       prof_begin(c, KESTEP1);
       k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
       prof_end(c, KESTEP1);
@@ -2868,7 +2934,7 @@ static int estep_occupancy(const fasst_ctx *c) {
       occ = std::max(1, n1);
       return;
     }
-    if constexpr (T::J <= 4) {
+    if constexpr (T::J <= 4 && T::NKS <= 16) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
               &n1, k_estep<T::J, T::NKS, T::RKU, 1, T::AB>, 256, estep_smem<T>(1)) != hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -2880,6 +2946,12 @@ static int estep_occupancy(const fasst_ctx *c) {
   return occ;
 }
 
+// frame tiles per wave of the TW contraction: KP = 128 keeps one (its
+// numerator / denominator tiles alone fill 128 VGPRs)
+template <int NKC>
+constexpr int tpw_for() { return NKC > 4 ? 1 : kTPW; }
+static int tpw_of(const fasst_ctx *c) { return c->KP > 64 ? 1 : kTPW; }
+
 template <int NKC>
 static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb, int nz = 0) {
   if (fb) {
@@ -2889,8 +2961,9 @@ static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool f
     prof_end(c, KFBC);
   } else {
     prof_begin(c, KTWC);
-    k_tw_contract<NKC, kTPW><<<dim3((c->ntt + kTPW - 1) / kTPW, c->J, c->nsplit_t), 64, 0,
-                               c->stream>>>(t);
+    constexpr int TPW = tpw_for<NKC>();
+    k_tw_contract<NKC, TPW><<<dim3((c->ntt + TPW - 1) / TPW, c->J, c->nsplit_t), 64, 0,
+                              c->stream>>>(t);
     prof_end(c, KTWC);
   }
 }
@@ -2907,9 +2980,13 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
       e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<2, kFPW>, 64, 0)
              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<2, kTPW>, 64, 0);
       break;
-    default:
+    case 4:
       e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<4, kFPW>, 64, 0)
              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<4, kTPW>, 64, 0);
+      break;
+    default:
+      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<8, kFPW>, 64, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<8, 1>, 64, 0);
       break;
   }
   return e == hipSuccess ? std::max(1, n) : 1;
@@ -3052,7 +3129,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     }
     FASST_LAUNCH_CHECK();
     k_fb_update<<<dim3(c->nft, J), 256,
-                  (size_t)(c->KP * c->KP + 16 * c->KP + c->KP + 16 * (c->KP + 1)) * sizeof(double),
+                  fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
                   c->stream>>>(u);
     FASST_LAUNCH_CHECK();
     bool any_fw = false;
@@ -3111,7 +3188,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
       }
       k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
       k_fw_final<<<J, 256, 0, c->stream>>>(w);
-      k_w_from_fb<<<dim3(c->nft, J), 256, (size_t)(16 * (c->KP + 1) + c->KP * c->KP) * sizeof(double),
+      k_w_from_fb<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
                     c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
                                  c->halt);
       FASST_LAUNCH_CHECK();
@@ -3186,6 +3263,17 @@ static int multi_spectral(fasst_ctx *c, double omega) {
 static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
                          int iter) {
   const int J = c->J;
+  if (c->KP > 64) {
+    // K > 64 per source: the single-component path (the constructors' models)
+    bool any_fw = false;
+    for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
+    if (c->multi || any_fw || J > 4) {
+      set_error("K > 64 NMF components on a spatial component is on the HIP path with at most "
+                "4 spatial components, one spectral component each, fixed FW, lambdaCorr = 0 "
+                "and no time blobs");
+      return FASST_ERR_UNSUPPORTED;
+    }
+  }
   // (FW.TW)^T and the TW row sums depend only on the previous iteration's
   // parameters: fork them onto the side stream (kept on the main stream
   // while per-kernel event timing is on)
@@ -3198,7 +3286,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   prof_begin(c, KFWH);
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-  k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, (size_t)(c->KP * c->KP + c->KP * 64) * sizeof(double),
+  k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, fw_lds(c, c->KP * 64),
             side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
                     c->halt);
   prof_end(c, KFWH);
@@ -3281,7 +3369,8 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
       switch (nkc) {
         case 1: launch_contract<1>(c, b, TArgs(), true, nb); break;
         case 2: launch_contract<2>(c, b, TArgs(), true, nb); break;
-        default: launch_contract<4>(c, b, TArgs(), true, nb); break;
+        case 4: launch_contract<4>(c, b, TArgs(), true, nb); break;
+        default: launch_contract<8>(c, b, TArgs(), true, nb); break;
       }
       FASST_LAUNCH_CHECK();
       ye += ne;
@@ -3421,13 +3510,14 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     switch (nkc) {
       case 1: launch_contract<1>(c, b, t, true); break;
       case 2: launch_contract<2>(c, b, t, true); break;
-      default: launch_contract<4>(c, b, t, true); break;
+      case 4: launch_contract<4>(c, b, t, true); break;
+      default: launch_contract<8>(c, b, t, true); break;
     }
     FASST_LAUNCH_CHECK();
   }
   prof_begin(c, KFBU);
   k_fb_update<<<dim3(c->nft, J), 256,
-                (size_t)(c->KP * c->KP + 16 * c->KP + c->KP + 16 * (c->KP + 1)) * sizeof(double),
+                fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
                 c->stream>>>(u);
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
@@ -3474,7 +3564,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     }
     k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
     k_fw_final<<<J, 256, 0, c->stream>>>(w);
-    k_w_from_fb<<<dim3(c->nft, J), 256, (size_t)(16 * (c->KP + 1) + c->KP * c->KP) * sizeof(double),
+    k_w_from_fb<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
                   c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
                                c->halt);
     prof_end(c, KFWU);
@@ -3483,7 +3573,8 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   switch (nkc) {
     case 1: launch_contract<1>(c, b, t, false); break;
     case 2: launch_contract<2>(c, b, t, false); break;
-    default: launch_contract<4>(c, b, t, false); break;
+    case 4: launch_contract<4>(c, b, t, false); break;
+    default: launch_contract<8>(c, b, t, false); break;
   }
   FASST_LAUNCH_CHECK();
   if (!c->tw_fused) {   // else applied by the contraction's last arrivers

@@ -93,7 +93,7 @@ __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
 template <int NT, int NKC>
 __device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT][NKC],
                                                double *__restrict__ pn, double *__restrict__ pd,
-                                               int r0, int R, int wv, int lane) {
+                                               int r0, int R, int wv, int lane, int k0 = 0) {
   constexpr int NE = NT * NKC * 4;
   __shared__ double red[2][NE][64];
   const int fl = lane & 15, tq = lane >> 4;
@@ -115,7 +115,7 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT]
               red[0][e][lane] = a;
               red[1][e][lane] = b;
             } else {
-              const int r = r0 + p * 16 + tq + 4 * m, k = kc * 16 + fl;
+              const int r = r0 + p * 16 + tq + 4 * m, k = k0 + kc * 16 + fl;
               if (r < R) {
                 pn[(size_t)k * R + r] = a;
                 pd[(size_t)k * R + r] = b;
@@ -130,12 +130,16 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT]
 // W update (nmf.py:39-44): numT[k][f] = sum_t H[k][t] X[f][t], denT with Y.
 // A workgroup owns FPW 16-bin tiles and 4 frame chunks (one per wave); the
 // W rows are loop-invariant B operands of the hat tiles.
-template <int NKC, int FPW>
-__global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
+// KS > 1: the contraction's K columns are split over blockIdx.z (each slice
+// recomputes the whole hat tile): fewer accumulators per wave, so two waves
+// per SIMD fit where one slice per wave needs the whole register file
+template <int NKC, int FPW, int KS = 1>
+__global__ __launch_bounds__(256, KS > 1 ? 2 : 1) void k_nmf_wnum(const double *__restrict__ W,
                                                   const double *__restrict__ H,
                                                   const double *__restrict__ SXt,
                                                   double *__restrict__ part, int F, int N, int tpc) {
-  constexpr int NKS = 4 * NKC, K = 16 * NKC;
+  constexpr int NKS = 4 * NKC, K = 16 * NKC, NKL = NKC / KS;
+  const int kc0 = blockIdx.z * NKL;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
   const int ft0 = blockIdx.x * FPW, nft = (F + 15) / 16, ntt = (N + 15) / 16;
   double wk[FPW][NKS];
@@ -145,15 +149,15 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
 #pragma unroll
     for (int s = 0; s < NKS; ++s) wk[p][s] = f < F ? W[(size_t)f * K + 4 * s + tq] : 0.0;
   }
-  d4 num[FPW][NKC], den[FPW][NKC];
+  d4 num[FPW][NKL], den[FPW][NKL];
 #pragma unroll
   for (int p = 0; p < FPW; ++p)
 #pragma unroll
-    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int kc = 0; kc < NKL; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int tb = (blockIdx.y * 4 + wv) * tpc, te = min(tb + tpc, ntt);
   // the next frame tile's H operands and SX values are loaded while this
   // tile's MFMAs run (the loop was L2-latency bound)
-  double th[2][NKS], hb[2][4][NKC], sxv[2][FPW][4];
+  double th[2][NKS], hb[2][4][NKL], sxv[2][FPW][4];
   auto load = [&](int tt, int slot) {
     const int t0 = tt * 16;
 #pragma unroll
@@ -163,8 +167,8 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
     for (int i = 0; i < 4; ++i) {
       const int t = t0 + tq + 4 * i;
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc)
-        hb[slot][i][kc] = t < N ? H[(size_t)(kc * 16 + fl) * N + t] : 0.0;
+      for (int kc = 0; kc < NKL; ++kc)
+        hb[slot][i][kc] = t < N ? H[(size_t)((kc0 + kc) * 16 + fl) * N + t] : 0.0;
 #pragma unroll
       for (int p = 0; p < FPW; ++p) {
         const int f = (ft0 + p) * 16 + fl;
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int kc = 0; kc < NKC; ++kc) {
+        for (int kc = 0; kc < NKL; ++kc) {
           num[p][kc] = nmfma(x[i], hb[cs][i][kc], num[p][kc]);
           den[p][kc] = nmfma(y[i], hb[cs][i][kc], den[p][kc]);
         }
@@ -224,20 +228,21 @@ __global__ __launch_bounds__(256) void k_nmf_wnum(const double *__restrict__ W,
   }
   const size_t slab = (size_t)K * F;
   double *pn = part + (size_t)blockIdx.y * 2 * slab;
-  nmf_fold_store<FPW, NKC>(num, den, pn, pn + slab, ft0 * 16, F, wv, lane);
+  nmf_fold_store<FPW, NKL>(num, den, pn, pn + slab, ft0 * 16, F, wv, lane, kc0 * 16);
 }
 
 // H update (nmf.py:53-59): num[k][t] = sum_f W[f][k] X[f][t], den with Y,
 // hat from the updated W and the rescaled H (hs = W column sums from the W
 // update, applied on load as k_nmf_hscale would; null when W is frozen).  A
 // workgroup owns TPW 16-frame tiles and 4 bin chunks (one per wave).
-template <int NKC, int TPW>
-__global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
+template <int NKC, int TPW, int KS = 1>
+__global__ __launch_bounds__(256, KS > 1 ? 2 : 1) void k_nmf_hnum(const double *__restrict__ W,
                                                   const double *__restrict__ H,
                                                   const double *__restrict__ hs,
                                                   const double *__restrict__ SX,
                                                   double *__restrict__ part, int F, int N, int fpc) {
-  constexpr int NKS = 4 * NKC, K = 16 * NKC;
+  constexpr int NKS = 4 * NKC, K = 16 * NKC, NKL = NKC / KS;
+  const int kc0 = blockIdx.z * NKL;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
   const int tt0 = blockIdx.x * TPW, nft = (F + 15) / 16, ntt = (N + 15) / 16;
   double bt[TPW][NKS];
@@ -250,15 +255,15 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
       bt[p][s] = hs ? h * hs[4 * s + tq] : h;
     }
   }
-  d4 num[TPW][NKC], den[TPW][NKC];
+  d4 num[TPW][NKL], den[TPW][NKL];
 #pragma unroll
   for (int p = 0; p < TPW; ++p)
 #pragma unroll
-    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int kc = 0; kc < NKL; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int fb = (blockIdx.y * 4 + wv) * fpc, fe = min(fb + fpc, nft);
   // the next bin tile's W operands and SX values are loaded while this
   // tile's MFMAs run
-  double ao[2][NKS], bw[2][4][NKC], sxv[2][TPW][4];
+  double ao[2][NKS], bw[2][4][NKL], sxv[2][TPW][4];
   auto load = [&](int ft, int slot) {
     const int f0 = ft * 16;
 #pragma unroll
@@ -268,7 +273,8 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
     for (int i = 0; i < 4; ++i) {
       const int f = f0 + 4 * i + tq;
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) bw[slot][i][kc] = f < F ? W[(size_t)f * K + kc * 16 + fl] : 0.0;
+      for (int kc = 0; kc < NKL; ++kc)
+        bw[slot][i][kc] = f < F ? W[(size_t)f * K + (kc0 + kc) * 16 + fl] : 0.0;
 #pragma unroll
       for (int p = 0; p < TPW; ++p) {
         const int t = (tt0 + p) * 16 + fl;
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int kc = 0; kc < NKC; ++kc) {
+        for (int kc = 0; kc < NKL; ++kc) {
           num[p][kc] = nmfma(x[i], bw[cs][i][kc], num[p][kc]);
           den[p][kc] = nmfma(y[i], bw[cs][i][kc], den[p][kc]);
         }
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(256) void k_nmf_hnum(const double *__restrict__ W,
   }
   const size_t slab = (size_t)K * N;
   double *pn = part + (size_t)blockIdx.y * 2 * slab;
-  nmf_fold_store<TPW, NKC>(num, den, pn, pn + slab, tt0 * 16, N, wv, lane);
+  nmf_fold_store<TPW, NKL>(num, den, pn, pn + slab, tt0 * 16, N, wv, lane, kc0 * 16);
 }
 
 // k_nmf_w over the fused path's group partials ([g][num / den][K][F])
@@ -546,7 +552,7 @@ struct nmf_ctx {
   int F = 0, N = 0, K = 0;
   DBuf<double> SX, W, H, hat, X, Y, numT, denT, num, den, s, work;
   // fused path (K % 16 == 0, K <= 64): transposed copies and chunk partials
-  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1, pw = 1;
+  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1, pw = 1, ks = 1;
   DBuf<double> SXt, part;
 };
 
@@ -567,20 +573,23 @@ int model_xy(nmf_ctx *c) {
 }
 
 constexpr int kNmfCUs = 256;
+#ifndef NMF_KS_DEFAULT
+#define NMF_KS_DEFAULT 1
+#endif
 
 // PW: 16-bin (W update) / 16-frame (H update) tiles per wave
-template <int NKC, int PW>
+template <int NKC, int PW, int KS = 1>
 static void nmf_fused_pw(nmf_ctx *c, int update_w, int update_h) {
   const int F = c->F, N = c->N, K = c->K;
   const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
   if (update_w) {
-    k_nmf_wnum<NKC, PW><<<dim3((nft + PW - 1) / PW, c->ng_w), 256, 0, c->stream>>>(
+    k_nmf_wnum<NKC, PW, KS><<<dim3((nft + PW - 1) / PW, c->ng_w, KS), 256, 0, c->stream>>>(
         c->W.p, c->H.p, c->SXt.p, c->part.p, F, N, c->tpc_w);
     k_nmf_w_part<<<K, 1024, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
   }
   const double *hs = update_w ? c->s.p : nullptr;
   if (update_h) {
-    k_nmf_hnum<NKC, PW><<<dim3((ntt + PW - 1) / PW, c->ng_h), 256, 0, c->stream>>>(
+    k_nmf_hnum<NKC, PW, KS><<<dim3((ntt + PW - 1) / PW, c->ng_h, KS), 256, 0, c->stream>>>(
         c->W.p, c->H.p, hs, c->SX.p, c->part.p, F, N, c->fpc_h);
     k_nmf_h_part<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->part.p, c->ng_h, hs, K,
                                                                 N);
@@ -591,6 +600,15 @@ static void nmf_fused_pw(nmf_ctx *c, int update_w, int update_h) {
 
 template <int NKC>
 static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
+  if constexpr (NKC >= 2) {
+    if (c->ks == 2) {
+      if (c->pw == 2)
+        nmf_fused_pw<NKC, 2, 2>(c, update_w, update_h);
+      else
+        nmf_fused_pw<NKC, 1, 2>(c, update_w, update_h);
+      return;
+    }
+  }
   if (c->pw == 2)
     nmf_fused_pw<NKC, 2>(c, update_w, update_h);
   else
@@ -677,7 +695,10 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
     // (C2, F=1025 T=2000 K=64: 2 tiles per wave, ~1024 waves measured best,
     // 0.103 ms per iteration; 1 tile: 0.106, 2048 waves: 0.124)
     c->pw = 2;
-    int waves = 4 * kNmfCUs;
+    c->ks = NMF_KS_DEFAULT;
+    if (const char *v = getenv("FASST_NMF_KS")) c->ks = atoi(v) == 2 ? 2 : 1;
+    if (K < 32) c->ks = 1;
+    int waves = 4 * kNmfCUs;   // per K slice
     if (const char *v = getenv("FASST_NMF_PW")) c->pw = atoi(v) == 2 ? 2 : 1;
     if (const char *v = getenv("FASST_NMF_WAVES")) waves = std::max(4, atoi(v));
     const int uw = (nft + c->pw - 1) / c->pw, uh = (ntt + c->pw - 1) / c->pw;

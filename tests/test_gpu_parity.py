@@ -213,6 +213,11 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (49, 60, 8, 4, 1, 2),        # 8 sources of rank 1
     (33, 40, 8, 16, 2, 2),       # 8 sources of rank 2: total rank 16 (the k_mix LU maximum)
     (57, 70, 5, 36, [3, 2, 3, 2, 3], 2),  # 5 sources, mixed ranks 13, K padded to 64
+    # K > 64 per source (padded to 128: the E-step's NKS = 32 instantiation,
+    # NKC = 8 contractions, FW read from L2 by its staging kernels)
+    (97, 150, 2, 100, 2, 3),     # K = 100
+    (65, 77, 4, 128, 1, 2),      # K = 128 on 4 sources
+    (129, 90, 3, 72, [1, 2, 1], 3),  # K = 72, mixed ranks
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
@@ -228,6 +233,18 @@ def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     S = m.separated_images()
     So = o.separated_images(X)
     assert rel(np.abs(S), np.abs(So)) < 1e-8
+
+
+def test_k_above_64_outside_single_component_path_fails_loudly():
+    """K > 64 runs the single-component path only (at most 4 spatial
+    components, fixed FW): other structures raise instead of running."""
+    m, o, X = _c3_like(33, 40, 5, 70, 1, 1)
+    with pytest.raises(NotImplementedError):
+        m.estim_param_a_post_model()
+    m, o, X = _c3_like(33, 40, 2, 70, 1, 1)
+    m.spec_comps[0]['factor'][0]['FW_frdm_prior'] = 'free'
+    with pytest.raises(NotImplementedError):
+        m.estim_param_a_post_model()
 
 
 def test_fixed_components_vs_oracle():
