@@ -20,6 +20,7 @@ import scipy.io.wavfile as wav
 from .. import _lib
 from . import separateLeadFunctions as slf
 from .tracking._tracking import viterbiTracking as viterbiTrackingArray
+from ..tools.nnls import nnls_columns
 
 eps = 10 ** -9      # SeparateLeadStereoTF.py:31
 
@@ -70,7 +71,8 @@ class SeparateLeadProcess(object):
     reference.  tfrepresentation 'stft' or the CQT-type 'cqt' / 'minqt' /
     'mqt' (GPU CQT / MinQT transforms and their inverses; the source
     dictionary of a CQT-type transform transforms the complex KLGLOTT88
-    comb on the GPU, dict_wf0_cqt), initHF00 'random' only.
+    comb on the GPU, dict_wf0_cqt); initHF00 'random' or 'nnls' (the per-frame
+    NNLS of each chunk as one batched GPU solve, tools/nnls.py).
 
     Addition: with inputAudioFilename=None the state that
     writeSeparatedSignals / runViterbi read can be given directly
@@ -111,9 +113,6 @@ class SeparateLeadProcess(object):
             raise AttributeError("The desired Time-Freq representation " + tfrepresentation +
                                  " is not a recognized one.\nPlease choose from " +
                                  str(knownTransfos))
-        if initHF00 != 'random':
-            raise NotImplementedError("initHF00=%r (per-frame NNLS) is outside the GPU path"
-                                      % initHF00)
         self.tfrepresentation = tfrepresentation
         self.stftParams['cqtfmin'] = cqtfmin
         self.stftParams['cqtfmax'] = cqtfmax
@@ -332,9 +331,16 @@ class SeparateLeadProcess(object):
             start = n * maxFrames
             stop = np.minimum((n + 1) * maxFrames, totFrames)
             SX = self.computeMonoX(start=start, stop=stop)
+            HF00 = None
+            if P['initHF00'] == 'nnls':
+                # per-frame NNLS of SX on the dictionary, + eps (:982-993), all
+                # frames of the chunk at once on the GPU (tools/nnls.py); the
+                # reference solves the first stop - start columns of SX
+                HF00 = nnls_columns(P['WF0'], SX[:, :stop - start], add_eps=eps,
+                                    device=self.device)
             HGAMMA, HPHI, HF0, HM, WM, recoError1 = SIMM.SIMM(
                 SX, WF0=P['WF0'], WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
-                numberOfAccompanimentSpectralShapes=R, HGAMMA0=None, HPHI0=None, HF00=None,
+                numberOfAccompanimentSpectralShapes=R, HGAMMA0=None, HPHI0=None, HF00=HF00,
                 WM0=None, HM0=None, numberOfIterations=P['niter'], updateRulePower=1.,
                 stepNotes=P['stepNotes'], lambdaHF0=0.0 / (1.0 * SX.max()), alphaHF0=0.9,
                 verbose=self.verbose, F0Table=P['F0Table'], chirpPerF0=P['chirpPerF0'],

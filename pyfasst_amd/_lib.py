@@ -119,6 +119,10 @@ SIGNATURES = {
                                      ctypes.c_double, ctypes.c_int, _dp, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_long, _dp]),
     "dict_last_ms": (ctypes.c_int, [_dp]),
+    # include/fasst_nnls.h
+    "nnls_columns": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int,
+                                    _dp, ctypes.c_double, ctypes.c_double, ctypes.c_int, _dp,
+                                    _ip]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -1271,6 +1271,9 @@ struct BArgs {
 // Without DEN and FPW even the tiles are interleaved (bin f in tile f mod
 // FPW), so each lane's rho values arrive as 16-byte loads (C3: 0.166 ->
 // 0.155 ms at FPW = 2, same-box A/B).
+#ifndef FB_REVERSE
+#define FB_REVERSE 0
+#endif
 template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
@@ -1286,7 +1289,11 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   for (int p = 0; p < (DEN ? FPW : 1); ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
-  const int tb = a.tbase + blockIdx.z * a.tpc, te = min(tb + a.tpc, a.ntt);
+  // FB_REVERSE: frame chunks taken last-first, so the chunks the E-step wrote
+  // last are read while they may still sit in the 256 MB infinity cache (the
+  // chunk's partial slot is its own index either way: same sums, same order)
+  const int zc = FB_REVERSE ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
+  const int tb = a.tbase + zc * a.tpc, te = min(tb + a.tpc, a.ntt);
   const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
   const double *rdj = DEN ? a.hatW2 + (size_t)j * a.Tp * a.Fp : nullptr;
   for (int tt = tb; tt < te; ++tt) {
@@ -1347,7 +1354,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       }
     }
   }
-  const size_t base = ((size_t)(a.zbase + blockIdx.z) * a.J + j) * a.Fp;
+  const size_t base = ((size_t)(a.zbase + zc) * a.J + j) * a.Fp;
   if constexpr (FPW % 2 == 0 && !DEN) {   // interleaved tiles: tile p holds bins p mod FPW
 #pragma unroll
     for (int p = 0; p < FPW; ++p)

@@ -1,0 +1,289 @@
+// Batched non-negative least squares on MI355X (gfx950), FP64: the
+// initHF00='nnls' initialisation of the lead pipeline's chunked mono SIMM.
+//
+// SeparateLeadStereoTF.py:982-993 (estimHF0) solves, for every frame n of a
+// chunk, HF00[:, n] = scipy.optimize.nnls(WF0, SX[:, n]) and adds eps
+// (:993).  scipy's nnls is Lawson & Hanson's active-set algorithm
+// ("Solving Least Squares Problems", 1974, ch. 23).  The minimiser is unique
+// when WF0 has full column rank, so an exact active-set method lands on it;
+// here the Lawson-Hanson iteration runs on the normal equations:
+//   G = WF0^T WF0 (once per dictionary) and C^T = SX^T WF0 (one product per
+//   chunk), both on k_dgemm2;
+//   one wave per frame: the passive set P kept in insertion order with the
+//   Cholesky factor L of G_PP (row-major in global scratch, plus its
+//   transpose so both triangular solves read contiguous rows); adding an
+//   index appends one row (a forward solve), removing indices recomputes the
+//   rows from the first removed position on (the leading rows are the
+//   Cholesky factor of the unchanged leading block).
+// Per outer step: j = argmax of the dual w = c - G x over the free indices
+// (first index on ties, as the reference's argmax); stop when w_j <= tol; the
+// candidate is skipped when it is numerically dependent on P or its trial
+// coefficient is not positive (Lawson-Hanson's acceptance test); inner loop:
+// z = G_PP^-1 c_P, while min z <= 0 step x towards z by the largest feasible
+// alpha and drop the indices that reach zero.  The lanes of the wave share
+// the work of every dot product / axpy; the wave's vectors sit in LDS.
+#include "fasst_common.h"
+#include "fasst_gemm.h"
+#include "../../include/fasst_nnls.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace fasst {
+
+constexpr int kNnlsMaxN = 2048;   // dictionary columns (LDS: 40 bytes each)
+
+struct NnlsArgs {
+  const double *G;    // [n][n]
+  const double *Ct;   // [nf][n]
+  double *X;          // [n][nf]
+  double *L, *Lt;     // [slots][n][n] scratch
+  int *info;          // [nf]: outer iterations, or -1 when maxiter was reached
+  int n, nf, maxiter;
+  double tol, add_eps;   // tol: relative to max |c| of the frame
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// forward solve L[0:p, 0:p] y = b (row-major L, pitch n), y in LDS
+__device__ void nnls_fwd(const double *L, int n, const double *b, double *y, int p, int lane) {
+  for (int k = 0; k < p; ++k) {
+    const double *row = L + (size_t)k * n;
+    double s = 0.0;
+    for (int i = lane; i < k; i += 64) s += row[i] * y[i];
+    s = wave_sum(s);
+    if (lane == 0) y[k] = (b[k] - s) / row[k];
+    __syncthreads();
+  }
+}
+
+// backward solve L[0:p, 0:p]^T z = y through Lt (row k of Lt = column k of L)
+__device__ void nnls_bwd(const double *Lt, int n, const double *y, double *z, int p, int lane) {
+  for (int k = p - 1; k >= 0; --k) {
+    const double *row = Lt + (size_t)k * n;
+    double s = 0.0;
+    for (int i = k + 1 + lane; i < p; i += 64) s += row[i] * z[i];
+    s = wave_sum(s);
+    if (lane == 0) z[k] = (y[k] - s) / row[k];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_nnls(const NnlsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int n = a.n, lane = threadIdx.x;
+  double *x = sm;              // [n] current solution (dense)
+  double *w = x + n;           // [n] dual
+  double *c = w + n;           // [n] right-hand side c = WF0^T sx
+  double *t = c + n;           // [n] work: c_P / y, then the trial z (list order)
+  int *lst = (int *)(t + n);   // [n] passive set, insertion order
+  int *st = lst + n;           // [n] 0 free, 1 passive, 2 skipped until P changes
+  __shared__ double s_y[kNnlsMaxN];   // forward-solve output
+  __shared__ int s_p, s_j;
+  double *L = a.L + (size_t)blockIdx.x * n * n, *Lt = a.Lt + (size_t)blockIdx.x * n * n;
+  for (int q = blockIdx.x; q < a.nf; q += gridDim.x) {
+    for (int i = lane; i < n; i += 64) {
+      c[i] = a.Ct[(size_t)q * n + i];
+      x[i] = 0.0;
+      w[i] = c[i];
+      st[i] = 0;
+    }
+    // stopping tolerance on the dual, relative to the right-hand side's scale
+    double cm = 0.0;
+    for (int i = lane; i < n; i += 64) cm = fmax(cm, fabs(a.Ct[(size_t)q * n + i]));
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) cm = fmax(cm, __shfl_xor(cm, m, 64));
+    const double tol = a.tol * cm;
+    if (lane == 0) s_p = 0;
+    __syncthreads();
+    int it = 0;
+    // appends index j as row p of L (forward solve of its G column); returns
+    // false when it is numerically dependent on the passive set
+    auto append_row = [&](int p, int j) -> bool {
+      for (int i = lane; i < p; i += 64) t[i] = a.G[(size_t)lst[i] * n + j];
+      __syncthreads();
+      nnls_fwd(L, n, t, s_y, p, lane);
+      double s = 0.0;
+      for (int i = lane; i < p; i += 64) s += s_y[i] * s_y[i];
+      s = wave_sum(s);
+      const double gjj = a.G[(size_t)j * n + j];
+      const double d2 = gjj - s;
+      if (!(d2 > 1e-14 * gjj)) return false;
+      const double d = sqrt(d2);
+      for (int i = lane; i < p; i += 64) {
+        L[(size_t)p * n + i] = s_y[i];
+        Lt[(size_t)i * n + p] = s_y[i];
+      }
+      if (lane == 0) {
+        L[(size_t)p * n + p] = d;
+        Lt[(size_t)p * n + p] = d;
+      }
+      __syncthreads();
+      return true;
+    };
+    // trial z = G_PP^-1 c_P into t[0:p]
+    auto solve_z = [&](int p) {
+      for (int i = lane; i < p; i += 64) t[i] = c[lst[i]];
+      __syncthreads();
+      nnls_fwd(L, n, t, s_y, p, lane);
+      nnls_bwd(Lt, n, s_y, t, p, lane);
+    };
+    while (true) {
+      // j = argmax of w over the free indices (first index on ties)
+      double bv = -INFINITY;
+      int bj = n;
+      for (int i = lane; i < n; i += 64)
+        if (st[i] == 0 && w[i] > bv) {
+          bv = w[i];
+          bj = i;
+        }
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        const double ov = __shfl_xor(bv, m, 64);
+        const int oj = __shfl_xor(bj, m, 64);
+        if (ov > bv || (ov == bv && oj < bj)) {
+          bv = ov;
+          bj = oj;
+        }
+      }
+      if (!(bv > tol) || bj >= n) break;
+      const int j = bj, p = s_p;
+      if (!append_row(p, j)) {
+        if (lane == 0) st[j] = 2;
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) {
+        lst[p] = j;
+        st[j] = 1;
+      }
+      __syncthreads();
+      solve_z(p + 1);
+      if (!(t[p] > 0.0)) {   // the candidate would not enter: skip it until P changes
+        if (lane == 0) st[j] = 2;
+        __syncthreads();
+        continue;
+      }
+      for (int i = lane; i < n; i += 64)
+        if (st[i] == 2) st[i] = 0;
+      if (lane == 0) s_p = p + 1;
+      __syncthreads();
+      // inner loop: step towards z while a coefficient is not positive
+      while (true) {
+        const int pp = s_p;
+        bool allpos = true;
+        double al = INFINITY;
+        for (int i = lane; i < pp; i += 64)
+          if (!(t[i] > 0.0)) {
+            allpos = false;
+            const double xi = x[lst[i]];
+            al = fmin(al, xi / (xi - t[i]));
+          }
+        allpos = __all(allpos);
+        if (allpos) break;
+        if (++it > a.maxiter) break;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) al = fmin(al, __shfl_xor(al, m, 64));
+        for (int i = lane; i < pp; i += 64) {
+          const int k = lst[i];
+          x[k] = x[k] + al * (t[i] - x[k]);
+        }
+        __syncthreads();
+        // drop the indices that reached zero; rows from the first drop on are
+        // recomputed for the compacted list
+        if (lane == 0) {
+          int np_ = 0, r1 = pp;
+          for (int i = 0; i < pp; ++i) {
+            const int k = lst[i];
+            if (x[k] > 0.0) {
+              lst[np_++] = k;
+            } else {
+              if (r1 == pp) r1 = np_;
+              x[k] = 0.0;
+              st[k] = 0;
+            }
+          }
+          s_p = np_;
+          s_j = r1;
+        }
+        __syncthreads();
+        const int np2 = s_p;
+        for (int r = s_j; r < np2; ++r) append_row(r, lst[r]);
+        solve_z(np2);
+      }
+      if (it > a.maxiter) break;
+      // x = z on P, 0 elsewhere; w = c - G x
+      const int pp = s_p;
+      for (int i = lane; i < pp; i += 64) x[lst[i]] = t[i];
+      __syncthreads();
+      for (int i = lane; i < n; i += 64) {
+        double s = c[i];
+        for (int k = 0; k < pp; ++k) s -= a.G[(size_t)lst[k] * n + i] * x[lst[k]];
+        w[i] = s;
+      }
+      __syncthreads();
+      ++it;
+      if (it > a.maxiter) break;
+    }
+    for (int i = lane; i < n; i += 64) a.X[(size_t)i * a.nf + q] = x[i] + a.add_eps;
+    if (lane == 0) a.info[q] = it > a.maxiter ? -1 : it;
+    __syncthreads();
+  }
+}
+
+}  // namespace fasst
+
+using namespace fasst;
+
+extern "C" {
+
+int nnls_columns(int device, int m, int n, const double *A, int nf, const double *B, double tol,
+                 double add_eps, int maxiter, double *X, int *info) {
+  if (m < 1 || n < 1 || n > kNnlsMaxN || nf < 1 || !A || !B || !X) {
+    set_error("nnls_columns: bad shape (m %d, n %d <= %d, frames %d)", m, n, kNnlsMaxN, nf);
+    return FASST_ERR_SHAPE;
+  }
+  DeviceGuard g(device);
+  int st;
+  hipStream_t s = nullptr;
+  const int slots = std::min(nf, 2048);
+  DBuf<double> dA, dB, dG, dCt, dX, dL, dLt;
+  DBuf<int> dinfo;
+  if ((st = dA.alloc((size_t)m * n)) || (st = dB.alloc((size_t)m * nf)) ||
+      (st = dG.alloc((size_t)n * n)) || (st = dCt.alloc((size_t)nf * n)) ||
+      (st = dX.alloc((size_t)n * nf)) || (st = dL.alloc((size_t)slots * n * n)) ||
+      (st = dLt.alloc((size_t)slots * n * n)) || (st = dinfo.alloc(nf)))
+    return st;
+  FASST_HIP(hipMemcpy(dA.p, A, (size_t)m * n * sizeof(double), hipMemcpyHostToDevice));
+  FASST_HIP(hipMemcpy(dB.p, B, (size_t)m * nf * sizeof(double), hipMemcpyHostToDevice));
+  // G = A^T A and C^T = B^T A (k_dgemm2: C[i][j] = sum_k A[k][i] B[k][j])
+  if ((st = dgemm2(s, n, n, m, dA.p, n, dA.p, n, dG.p, n))) return st;
+  if ((st = dgemm2(s, nf, n, m, dB.p, nf, dA.p, n, dCt.p, n))) return st;
+  NnlsArgs a;
+  a.G = dG.p;
+  a.Ct = dCt.p;
+  a.X = dX.p;
+  a.L = dL.p;
+  a.Lt = dLt.p;
+  a.info = dinfo.p;
+  a.n = n;
+  a.nf = nf;
+  a.maxiter = maxiter > 0 ? maxiter : 3 * n;
+  a.tol = tol;
+  a.add_eps = add_eps;
+  const size_t smem = (size_t)n * (4 * sizeof(double) + 2 * sizeof(int));
+  FASST_HIP(hipFuncSetAttribute((const void *)k_nnls, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)smem));
+  k_nnls<<<slots, 64, smem, s>>>(a);
+  FASST_LAUNCH_CHECK();
+  FASST_HIP(hipStreamSynchronize(s));
+  FASST_HIP(hipMemcpy(X, dX.p, (size_t)n * nf * sizeof(double), hipMemcpyDeviceToHost));
+  if (info) FASST_HIP(hipMemcpy(info, dinfo.p, (size_t)nf * sizeof(int), hipMemcpyDeviceToHost));
+  return FASST_OK;
+}
+
+}  // extern "C"

@@ -570,6 +570,60 @@ def pipeline_signal(fs, n, seed=61):
     return (x / np.abs(x).max() * 12000).astype(np.int16)
 
 
+def run_pipeline_nnls():
+    """The STFT lead pipeline of run_pipeline with initHF00='nnls'
+    (SeparateLeadStereoTF.py:982-993: per-frame scipy.optimize.nnls of each
+    chunk's SX on WF0, + eps, as the mono SIMM's HF00).  Records each chunk's
+    SX and the HF00 handed to SIMM, and the pipeline's outputs."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import shutil
+    import numpy as np
+    import scipy
+    import scipy.io.wavfile as wf
+    from pyfasst.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    from pyfasst.SeparateLeadStereo.tracking import tracking as TR
+
+    def tracker(S_, N_, logD, prior, logT, verbose=False):
+        return TR.viterbiTrackingArray(logD[:S_, :N_], prior[:S_], logT[:S_, :S_])
+    SL.viterbiTrackingArray = tracker
+    caps = []
+    orig = SL.SIMM.SIMM
+
+    def rec(SX, *a, **kw):
+        if kw.get('HF00') is not None:
+            caps.append((np.array(SX), np.array(kw['HF00'])))
+        return orig(SX, *a, **kw)
+    SL.SIMM.SIMM = rec
+    work = "/tmp/golden_pipeline_nnls"
+    shutil.rmtree(work, ignore_errors=True)
+    os.makedirs(work)
+    os.chdir(work)
+    fs = 8000
+    g = np.load(os.path.join(HERE, "pipeline.npz"))
+    x = g['wav']
+    wav = os.path.join(work, "mix.wav")
+    wf.write(wav, fs, x)
+    np.random.seed(3)
+    proc = SL.SeparateLeadProcess(wav, windowSize=0.0464, nbIter=3, numCompAccomp=6, minF0=100,
+                                  maxF0=800, stepNotes=4, K_numFilters=3, P_numAtomFilters=10,
+                                  verbose=False, outputDirSuffix='out', initHF00='nnls')
+    proc.autoMelSepAndWrite(maxFrames=60)
+    SL.SIMM.SIMM = orig
+    out = {'wav': x, 'fs': np.array(fs), 'WF0': proc.SIMMParams['WF0'],
+           'indexBestPath': np.array(proc.indexBestPath),
+           'HF00': proc.SIMMParams['HF00'],
+           'lead': wf.read(proc.files['voc_output_file'])[1],
+           'acc': wf.read(proc.files['mus_output_file'])[1],
+           'scipy_version': np.array(scipy.__version__), 'nchunks': np.array(len(caps))}
+    for i, (SX, H) in enumerate(caps):
+        out['SX_%d' % i] = SX
+        out['nnls_HF00_%d' % i] = H
+    np.savez_compressed(os.path.join(HERE, "pipeline_nnls.npz"), **out)
+    print("pipeline_nnls", {k: np.shape(v) for k, v in out.items()})
+
+
 def run_pipeline_mqt():
     """The lead/accompaniment pipeline on the MinQT, tfrepresentation='mqt'
     (the reference's own MinQTSLStest, pyfasst_tests/.../
@@ -645,13 +699,15 @@ if __name__ == "__main__":
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
          "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0, "nmfinit_same": lambda: run_nmfinit(True),
          "nmfinit_indiv": lambda: run_nmfinit(False), "pipeline": run_pipeline,
-         "wf0_cqt": run_wf0_cqt, "pipeline_mqt": run_pipeline_mqt}.get(
+         "wf0_cqt": run_wf0_cqt, "pipeline_mqt": run_pipeline_mqt,
+         "pipeline_nnls": run_pipeline_nnls}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
     names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0", "nmfinit_same",
-                              "nmfinit_indiv", "pipeline", "wf0_cqt", "pipeline_mqt"] + list(CASES))
+                              "nmfinit_indiv", "pipeline", "wf0_cqt", "pipeline_mqt",
+                              "pipeline_nnls"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

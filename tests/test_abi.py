@@ -14,7 +14,7 @@ def declared_symbols():
     syms = set()
     for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))):
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        syms |= set(re.findall(r"\b((?:fasst|simm|nmf|cqt|viterbi|dict)_\w+)\s*\(", src))
+        syms |= set(re.findall(r"\b((?:fasst|simm|nmf|cqt|viterbi|dict|nnls)_\w+)\s*\(", src))
     return sorted(syms)
 
 

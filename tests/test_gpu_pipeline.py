@@ -77,3 +77,47 @@ def test_auto_melody_separation_mqt_vs_reference(tmp_path, monkeypatch):
         y = wf.read(proc.files[key])[1].astype(np.int64)
         assert y.shape == ref.shape
         assert np.max(np.abs(y - ref.astype(np.int64))) <= 2
+
+
+def test_nnls_columns_vs_reference_chunks():
+    """The batched GPU NNLS on each chunk's SX (the reference's per-frame
+    scipy.optimize.nnls, tests/golden/pipeline_nnls.npz): same active set,
+    values to 1e-10 of the column maximum, plus edge cases (an all-zero
+    right-hand side, a right-hand side in the span of one column)."""
+    from pyfasst_amd.tools.nnls import nnls_columns
+    g = load("pipeline_nnls")
+    W = g['WF0']
+    for i in range(int(g['nchunks'])):
+        X = nnls_columns(W, g['SX_%d' % i], add_eps=1e-9)
+        ref = g['nnls_HF00_%d' % i]
+        np.testing.assert_array_equal(X > 1e-9, ref > 1e-9)
+        assert rel(X, ref) < 1e-10
+    B = np.zeros((W.shape[0], 3))
+    B[:, 1] = 2.5 * W[:, 7]
+    B[:, 2] = -W[:, 3]
+    X = nnls_columns(W, B)
+    np.testing.assert_array_equal(X[:, 0], 0.0)
+    np.testing.assert_array_equal(X[:, 2], 0.0)
+    assert abs(X[7, 1] - 2.5) < 1e-10 and np.sum(np.abs(np.delete(X[:, 1], 7))) < 1e-10
+
+
+def test_auto_melody_separation_nnls_init_vs_reference(tmp_path, monkeypatch):
+    """initHF00='nnls' end to end (SeparateLeadStereoTF.py:982-993): the chunk
+    HF00 of the mono SIMM from the batched GPU NNLS; melody path exact,
+    WAVs within 2 LSB of the reference run (tests/golden/pipeline_nnls.npz)."""
+    from pyfasst_amd.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    monkeypatch.chdir(tmp_path)
+    g = load("pipeline_nnls")
+    wav = os.path.join(str(tmp_path), "mix.wav")
+    wf.write(wav, int(g['fs']), g['wav'])
+    np.random.seed(3)
+    proc = SL.SeparateLeadProcess(wav, windowSize=0.0464, nbIter=3, numCompAccomp=6, minF0=100,
+                                  maxF0=800, stepNotes=4, K_numFilters=3, P_numAtomFilters=10,
+                                  verbose=False, outputDirSuffix='out', initHF00='nnls')
+    proc.autoMelSepAndWrite(maxFrames=60)
+    np.testing.assert_array_equal(proc.indexBestPath, g['indexBestPath'])
+    assert rel(proc.SIMMParams['HF00'], g['HF00']) < 1e-8
+    for key, ref in (('voc_output_file', g['lead']), ('mus_output_file', g['acc'])):
+        y = wf.read(proc.files[key])[1].astype(np.int64)
+        assert y.shape == ref.shape
+        assert np.max(np.abs(y - ref.astype(np.int64))) <= 2

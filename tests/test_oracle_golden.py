@@ -237,3 +237,13 @@ def test_nmf_init_golden(same):
     np.testing.assert_array_equal(m.estim_param_a_post_model(), g['logliks'])
     for k in range(3):
         np.testing.assert_array_equal(m.spec_comps[k]['factor'][0]['FB'], g['final_FB_%d' % k])
+
+
+def test_nnls_oracle_matches_reference_run():
+    """initHF00='nnls' (SeparateLeadStereoTF.py:982-993): the oracle's per-frame
+    scipy.optimize.nnls reproduces the HF00 the reference handed to SIMM."""
+    import nnls_ref
+    g = load("pipeline_nnls")
+    for i in range(int(g['nchunks'])):
+        np.testing.assert_array_equal(nnls_ref.nnls_hf00(g['WF0'], g['SX_%d' % i]),
+                                      g['nnls_HF00_%d' % i])
