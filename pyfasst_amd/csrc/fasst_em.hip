@@ -70,6 +70,7 @@ __device__ __forceinline__ double rcp_nr(double x) {
 // W[j] = FB[j] . FW[j], written [KP][Fp] (f contiguous).
 // one block per (16-bin tile, source): FB tile and FW staged in LDS; the
 // outputs are written bin-fastest (coalesced Wkf rows)
+template <bool FWG>   // FWG: FW read from L2 (KP > 64), else staged in LDS
 __global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB,
                                                    const double *__restrict__ FW,
                                                    double *__restrict__ Wkf,
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB
   extern __shared__ __attribute__((aligned(16))) double s_m[];
   double *s_fb = s_m;             // [16][KP + 1]
   double *s_fw = s_m + 16 * (KP + 1);  // [KP][KP] (KP <= 64; else FW is read from L2)
-  const bool fwg = KP > 64;
+  constexpr bool fwg = FWG;
   const int j = blockIdx.y, f0 = blockIdx.x * 16;
   const double *fw = fwg ? FW + (size_t)j * KP * KP : s_fw;
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
@@ -101,13 +102,14 @@ __global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB
 
 // FWHt[j][t][k] = sum_q FW[j][k][q] TW[j][q][t]; one block per (64-frame
 // tile, source): FW and the TW tile staged in LDS, coalesced [t][k] writes.
+template <bool FWG>
 __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
                                                const double *__restrict__ TW,
                                                double *__restrict__ FWHt, double *__restrict__ TWt,
                                                int J, int Tp, int KP, const int *halt) {
   HALT_GUARD(halt);
   extern __shared__ __attribute__((aligned(16))) double s_f[];
-  const bool fwg = KP > 64;       // FW read from L2 (its [KP][KP] copy would not fit)
+  constexpr bool fwg = FWG;       // FW read from L2 (its [KP][KP] copy would not fit)
   double *s_fw = s_f;             // [KP][KP] (KP <= 64)
   double *s_tw = s_f + (fwg ? 0 : KP * KP);   // [KP][64]
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
@@ -1394,13 +1396,14 @@ struct UArgs {
 // FB *= (num / max(den, eps))^omega with den = FW . rowsum(TW) (see
 // k_fb_contract) or, for one of several spectral components, the contracted
 // denominator; then W_new = FB . FW in both layouts.
+template <bool FWG>
 __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   HALT_GUARD(a.halt);
   // LDS: FW [KP][KP] | FB rows [16][KP] | den [KP] | W_new rows [16][KP + 1]
   extern __shared__ __attribute__((aligned(16))) double s_fw[];
   const int f0 = blockIdx.x * 16, j = blockIdx.y;
   const int KP = a.KP;
-  const bool fwg = KP > 64;   // FW read from L2 (its [KP][KP] copy would not fit)
+  constexpr bool fwg = FWG;   // FW read from L2 (its [KP][KP] copy would not fit)
   const double *fw = fwg ? a.FW + (size_t)j * KP * KP : s_fw;
   double *s_fb = s_fw + (fwg ? 0 : KP * KP);
   double *s_den = s_fb + 16 * KP;
@@ -2111,6 +2114,7 @@ __global__ __launch_bounds__(256) void k_renorm_stats(const RArgs a) {
 // with partial sums for the restart test), the mixing filters / sqrt(e).
 // FW and the 'inst' parameters are read by every block here, so they are
 // rewritten in stage 3 from the scales chunk 0 records.
+template <bool BIG>
 __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
   HALT_GUARD(a.halt);
   __shared__ double s_red[256];
@@ -2133,7 +2137,7 @@ __global__ __launch_bounds__(256) void k_renorm_apply(const RArgs a) {
       s_red[q] = x.x * x.x + x.y * x.y;
     }
   }
-  const bool big = a.nchunk * KP > 64 * 64 || KP > 64;
+  constexpr bool big = BIG;   // chunk maxima / FW too large for s_big: read from L2
   const double *pmx = big ? a.pmax + (size_t)j * a.nchunk * KP : s_big;
   const double *fwb = big ? a.FW + (size_t)j * KP * KP : s_big;
   if (!big)
@@ -2700,7 +2704,7 @@ int build_inst_A(fasst_ctx *c) {
 
 int launch_w_old(fasst_ctx *c) {
   prof_begin(c, KW);
-  k_w_from_fb<<<dim3(c->nft, c->J), 256, fw_lds(c, 16 * (c->KP + 1)),
+  (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, c->J), 256, fw_lds(c, 16 * (c->KP + 1)),
                 c->stream>>>(c->FB.p, c->FW.p, c->Wkf.p, nullptr, c->J, c->Fp, c->KP, c->halt);
   prof_end(c, KW);
   FASST_LAUNCH_CHECK();
@@ -2801,7 +2805,10 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   }
   prof_begin(c, KREN);
   k_renorm_stats<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
-  k_renorm_apply<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
+  if (c->nchunk_r * c->KP > 64 * 64 || c->KP > 64)
+    k_renorm_apply<true><<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
+  else
+    k_renorm_apply<false><<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
   k_renorm_final<<<1, 256, 0, c->stream>>>(r, c->J, iter);
   FASST_LAUNCH_CHECK();
   if (c->anytb) {
@@ -3135,7 +3142,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
         break;
     }
     FASST_LAUNCH_CHECK();
-    k_fb_update<<<dim3(c->nft, J), 256,
+    (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
                   fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
                   c->stream>>>(u);
     FASST_LAUNCH_CHECK();
@@ -3195,7 +3202,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
       }
       k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
       k_fw_final<<<J, 256, 0, c->stream>>>(w);
-      k_w_from_fb<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
+      (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
                     c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
                                  c->halt);
       FASST_LAUNCH_CHECK();
@@ -3293,7 +3300,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   prof_begin(c, KFWH);
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-  k_fwh_t<<<dim3((c->Tp + 63) / 64, J), 256, fw_lds(c, c->KP * 64),
+  (c->KP > 64 ? k_fwh_t<true> : k_fwh_t<false>)<<<dim3((c->Tp + 63) / 64, J), 256, fw_lds(c, c->KP * 64),
             side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
                     c->halt);
   prof_end(c, KFWH);
@@ -3523,7 +3530,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     FASST_LAUNCH_CHECK();
   }
   prof_begin(c, KFBU);
-  k_fb_update<<<dim3(c->nft, J), 256,
+  (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
                 fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
                 c->stream>>>(u);
   prof_end(c, KFBU);
@@ -3571,7 +3578,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     }
     k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
     k_fw_final<<<J, 256, 0, c->stream>>>(w);
-    k_w_from_fb<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
+    (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
                   c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
                                c->halt);
     prof_end(c, KFWU);

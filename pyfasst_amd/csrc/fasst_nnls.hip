@@ -250,7 +250,10 @@ int nnls_columns(int device, int m, int n, const double *A, int nf, const double
   DeviceGuard g(device);
   int st;
   hipStream_t s = nullptr;
-  const int slots = std::min(nf, 2048);
+  // one wave (and one L / L^T scratch pair, 16 n^2 bytes) per slot: up to
+  // 1024 slots within ~16 GB of scratch
+  const size_t per = (size_t)16 * n * n;
+  const int slots = (int)std::min<size_t>(nf, std::max<size_t>(64, std::min<size_t>(1024, (16ull << 30) / per)));
   DBuf<double> dA, dB, dG, dCt, dX, dL, dLt;
   DBuf<int> dinfo;
   if ((st = dA.alloc((size_t)m * n)) || (st = dB.alloc((size_t)m * nf)) ||

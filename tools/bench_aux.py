@@ -256,6 +256,54 @@ def bench_wf0(steps, warmup):
                                        % F0Table.size}}
 
 
+def bench_nnls(steps, warmup, frames=1000, seed=0):
+    """initHF00='nnls' on one pipeline chunk at config-5 scale: the C5 STFT
+    dictionary (1092 combs, F=2049) and 1000 frames of synthetic spectra
+    (a few combs + noise), one batched GPU solve per step; the CPU baseline
+    is scipy.optimize.nnls (the reference's call) on a sample of frames."""
+    import tempfile
+    from pyfasst_amd.SeparateLeadStereo import separateLeadFunctions as slf
+    from pyfasst_amd.tftransforms.stft import STFT
+    from pyfasst_amd.tools.nnls import nnls_columns
+    from pyfasst_amd.tools.utils import sqrt_blackmanharris
+    os.chdir(tempfile.mkdtemp())
+    t = STFT(linFTLen=4096, atomHopFactor=0.25, winFunc=sqrt_blackmanharris, fs=44100)
+    F0Table, WF0, _ = slf.generate_WF0_TR_chirped(t, 39, 2000, stepNotes=16, loadWF0=False)
+    rs = np.random.RandomState(seed)
+    F, n = WF0.shape
+    H = np.zeros((n, frames))
+    for q in range(frames):
+        H[rs.choice(n, 4, replace=False), q] = rs.rand(4)
+    SX = WF0.dot(H) + 1e-3 * WF0.max() * rs.rand(F, frames)
+    ms = []
+    for i in range(warmup + steps):
+        t0 = time.perf_counter()
+        X = nnls_columns(WF0, SX)
+        if i >= warmup:
+            ms.append((time.perf_counter() - t0) * 1e3)
+    dm = float(np.median(ms))
+    out = {"metric": "NNLS frames/sec (initHF00='nnls', one 1000-frame chunk, host-inclusive)",
+           "value": round(frames / (dm * 1e-3), 2), "unit": "frames/s", "ms_per_chunk": round(dm, 2),
+           "steps": steps, "warmup": warmup, "dtype": "f64",
+           "config": {"workload": "nnls(WF0 %d x %d, 1000 frames)" % (F, n)},
+           "active_mean": round(float(np.mean(np.sum(X > 0, axis=0))), 1)}
+    if not NO_CPU:
+        from scipy.optimize import nnls
+        t0 = time.perf_counter()
+        k = 4
+        ref = [nnls(WF0, SX[:, q])[0] for q in range(k)]
+        cpu = (time.perf_counter() - t0) / k
+        out["vs_scipy"] = {"max_rel": float(max(np.max(np.abs(X[:, q] - ref[q])) /
+                                              max(np.max(np.abs(ref[q])), 1e-300)
+                                              for q in range(k))),
+                           "same_support": bool(all(np.array_equal(X[:, q] > 0, ref[q] > 0)
+                                                    for q in range(k)))}
+        out["cpu_baseline"] = {"value": round(1.0 / cpu, 3), "unit": "frames/s", "cores": 1,
+                               "kind": "reference",
+                               "sample": "scipy.optimize.nnls (the reference's call) on 4 frames"}
+    return out
+
+
 def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
     from pyfasst_amd import _lib
     from pyfasst_amd.SeparateLeadStereo.tracking._tracking import viterbiTracking
@@ -295,7 +343,8 @@ def bench_viterbi(steps, warmup, S=1092, N=20000, seed=0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi", "wf0", "separate"),
+    ap.add_argument("--workload", choices=("simm", "nmf", "cqt", "viterbi", "wf0", "separate",
+                                           "nnls"),
                     required=True)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
@@ -305,7 +354,7 @@ def main():
     global NO_CPU
     NO_CPU = a.no_cpu_baseline
     fn = {"simm": bench_simm, "nmf": bench_nmf, "cqt": bench_cqt, "viterbi": bench_viterbi,
-          "wf0": bench_wf0, "separate": bench_separate}[a.workload]
+          "wf0": bench_wf0, "separate": bench_separate, "nnls": bench_nnls}[a.workload]
     print(json.dumps(fn(a.steps, a.warmup)), flush=True)
 
 
