@@ -4,8 +4,12 @@ Workload (BASELINE.json configs[2] / [3]): synthetic stereo STFT-domain clip,
 F=2049 bins x T=10000 frames, J=4 convolutive sources of spatial rank 2,
 K=32 NMF components (MultiChanNMFConv + makeItConvolutive).  One clip per
 GPU (config 4 = 8 independent clips): weak scaling, no collective in the
-data path; torch.distributed (RCCL) only provides the start/stop barrier and
-the max-over-ranks time.
+data path; torch.distributed only provides the start/stop barrier and the
+max-over-ranks time, on the gloo backend (host-side, nothing on the GPUs)
+unless FASST_BENCH_BACKEND=nccl selects RCCL: measured on one MI355X, an
+RCCL process group alone costs the timed GEM loop ~2.5% (925-930 vs 945-949
+EM it/s at one rank, profiles/r3_dist_backend.txt), and the path has no
+exchange step that would need it.
 
 A "step" is one GEM iteration (audioModel.py:384-428) on the GPU, inputs
 resident in HBM.  Prints ONE JSON line on rank 0.
@@ -188,11 +192,12 @@ def main():
 
     world, rank, local, seed, device = rank_setup()
     dist = None
-    # RCCL ("nccl") is the product; FASST_BENCH_BACKEND=gloo rehearses the
-    # multi-rank path with more ranks than GPUs (ranks share cards round-robin)
-    backend = os.environ.get("FASST_BENCH_BACKEND", "nccl")
+    # control plane only (barrier + max): gloo by default, RCCL with
+    # FASST_BENCH_BACKEND=nccl (rank r on GPU LOCAL_RANK either way; with gloo
+    # more ranks than GPUs share the cards round-robin)
+    backend = os.environ.get("FASST_BENCH_BACKEND", "gloo")
     # FASST_BENCH_DIST=1 initialises the process group even for one rank (the
-    # RCCL barrier / max-over-ranks path exercised on a one-GPU box)
+    # barrier / max-over-ranks path exercised on a one-GPU box)
     if world > 1 or os.environ.get("FASST_BENCH_DIST") == "1":
         import torch
         import torch.distributed as dist
