@@ -77,6 +77,21 @@ __device__ __forceinline__ double nmf_rcp(double x) {
   return fma(fma(-x, r, 1.0), r, r);
 }
 
+// raw-buffer loads for the fused contractions: wave-uniform resource in
+// SGPRs + a 32-bit lane offset, so every load of a tile is issued
+// unconditionally (a guarded pointer load compiles into an exec branch per
+// load, and the branches made the compiler wait for ALL outstanding loads --
+// the next tile's prefetch included -- before each tile's MFMAs).  An offset
+// of kNmfOOB is outside every resource and reads 0.0; otherwise the accesses
+// stay inside the (padded, zero-filled) allocations, see nmf_create.
+typedef unsigned nmf_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nmf_rsrc(const double *p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double nmf_ld(__amdgpu_buffer_rsrc_t r, unsigned vo) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, 0, 0));
+}
+
 __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -85,22 +100,52 @@ __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
 // is recomputed tile by tile on the MFMA pipe and never stored, the ratios
 // X = SX / max(hat^2, eps), Y = 1 / max(hat, eps) stay in registers, and the
 // accumulator-as-operand layout of 16x16x4 feeds them straight into the
-// contraction (as the FASST FB / TW contractions, fasst_em.hip).  Each
-// 4-wave workgroup splits its reduction range over its waves, folds the four
-// partials in LDS in wave order, and writes one partial per workgroup row to
-// `part` ([group][num / den][K][F or N]); the consumer (k_nmf_w_part /
-// k_nmf_h_part) sums the groups in index order: deterministic.
-template <int NT, int NKC>
-__device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT][NKC],
+// contraction (as the FASST FB / TW contractions, fasst_em.hip).
+//
+// Register layouts are chosen so that every operand a lane needs is a run of
+// consecutive doubles (16-byte loads, 20 per 16 x 32 tile instead of 40
+// 8-byte ones, so a tile's prefetch and the tile in flight fit the 63 loads
+// the wave's vmcnt can track):
+//   - the hat product's component index is k = tq * NKS + s (step s, lane
+//     row tq): W rows and frame-major H rows (Ht, N x K, the fused path's
+//     copy of H) are contiguous in s;
+//   - the contraction's output column is component fl * NKC + kc: the H / W
+//     row of a frame / bin is contiguous in kc;
+//   - the kept dimension is split over PW = 2 interleaved 16-wide tiles
+//     (element e of a 32-wide group sits in tile e & 1 at lane row e >> 1):
+//     the SX values of a lane are contiguous in p.
+// Each 4-wave workgroup splits its reduction range over its waves, folds the
+// four partials in LDS in wave order, and writes one partial per workgroup
+// row to `part`; the consumer (k_nmf_w_part / k_nmf_h_part) sums the groups
+// in index order: deterministic.
+constexpr int kNmfPW = 2;
+
+typedef unsigned nmf_u4 __attribute__((ext_vector_type(4)));
+// NV consecutive doubles from byte offset vo (16-byte loads, one 8-byte tail)
+template <int NV>
+__device__ __forceinline__ void nmf_ldv(__amdgpu_buffer_rsrc_t r, unsigned vo, double (&d)[NV]) {
+#pragma unroll
+  for (int j = 0; j + 1 < NV; j += 2) {
+    const nmf_u4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(vo + 8u * j), 0, 0);
+    d[j] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 0, 1));
+    d[j + 1] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 2, 3));
+  }
+  if constexpr (NV & 1) d[NV - 1] = nmf_ld(r, vo + 8u * (NV - 1));
+}
+
+// partial for (kept index r0 + PW (tq + 4m) + p, component fl * NKC + kc);
+// TR: [r][K] rows (the H update's frame-major partials), else [K][R]
+template <int NKC, bool TR>
+__device__ __forceinline__ void nmf_fold_store(d4 (&num)[kNmfPW][NKC], d4 (&den)[kNmfPW][NKC],
                                                double *__restrict__ pn, double *__restrict__ pd,
-                                               int r0, int R, int wv, int lane, int k0 = 0) {
-  constexpr int NE = NT * NKC * 4;
+                                               int r0, int R, int wv, int lane) {
+  constexpr int NE = kNmfPW * NKC * 4, K = 16 * NKC;
   __shared__ double red[2][NE][64];
   const int fl = lane & 15, tq = lane >> 4;
   for (int w = 0; w < 4; ++w) {
     if (wv == w) {
 #pragma unroll
-      for (int p = 0; p < NT; ++p)
+      for (int p = 0; p < kNmfPW; ++p)
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc)
 #pragma unroll
@@ -115,10 +160,11 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT]
               red[0][e][lane] = a;
               red[1][e][lane] = b;
             } else {
-              const int r = r0 + p * 16 + tq + 4 * m, k = k0 + kc * 16 + fl;
+              const int r = r0 + kNmfPW * (tq + 4 * m) + p, k = fl * NKC + kc;
               if (r < R) {
-                pn[(size_t)k * R + r] = a;
-                pd[(size_t)k * R + r] = b;
+                const size_t o = TR ? (size_t)r * K + k : (size_t)k * R + r;
+                pn[o] = a;
+                pd[o] = b;
               }
             }
           }
@@ -128,61 +174,51 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[NT][NKC], d4 (&den)[NT]
 }
 
 // W update (nmf.py:39-44): numT[k][f] = sum_t H[k][t] X[f][t], denT with Y.
-// A workgroup owns FPW 16-bin tiles and 4 frame chunks (one per wave); the
-// W rows are loop-invariant B operands of the hat tiles.
-// KS > 1: the contraction's K columns are split over blockIdx.z (each slice
-// recomputes the whole hat tile): fewer accumulators per wave, so two waves
-// per SIMD fit where one slice per wave needs the whole register file
-template <int NKC, int FPW, int KS = 1>
-__global__ __launch_bounds__(256, KS > 1 ? 2 : 1) void k_nmf_wnum(const double *__restrict__ W,
-                                                  const double *__restrict__ H,
-                                                  const double *__restrict__ SXt,
-                                                  double *__restrict__ part, int F, int N, int tpc) {
-  constexpr int NKS = 4 * NKC, K = 16 * NKC, NKL = NKC / KS;
-  const int kc0 = blockIdx.z * NKL;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
-  const int ft0 = blockIdx.x * FPW, nft = (F + 15) / 16, ntt = (N + 15) / 16;
-  double wk[FPW][NKS];
+// A workgroup owns one 32-bin group (bin g0 + 2 fl + p) and 4 frame chunks
+// (one per wave); the group's W rows are loop-invariant hat operands.
+template <int NKC>
+__global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ W,
+                                                     const double *__restrict__ Ht,
+                                                     const double *__restrict__ SXt,
+                                                     double *__restrict__ part, int F, int N, int tpc) {
+  constexpr int NKS = 4 * NKC, K = 16 * NKC, PW = kNmfPW;
+  const int lane = threadIdx.x & 63, fl = lane & 15, tq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g0 = blockIdx.x * 16 * PW, ntt = (N + 15) / 16;
+  const __amdgpu_buffer_rsrc_t rW = nmf_rsrc(W), rH = nmf_rsrc(Ht);
+  double wk[PW][NKS];  // bins past F: W's zero pad rows
 #pragma unroll
-  for (int p = 0; p < FPW; ++p) {
-    const int f = (ft0 + p) * 16 + fl;
+  for (int p = 0; p < PW; ++p) nmf_ldv(rW, (unsigned)(((g0 + PW * fl + p) * K + tq * NKS) * 8), wk[p]);
+  d4 num[PW][NKC], den[PW][NKC];
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) wk[p][s] = f < F ? W[(size_t)f * K + 4 * s + tq] : 0.0;
-  }
-  d4 num[FPW][NKL], den[FPW][NKL];
+  for (int p = 0; p < PW; ++p)
 #pragma unroll
-  for (int p = 0; p < FPW; ++p)
-#pragma unroll
-    for (int kc = 0; kc < NKL; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int tb = (blockIdx.y * 4 + wv) * tpc, te = min(tb + tpc, ntt);
-  // the next frame tile's H operands and SX values are loaded while this
-  // tile's MFMAs run (the loop was L2-latency bound)
-  double th[2][NKS], hb[2][4][NKL], sxv[2][FPW][4];
+  // the next frame tile's operands are loaded while this tile's MFMAs run.
+  // Frames past N read Ht's zero pad rows (hb = 0: they add nothing) and
+  // SXt's pad; bins past F read the next SXt row (finite, never stored)
+  double th[2][NKS], hb[2][4][NKC], sxv[2][4][PW];
+  const unsigned vo_th = (unsigned)((fl * K + tq * NKS) * 8);
+  const unsigned vo_hb = (unsigned)((tq * K + fl * NKC) * 8);
+  const unsigned vo_sx = (unsigned)((tq * F + g0 + PW * fl) * 8);
   auto load = [&](int tt, int slot) {
     const int t0 = tt * 16;
-#pragma unroll
-    for (int s = 0; s < NKS; ++s)
-      th[slot][s] = t0 + fl < N ? H[(size_t)(4 * s + tq) * N + t0 + fl] : 0.0;
+    const unsigned ho = (unsigned)(t0 * K * 8);
+    nmf_ldv(rH, vo_th + ho, th[slot]);
+    const __amdgpu_buffer_rsrc_t rS = nmf_rsrc(SXt + (size_t)t0 * F);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int t = t0 + tq + 4 * i;
-#pragma unroll
-      for (int kc = 0; kc < NKL; ++kc)
-        hb[slot][i][kc] = t < N ? H[(size_t)((kc0 + kc) * 16 + fl) * N + t] : 0.0;
-#pragma unroll
-      for (int p = 0; p < FPW; ++p) {
-        const int f = (ft0 + p) * 16 + fl;
-        sxv[slot][p][i] = (f < F && t < N) ? SXt[(size_t)t * F + f] : 0.0;
-      }
+      nmf_ldv(rH, vo_hb + ho + (unsigned)(4 * i * K * 8), hb[slot][i]);
+      nmf_ldv(rS, vo_sx + (unsigned)(4 * i * F * 8), sxv[slot][i]);
     }
   };
-  auto compute = [&](int tt, int cs) {
-    const int t0 = tt * 16;
-    // the hat tiles of all FPW bin tiles first, four accumulation chains each
+  auto compute = [&](int cs) {
+    // the hat tiles of both bin tiles first, four accumulation chains each
     // (one wave per SIMD: the MFMA latency is hidden by independent chains)
-    d4 hv[FPW];
+    d4 hv[PW];
 #pragma unroll
-    for (int p = 0; p < FPW; ++p) {
+    for (int p = 0; p < PW; ++p) {
       d4 v0 = d4{0.0, 0.0, 0.0, 0.0}, v1 = v0, v2 = v0, v3 = v0;
 #pragma unroll
       for (int s = 0; s < NKS; s += 4) {
@@ -194,99 +230,110 @@ __global__ __launch_bounds__(256, KS > 1 ? 2 : 1) void k_nmf_wnum(const double *
       hv[p] = (v0 + v1) + (v2 + v3);
     }
 #pragma unroll
-    for (int p = 0; p < FPW; ++p) {
-      if (ft0 + p >= nft) break;  // wave-uniform
-      const int f = (ft0 + p) * 16 + fl;
-      const d4 v = hv[p];  // hat at (frame t0+tq+4i, bin f)
+    for (int p = 0; p < PW; ++p) {
+      const d4 v = hv[p];  // hat at (frame t0+tq+4i, bin g0+2fl+p)
+      // no masks: frames past N meet hb = 0, bins past F are never stored,
+      // and every ratio is finite (hat >= 0, floored at eps)
       double x[4], y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int t = t0 + tq + 4 * i;
-        const bool ok = f < F && t < N;
         const double h = v[i];
-        x[i] = ok ? sxv[cs][p][i] * nmf_rcp(fmax(h * h, kNmfEps)) : 0.0;
-        y[i] = ok ? nmf_rcp(fmax(h, kNmfEps)) : 0.0;
+        x[i] = sxv[cs][i][p] * nmf_rcp(fmax(h * h, kNmfEps));
+        y[i] = nmf_rcp(fmax(h, kNmfEps));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int kc = 0; kc < NKL; ++kc) {
+        for (int kc = 0; kc < NKC; ++kc) {
           num[p][kc] = nmfma(x[i], hb[cs][i][kc], num[p][kc]);
           den[p][kc] = nmfma(y[i], hb[cs][i][kc], den[p][kc]);
         }
     }
   };
-  // two tiles per trip so the double-buffer slot is a compile-time index
-  if (tb < te) load(tb, 0);
-  for (int tt = tb; tt < te; tt += 2) {
-    if (tt + 1 < te) load(tt + 1, 1);
-    compute(tt, 0);
-    if (tt + 1 < te) {
-      if (tt + 2 < te) load(tt + 2, 0);
-      compute(tt + 1, 1);
+  // one tile per trip: the next tile is loaded into slot 1 while slot 0's
+  // MFMAs run, then moved into slot 0 (40 register moves per 192 MFMAs).
+  // The prefetch is unconditional (the last tile again past the end) and its
+  // values are consumed on every path, so it can neither be sunk below the
+  // MFMAs nor make the compiler's vmcnt waits cover it before they run
+  auto rotate = [&]() {
+#pragma unroll
+    for (int s2 = 0; s2 < NKS; ++s2) th[0][s2] = th[1][s2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) hb[0][i][kc] = hb[1][i][kc];
+#pragma unroll
+      for (int p = 0; p < PW; ++p) sxv[0][i][p] = sxv[1][i][p];
     }
+  };
+  if (tb < te) load(tb, 0);
+  for (int tt = tb; tt < te; ++tt) {
+    load(min(tt + 1, te - 1), 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
+    compute(0);
+    __builtin_amdgcn_sched_barrier(0);  // the moves wait for the prefetch
+    rotate();
   }
   const size_t slab = (size_t)K * F;
   double *pn = part + (size_t)blockIdx.y * 2 * slab;
-  nmf_fold_store<FPW, NKL>(num, den, pn, pn + slab, ft0 * 16, F, wv, lane, kc0 * 16);
+  nmf_fold_store<NKC, false>(num, den, pn, pn + slab, g0, F, wv, lane);
 }
 
 // H update (nmf.py:53-59): num[k][t] = sum_f W[f][k] X[f][t], den with Y,
 // hat from the updated W and the rescaled H (hs = W column sums from the W
 // update, applied on load as k_nmf_hscale would; null when W is frozen).  A
-// workgroup owns TPW 16-frame tiles and 4 bin chunks (one per wave).
-template <int NKC, int TPW, int KS = 1>
-__global__ __launch_bounds__(256, KS > 1 ? 2 : 1) void k_nmf_hnum(const double *__restrict__ W,
-                                                  const double *__restrict__ H,
-                                                  const double *__restrict__ hs,
-                                                  const double *__restrict__ SX,
-                                                  double *__restrict__ part, int F, int N, int fpc) {
-  constexpr int NKS = 4 * NKC, K = 16 * NKC, NKL = NKC / KS;
-  const int kc0 = blockIdx.z * NKL;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
-  const int tt0 = blockIdx.x * TPW, nft = (F + 15) / 16, ntt = (N + 15) / 16;
-  double bt[TPW][NKS];
+// workgroup owns one 32-frame group (frame t0 + 2 fl + p) and 4 bin chunks
+// (one per wave).
+template <int NKC>
+__global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ W,
+                                                     const double *__restrict__ Ht,
+                                                     const double *__restrict__ hs,
+                                                     const double *__restrict__ SX,
+                                                     double *__restrict__ part, int F, int N, int fpc) {
+  constexpr int NKS = 4 * NKC, K = 16 * NKC, PW = kNmfPW;
+  const int lane = threadIdx.x & 63, fl = lane & 15, tq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t0g = blockIdx.x * 16 * PW, nft = (F + 15) / 16;
+  const __amdgpu_buffer_rsrc_t rW = nmf_rsrc(W), rH = nmf_rsrc(Ht);
+  // frames past N read the next Ht rows or its zero pad: finite, and their
+  // output columns are never stored
+  double bt[PW][NKS], hsv[NKS];
 #pragma unroll
-  for (int p = 0; p < TPW; ++p) {
-    const int t = (tt0 + p) * 16 + fl;
+  for (int s = 0; s < NKS; ++s) hsv[s] = hs ? hs[tq * NKS + s] : 1.0;
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      const double h = t < N ? H[(size_t)(4 * s + tq) * N + t] : 0.0;
-      bt[p][s] = hs ? h * hs[4 * s + tq] : h;
-    }
-  }
-  d4 num[TPW][NKL], den[TPW][NKL];
+  for (int p = 0; p < PW; ++p) nmf_ldv(rH, (unsigned)(((t0g + PW * fl + p) * K + tq * NKS) * 8), bt[p]);
 #pragma unroll
-  for (int p = 0; p < TPW; ++p)
+  for (int p = 0; p < PW; ++p)
 #pragma unroll
-    for (int kc = 0; kc < NKL; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < NKS; ++s) bt[p][s] *= hsv[s];
+  d4 num[PW][NKC], den[PW][NKC];
+#pragma unroll
+  for (int p = 0; p < PW; ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
   const int fb = (blockIdx.y * 4 + wv) * fpc, fe = min(fb + fpc, nft);
-  // the next bin tile's W operands and SX values are loaded while this
-  // tile's MFMAs run
-  double ao[2][NKS], bw[2][4][NKL], sxv[2][TPW][4];
+  // the next bin tile's operands are loaded while this tile's MFMAs run;
+  // bins past F read W's zero pad rows (bw = 0: they add nothing) and SX's
+  // pad or the next SX row
+  double ao[2][NKS], bw[2][4][NKC], sxv[2][4][PW];
+  const unsigned vo_ao = (unsigned)((fl * K + tq * NKS) * 8);
+  const unsigned vo_bw = (unsigned)((tq * K + fl * NKC) * 8);
+  const unsigned vo_sx = (unsigned)((tq * N + t0g + PW * fl) * 8);
   auto load = [&](int ft, int slot) {
     const int f0 = ft * 16;
-#pragma unroll
-    for (int s = 0; s < NKS; ++s)
-      ao[slot][s] = f0 + fl < F ? W[(size_t)(f0 + fl) * K + 4 * s + tq] : 0.0;
+    const unsigned wo = (unsigned)(f0 * K * 8);
+    nmf_ldv(rW, vo_ao + wo, ao[slot]);
+    const __amdgpu_buffer_rsrc_t rS = nmf_rsrc(SX + (size_t)f0 * N);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int f = f0 + 4 * i + tq;
-#pragma unroll
-      for (int kc = 0; kc < NKL; ++kc)
-        bw[slot][i][kc] = f < F ? W[(size_t)f * K + (kc0 + kc) * 16 + fl] : 0.0;
-#pragma unroll
-      for (int p = 0; p < TPW; ++p) {
-        const int t = (tt0 + p) * 16 + fl;
-        sxv[slot][p][i] = (f < F && t < N) ? SX[(size_t)f * N + t] : 0.0;
-      }
+      nmf_ldv(rW, vo_bw + wo + (unsigned)(4 * i * K * 8), bw[slot][i]);
+      nmf_ldv(rS, vo_sx + (unsigned)(4 * i * N * 8), sxv[slot][i]);
     }
   };
-  auto compute = [&](int ft, int cs) {
-    const int f0 = ft * 16;
-    d4 hv[TPW];   // as k_nmf_wnum: all hat tiles first, four chains each
+  auto compute = [&](int cs) {
+    d4 hv[PW];  // as k_nmf_wnum: both hat tiles first, four chains each
 #pragma unroll
-    for (int p = 0; p < TPW; ++p) {
+    for (int p = 0; p < PW; ++p) {
       d4 v0 = d4{0.0, 0.0, 0.0, 0.0}, v1 = v0, v2 = v0, v3 = v0;
 #pragma unroll
       for (int s = 0; s < NKS; s += 4) {
@@ -298,40 +345,46 @@ __global__ __launch_bounds__(256, KS > 1 ? 2 : 1) void k_nmf_hnum(const double *
       hv[p] = (v0 + v1) + (v2 + v3);
     }
 #pragma unroll
-    for (int p = 0; p < TPW; ++p) {
-      if (tt0 + p >= ntt) break;  // wave-uniform
-      const int t = (tt0 + p) * 16 + fl;
-      const d4 v = hv[p];  // hat at (bin f0+tq+4i, frame t)
+    for (int p = 0; p < PW; ++p) {
+      const d4 v = hv[p];  // hat at (bin f0+tq+4i, frame t0g+2fl+p)
       double x[4], y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int f = f0 + tq + 4 * i;
-        const bool ok = f < F && t < N;
         const double h = v[i];
-        x[i] = ok ? sxv[cs][p][i] * nmf_rcp(fmax(h * h, kNmfEps)) : 0.0;
-        y[i] = ok ? nmf_rcp(fmax(h, kNmfEps)) : 0.0;
+        x[i] = sxv[cs][i][p] * nmf_rcp(fmax(h * h, kNmfEps));
+        y[i] = nmf_rcp(fmax(h, kNmfEps));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int kc = 0; kc < NKL; ++kc) {
+        for (int kc = 0; kc < NKC; ++kc) {
           num[p][kc] = nmfma(x[i], bw[cs][i][kc], num[p][kc]);
           den[p][kc] = nmfma(y[i], bw[cs][i][kc], den[p][kc]);
         }
     }
   };
-  if (fb < fe) load(fb, 0);
-  for (int ft = fb; ft < fe; ft += 2) {
-    if (ft + 1 < fe) load(ft + 1, 1);
-    compute(ft, 0);
-    if (ft + 1 < fe) {
-      if (ft + 2 < fe) load(ft + 2, 0);
-      compute(ft + 1, 1);
+  auto rotate = [&]() {  // as k_nmf_wnum
+#pragma unroll
+    for (int s2 = 0; s2 < NKS; ++s2) ao[0][s2] = ao[1][s2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc) bw[0][i][kc] = bw[1][i][kc];
+#pragma unroll
+      for (int p = 0; p < PW; ++p) sxv[0][i][p] = sxv[1][i][p];
     }
+  };
+  if (fb < fe) load(fb, 0);
+  for (int ft = fb; ft < fe; ++ft) {
+    load(min(ft + 1, fe - 1), 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0);
+    __builtin_amdgcn_sched_barrier(0);  // the moves wait for the prefetch
+    rotate();
   }
   const size_t slab = (size_t)K * N;
   double *pn = part + (size_t)blockIdx.y * 2 * slab;
-  nmf_fold_store<TPW, NKL>(num, den, pn, pn + slab, tt0 * 16, N, wv, lane, kc0 * 16);
+  nmf_fold_store<NKC, true>(num, den, pn, pn + slab, t0g, N, wv, lane);
 }
 
 // k_nmf_w over the fused path's group partials ([g][num / den][K][F])
@@ -376,8 +429,9 @@ __global__ __launch_bounds__(1024) void k_nmf_w_part(double *__restrict__ W,
   if (threadIdx.x == 0) s_out[k] = s;
 }
 
-// k_nmf_hscale + k_nmf_h over the group partials ([g][num / den][K][N])
-__global__ void k_nmf_h_part(double *__restrict__ H, const double *__restrict__ part, int ng,
+// k_nmf_hscale + k_nmf_h on the frame-major Ht over the group partials
+// ([g][num / den][N][K])
+__global__ void k_nmf_h_part(double *__restrict__ Ht, const double *__restrict__ part, int ng,
                              const double *__restrict__ hs, int K, int N) {
   const size_t slab = (size_t)K * N;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slab;
@@ -387,9 +441,17 @@ __global__ void k_nmf_h_part(double *__restrict__ H, const double *__restrict__ 
       n += part[(size_t)g * 2 * slab + i];
       d += part[(size_t)g * 2 * slab + slab + i];
     }
-    const double h = hs ? H[i] * hs[i / N] : H[i];
-    H[i] = h * (n / fmax(d, kNmfEps));
+    const double h = hs ? Ht[i] * hs[i % K] : Ht[i];
+    Ht[i] = h * (n / fmax(d, kNmfEps));
   }
+}
+
+// Ht *= s per component (the W update's renormalisation when H is frozen)
+__global__ void k_nmf_hscale_t(double *__restrict__ Ht, const double *__restrict__ s, int K,
+                               int N) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)K * N;
+       i += (size_t)gridDim.x * blockDim.x)
+    Ht[i] *= s[i % K];
 }
 
 // out[c][r] = in[r][c] for an R x C matrix (row-major), 16 x 16 LDS tiles
@@ -552,8 +614,9 @@ struct nmf_ctx {
   int F = 0, N = 0, K = 0;
   DBuf<double> SX, W, H, hat, X, Y, numT, denT, num, den, s, work;
   // fused path (K % 16 == 0, K <= 64): transposed copies and chunk partials
-  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1, pw = 1, ks = 1;
-  DBuf<double> SXt, part;
+  // (H lives frame-major in Ht there; H is its staging copy for set / get)
+  int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1;
+  DBuf<double> SXt, Ht, part;
 };
 
 namespace {
@@ -573,46 +636,24 @@ int model_xy(nmf_ctx *c) {
 }
 
 constexpr int kNmfCUs = 256;
-#ifndef NMF_KS_DEFAULT
-#define NMF_KS_DEFAULT 1
-#endif
-
-// PW: 16-bin (W update) / 16-frame (H update) tiles per wave
-template <int NKC, int PW, int KS = 1>
-static void nmf_fused_pw(nmf_ctx *c, int update_w, int update_h) {
+template <int NKC>
+static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
   const int F = c->F, N = c->N, K = c->K;
-  const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
+  const int gw = (F + 16 * kNmfPW - 1) / (16 * kNmfPW), gh = (N + 16 * kNmfPW - 1) / (16 * kNmfPW);
   if (update_w) {
-    k_nmf_wnum<NKC, PW, KS><<<dim3((nft + PW - 1) / PW, c->ng_w, KS), 256, 0, c->stream>>>(
-        c->W.p, c->H.p, c->SXt.p, c->part.p, F, N, c->tpc_w);
+    k_nmf_wnum<NKC><<<dim3(gw, c->ng_w), 256, 0, c->stream>>>(c->W.p, c->Ht.p, c->SXt.p, c->part.p,
+                                                              F, N, c->tpc_w);
     k_nmf_w_part<<<K, 1024, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
   }
   const double *hs = update_w ? c->s.p : nullptr;
   if (update_h) {
-    k_nmf_hnum<NKC, PW, KS><<<dim3((ntt + PW - 1) / PW, c->ng_h, KS), 256, 0, c->stream>>>(
-        c->W.p, c->H.p, hs, c->SX.p, c->part.p, F, N, c->fpc_h);
-    k_nmf_h_part<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->part.p, c->ng_h, hs, K,
-                                                                N);
+    k_nmf_hnum<NKC><<<dim3(gh, c->ng_h), 256, 0, c->stream>>>(c->W.p, c->Ht.p, hs, c->SX.p,
+                                                              c->part.p, F, N, c->fpc_h);
+    k_nmf_h_part<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->Ht.p, c->part.p, c->ng_h, hs,
+                                                                K, N);
   } else if (update_w) {
-    k_nmf_hscale<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->H.p, c->s.p, K, N);
+    k_nmf_hscale_t<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->Ht.p, c->s.p, K, N);
   }
-}
-
-template <int NKC>
-static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
-  if constexpr (NKC >= 2) {
-    if (c->ks == 2) {
-      if (c->pw == 2)
-        nmf_fused_pw<NKC, 2, 2>(c, update_w, update_h);
-      else
-        nmf_fused_pw<NKC, 1, 2>(c, update_w, update_h);
-      return;
-    }
-  }
-  if (c->pw == 2)
-    nmf_fused_pw<NKC, 2>(c, update_w, update_h);
-  else
-    nmf_fused_pw<NKC, 1>(c, update_w, update_h);
 }
 
 int nmf_iteration(nmf_ctx *c, int update_w, int update_h) {
@@ -671,8 +712,10 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
   size_t gw = std::max({gemm_workspace(F, N, K, 1), gemm_workspace(K, F, N, 2),
                         gemm_workspace(K, N, F, 2), (size_t)1});
-  if (!st) st = c->SX.alloc(FN);
-  if (!st) st = c->W.alloc((size_t)F * K);
+  // zero pads read by the fused contractions' unmasked loads (tiles past
+  // the last bin / frame): 32 W rows, 16 SX rows (+64 values)
+  if (!st) st = c->SX.alloc((size_t)(F + 16) * N + 64);
+  if (!st) st = c->W.alloc((size_t)(F + 32) * K);
   if (!st) st = c->H.alloc((size_t)K * N);
   if (!st) st = c->hat.alloc(FN);
   if (!st) st = c->X.alloc(FN);
@@ -685,23 +728,19 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
   if (!st) st = c->work.alloc(gw);
   // fused path: 4-wave groups (one per CU at the kernels' occupancy of one
   // wave per SIMD), as many groups as fit in one pass over the 256 CUs
-  c->fused = K % 16 == 0 && K <= 64;
+  // (their buffer offsets into W, Ht and 16-row SX / SXt slabs are 32-bit)
+  c->fused = K % 16 == 0 && K <= 64 && (size_t)(N + 32) * K * 8 < 0x7fffffffu &&
+             (size_t)(F + 32) * K * 8 < 0x7fffffffu && (size_t)32 * (F + N + 64) * 8 < 0x7fffffffu;
   if (const char *v = getenv("FASST_NMF_FUSED")) c->fused = c->fused && atoi(v) != 0;
   if (c->fused) {
     const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
-    // launch geometry: PW tiles per wave along the kept dimension, the
-    // contracted dimension split over 4 waves x ng groups so the grid holds
-    // about `waves` waves (A/B knobs FASST_NMF_PW / FASST_NMF_WAVES)
-    // (C2, F=1025 T=2000 K=64: 2 tiles per wave, ~1024 waves measured best,
-    // 0.103 ms per iteration; 1 tile: 0.106, 2048 waves: 0.124)
-    c->pw = 2;
-    c->ks = NMF_KS_DEFAULT;
-    if (const char *v = getenv("FASST_NMF_KS")) c->ks = atoi(v) == 2 ? 2 : 1;
-    if (K < 32) c->ks = 1;
-    int waves = 4 * kNmfCUs;   // per K slice
-    if (const char *v = getenv("FASST_NMF_PW")) c->pw = atoi(v) == 2 ? 2 : 1;
+    // launch geometry: a 32-wide group of the kept dimension per workgroup,
+    // the contracted dimension split over 4 waves x ng groups so the grid
+    // holds about `waves` waves (A/B knob FASST_NMF_WAVES; round 2 at C2,
+    // F=1025 T=2000 K=64: ~1024 waves best, 2048: +20%)
+    int waves = 4 * kNmfCUs;
     if (const char *v = getenv("FASST_NMF_WAVES")) waves = std::max(4, atoi(v));
-    const int uw = (nft + c->pw - 1) / c->pw, uh = (ntt + c->pw - 1) / c->pw;
+    const int uw = (nft + kNmfPW - 1) / kNmfPW, uh = (ntt + kNmfPW - 1) / kNmfPW;
     int ng = std::max(1, std::min((ntt + 3) / 4, waves / (4 * uw)));
     c->tpc_w = (ntt + 4 * ng - 1) / (4 * ng);
     c->ng_w = ((ntt + c->tpc_w - 1) / c->tpc_w + 3) / 4;
@@ -709,7 +748,8 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
     c->fpc_h = (nft + 4 * ng - 1) / (4 * ng);
     c->ng_h = ((nft + c->fpc_h - 1) / c->fpc_h + 3) / 4;
     const size_t np = std::max((size_t)c->ng_w * 2 * K * F, (size_t)c->ng_h * 2 * K * N);
-    if (!st) st = c->SXt.alloc(FN);
+    if (!st) st = c->SXt.alloc((size_t)(N + 16) * F + 64);
+    if (!st) st = c->Ht.alloc((size_t)(N + 32) * K);
     if (!st) st = c->part.alloc(np);
   }
   if (st) {
@@ -749,6 +789,9 @@ int nmf_set_params(nmf_ctx *c, const double *W, const double *H) {
   DeviceGuard g(c->device);
   FASST_HIP(hipMemcpyAsync(c->W.p, W, (size_t)c->F * c->K * 8, hipMemcpyHostToDevice, c->stream));
   FASST_HIP(hipMemcpyAsync(c->H.p, H, (size_t)c->K * c->N * 8, hipMemcpyHostToDevice, c->stream));
+  if (c->fused)
+    k_nmf_transpose<<<dim3((c->N + 15) / 16, (c->K + 15) / 16), 256, 0, c->stream>>>(
+        c->H.p, c->Ht.p, c->K, c->N);
   FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
 }
@@ -821,6 +864,9 @@ int nmf_get_params(nmf_ctx *c, double *W, double *H) {
   if (!c) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   if (W) FASST_HIP(hipMemcpyAsync(W, c->W.p, (size_t)c->F * c->K * 8, hipMemcpyDeviceToHost, c->stream));
+  if (H && c->fused)
+    k_nmf_transpose<<<dim3((c->K + 15) / 16, (c->N + 15) / 16), 256, 0, c->stream>>>(
+        c->Ht.p, c->H.p, c->N, c->K);
   if (H) FASST_HIP(hipMemcpyAsync(H, c->H.p, (size_t)c->K * c->N * 8, hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
