@@ -106,11 +106,13 @@ __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
 // consecutive doubles (16-byte loads, 20 per 16 x 32 tile instead of 40
 // 8-byte ones, so a tile's prefetch and the tile in flight fit the 63 loads
 // the wave's vmcnt can track):
-//   - the hat product's component index is k = tq * NKS + s (step s, lane
-//     row tq): W rows and frame-major H rows (Ht, N x K, the fused path's
-//     copy of H) are contiguous in s;
-//   - the contraction's output column is component fl * NKC + kc: the H / W
-//     row of a frame / bin is contiguous in kc;
+//   - the hat product's component index at step s, lane row tq is
+//     k = 8 (s >> 1) + 2 tq + (s & 1): a lane's W row / frame-major H row
+//     (Ht, N x K, the fused path's copy of H) values come in 16-byte pairs,
+//     and the four lane rows of one load cover 64 contiguous bytes;
+//   - the contraction's output column kc of lane column fl is component
+//     32 (kc >> 1) + 2 fl + (kc & 1) (a 16-wide tail 16 kc + fl for odd
+//     NKC): 16-byte pairs again, 16 lanes on 256 contiguous bytes;
 //   - the kept dimension is split over PW = 2 interleaved 16-wide tiles
 //     (element e of a 32-wide group sits in tile e & 1 at lane row e >> 1):
 //     the SX values of a lane are contiguous in p.
@@ -119,29 +121,107 @@ __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
 // row to `part`; the consumer (k_nmf_w_part / k_nmf_h_part) sums the groups
 // in index order: deterministic.
 constexpr int kNmfPW = 2;
+#ifndef NMF_ABLATE
+#define NMF_ABLATE 0  // timing-only ablations (1: no per-tile loads, 2: no ratio VALU, 3: no fold, 4: no tiles)
+#endif
 
 typedef unsigned nmf_u4 __attribute__((ext_vector_type(4)));
-// NV consecutive doubles from byte offset vo (16-byte loads, one 8-byte tail)
-template <int NV>
-__device__ __forceinline__ void nmf_ldv(__amdgpu_buffer_rsrc_t r, unsigned vo, double (&d)[NV]) {
+__device__ __forceinline__ void nmf_ld2(__amdgpu_buffer_rsrc_t r, unsigned vo, double &a, double &b) {
+  const nmf_u4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)vo, 0, 0);
+  a = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 0, 1));
+  b = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 2, 3));
+}
+// the hat operand run of a lane: pairs j at byte offset vo + 64 j
+template <int NKS>
+__device__ __forceinline__ void nmf_ld_hat(__amdgpu_buffer_rsrc_t r, unsigned vo, double (&d)[NKS]) {
 #pragma unroll
-  for (int j = 0; j + 1 < NV; j += 2) {
-    const nmf_u4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(vo + 8u * j), 0, 0);
-    d[j] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 0, 1));
-    d[j + 1] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 2, 3));
-  }
-  if constexpr (NV & 1) d[NV - 1] = nmf_ld(r, vo + 8u * (NV - 1));
+  for (int j = 0; j < NKS / 2; ++j) nmf_ld2(r, vo + 64u * j, d[2 * j], d[2 * j + 1]);
+}
+__device__ __forceinline__ constexpr int nmf_hat_k(int s, int tq) { return 8 * (s >> 1) + 2 * tq + (s & 1); }
+// the contraction operand of a lane: pairs m at byte offset vo + 256 m
+// (vo = row + 16 fl), the odd tail at row + 8 (16 (NKC - 1) + fl)
+template <int NKC>
+__device__ __forceinline__ void nmf_ld_con(__amdgpu_buffer_rsrc_t r, unsigned vo, int fl, double (&d)[NKC]) {
+#pragma unroll
+  for (int m = 0; m < NKC / 2; ++m) nmf_ld2(r, vo + 256u * m, d[2 * m], d[2 * m + 1]);
+  if constexpr (NKC & 1) d[NKC - 1] = nmf_ld(r, vo - 8u * fl + 128u * (NKC - 1));
+}
+template <int NKC>
+__device__ __forceinline__ constexpr int nmf_con_k(int kc, int fl) {
+  return kc < (NKC & ~1) ? 32 * (kc >> 1) + 2 * fl + (kc & 1) : 16 * kc + fl;
 }
 
-// partial for (kept index r0 + PW (tq + 4m) + p, component fl * NKC + kc);
+#ifndef NMF_SPREAD
+#define NMF_SPREAD 1
+#endif
+#ifndef NMF_FOLD4
+#define NMF_FOLD4 1
+#endif
+// interleave a tile's prefetch (NL 16-byte loads) with the first MFMAs of
+// the tile in flight, one load per two MFMAs: issued all at once, the four
+// waves' loads queue on the CU's address unit and hold back their MFMAs
+template <int NKC>
+__device__ __forceinline__ void nmf_spread_loads() {
+  if constexpr (NMF_SPREAD) {
+    constexpr int NL = 4 + 2 * NKC + 4 * (NKC / 2 + (NKC & 1));
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // one VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);   // two MFMAs
+    }
+  }
+}
+
+// partial for (kept index r0 + PW (tq + 4m) + p, component nmf_con_k(kc, fl));
 // TR: [r][K] rows (the H update's frame-major partials), else [K][R]
 template <int NKC, bool TR>
 __device__ __forceinline__ void nmf_fold_store(d4 (&num)[kNmfPW][NKC], d4 (&den)[kNmfPW][NKC],
                                                double *__restrict__ pn, double *__restrict__ pd,
                                                int r0, int R, int wv, int lane) {
   constexpr int NE = kNmfPW * NKC * 4, K = 16 * NKC;
-  __shared__ double red[2][NE][64];
+  if (NMF_ABLATE == 3) {  // timing only: no fold, one store per lane
+    double a = 0.0;
+#pragma unroll
+    for (int p = 0; p < kNmfPW; ++p)
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a += num[p][kc][m] + den[p][kc][m];
+    pn[lane + 64 * wv] = a;
+    return;
+  }
   const int fl = lane & 15, tq = lane >> 4;
+  if (NMF_FOLD4) {
+    // all four partials into LDS at once (NE x 2 KB per wave), one barrier,
+    // then each wave sums a quarter of the elements in wave order (the
+    // sequential fold's association: bit-identical) and stores them
+    __shared__ double red4[4][2][NE][64];
+#pragma unroll
+    for (int p = 0; p < kNmfPW; ++p)
+#pragma unroll
+      for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int e = (p * NKC + kc) * 4 + m;
+          red4[wv][0][e][lane] = num[p][kc][m];
+          red4[wv][1][e][lane] = den[p][kc][m];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int e0 = 0; e0 < NE; e0 += 4) {
+      const int e = e0 + wv, m = e & 3, kc = (e >> 2) % NKC, p = (e >> 2) / NKC;
+      const double a = ((red4[0][0][e][lane] + red4[1][0][e][lane]) + red4[2][0][e][lane]) + red4[3][0][e][lane];
+      const double b = ((red4[0][1][e][lane] + red4[1][1][e][lane]) + red4[2][1][e][lane]) + red4[3][1][e][lane];
+      const int r = r0 + kNmfPW * (tq + 4 * m) + p, k = nmf_con_k<NKC>(kc, fl);
+      if (r < R) {
+        const size_t o = TR ? (size_t)r * K + k : (size_t)k * R + r;
+        pn[o] = a;
+        pd[o] = b;
+      }
+    }
+    return;
+  }
+  __shared__ double red[2][NE][64];
   for (int w = 0; w < 4; ++w) {
     if (wv == w) {
 #pragma unroll
@@ -160,7 +240,7 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[kNmfPW][NKC], d4 (&den)
               red[0][e][lane] = a;
               red[1][e][lane] = b;
             } else {
-              const int r = r0 + kNmfPW * (tq + 4 * m) + p, k = fl * NKC + kc;
+              const int r = r0 + kNmfPW * (tq + 4 * m) + p, k = nmf_con_k<NKC>(kc, fl);
               if (r < R) {
                 const size_t o = TR ? (size_t)r * K + k : (size_t)k * R + r;
                 pn[o] = a;
@@ -188,7 +268,7 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
   const __amdgpu_buffer_rsrc_t rW = nmf_rsrc(W), rH = nmf_rsrc(Ht);
   double wk[PW][NKS];  // bins past F: W's zero pad rows
 #pragma unroll
-  for (int p = 0; p < PW; ++p) nmf_ldv(rW, (unsigned)(((g0 + PW * fl + p) * K + tq * NKS) * 8), wk[p]);
+  for (int p = 0; p < PW; ++p) nmf_ld_hat(rW, (unsigned)(((g0 + PW * fl + p) * K + 2 * tq) * 8), wk[p]);
   d4 num[PW][NKC], den[PW][NKC];
 #pragma unroll
   for (int p = 0; p < PW; ++p)
@@ -199,19 +279,20 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
   // Frames past N read Ht's zero pad rows (hb = 0: they add nothing) and
   // SXt's pad; bins past F read the next SXt row (finite, never stored)
   double th[2][NKS], hb[2][4][NKC], sxv[2][4][PW];
-  const unsigned vo_th = (unsigned)((fl * K + tq * NKS) * 8);
-  const unsigned vo_hb = (unsigned)((tq * K + fl * NKC) * 8);
+  const unsigned vo_th = (unsigned)((fl * K + 2 * tq) * 8);
+  const unsigned vo_hb = (unsigned)((tq * K + 2 * fl) * 8);
   const unsigned vo_sx = (unsigned)((tq * F + g0 + PW * fl) * 8);
   auto load = [&](int tt, int slot) {
     const int t0 = tt * 16;
     const unsigned ho = (unsigned)(t0 * K * 8);
-    nmf_ldv(rH, vo_th + ho, th[slot]);
+    // the SX stream (HBM) first, then the L2-resident Ht tile
     const __amdgpu_buffer_rsrc_t rS = nmf_rsrc(SXt + (size_t)t0 * F);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      nmf_ldv(rH, vo_hb + ho + (unsigned)(4 * i * K * 8), hb[slot][i]);
-      nmf_ldv(rS, vo_sx + (unsigned)(4 * i * F * 8), sxv[slot][i]);
-    }
+    for (int i = 0; i < 4; ++i)
+      nmf_ld2(rS, vo_sx + (unsigned)(4 * i * F * 8), sxv[slot][i][0], sxv[slot][i][1]);
+    nmf_ld_hat(rH, vo_th + ho, th[slot]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) nmf_ld_con(rH, vo_hb + ho + (unsigned)(4 * i * K * 8), fl, hb[slot][i]);
   };
   auto compute = [&](int cs) {
     // the hat tiles of both bin tiles first, four accumulation chains each
@@ -238,8 +319,13 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double h = v[i];
+#if NMF_ABLATE == 2
+        x[i] = sxv[cs][i][p] * h;
+        y[i] = h;
+#else
         x[i] = sxv[cs][i][p] * nmf_rcp(fmax(h * h, kNmfEps));
         y[i] = nmf_rcp(fmax(h, kNmfEps));
+#endif
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -267,10 +353,11 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
     }
   };
   if (tb < te) load(tb, 0);
-  for (int tt = tb; tt < te; ++tt) {
-    load(min(tt + 1, te - 1), 1);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
+  for (int tt = tb; tt < (NMF_ABLATE == 4 ? tb : te); ++tt) {
+    if (NMF_ABLATE != 1) load(min(tt + 1, te - 1), 1);
+    if (!NMF_SPREAD) __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
     compute(0);
+    nmf_spread_loads<NKC>();
     __builtin_amdgcn_sched_barrier(0);  // the moves wait for the prefetch
     rotate();
   }
@@ -299,9 +386,9 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
   // output columns are never stored
   double bt[PW][NKS], hsv[NKS];
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) hsv[s] = hs ? hs[tq * NKS + s] : 1.0;
+  for (int s = 0; s < NKS; ++s) hsv[s] = hs ? hs[nmf_hat_k(s, tq)] : 1.0;
 #pragma unroll
-  for (int p = 0; p < PW; ++p) nmf_ldv(rH, (unsigned)(((t0g + PW * fl + p) * K + tq * NKS) * 8), bt[p]);
+  for (int p = 0; p < PW; ++p) nmf_ld_hat(rH, (unsigned)(((t0g + PW * fl + p) * K + 2 * tq) * 8), bt[p]);
 #pragma unroll
   for (int p = 0; p < PW; ++p)
 #pragma unroll
@@ -316,19 +403,19 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
   // bins past F read W's zero pad rows (bw = 0: they add nothing) and SX's
   // pad or the next SX row
   double ao[2][NKS], bw[2][4][NKC], sxv[2][4][PW];
-  const unsigned vo_ao = (unsigned)((fl * K + tq * NKS) * 8);
-  const unsigned vo_bw = (unsigned)((tq * K + fl * NKC) * 8);
+  const unsigned vo_ao = (unsigned)((fl * K + 2 * tq) * 8);
+  const unsigned vo_bw = (unsigned)((tq * K + 2 * fl) * 8);
   const unsigned vo_sx = (unsigned)((tq * N + t0g + PW * fl) * 8);
   auto load = [&](int ft, int slot) {
     const int f0 = ft * 16;
     const unsigned wo = (unsigned)(f0 * K * 8);
-    nmf_ldv(rW, vo_ao + wo, ao[slot]);
     const __amdgpu_buffer_rsrc_t rS = nmf_rsrc(SX + (size_t)f0 * N);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      nmf_ldv(rW, vo_bw + wo + (unsigned)(4 * i * K * 8), bw[slot][i]);
-      nmf_ldv(rS, vo_sx + (unsigned)(4 * i * N * 8), sxv[slot][i]);
-    }
+    for (int i = 0; i < 4; ++i)
+      nmf_ld2(rS, vo_sx + (unsigned)(4 * i * N * 8), sxv[slot][i][0], sxv[slot][i][1]);
+    nmf_ld_hat(rW, vo_ao + wo, ao[slot]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) nmf_ld_con(rW, vo_bw + wo + (unsigned)(4 * i * K * 8), fl, bw[slot][i]);
   };
   auto compute = [&](int cs) {
     d4 hv[PW];  // as k_nmf_wnum: both hat tiles first, four chains each
@@ -351,8 +438,13 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double h = v[i];
+#if NMF_ABLATE == 2
+        x[i] = sxv[cs][i][p] * h;
+        y[i] = h;
+#else
         x[i] = sxv[cs][i][p] * nmf_rcp(fmax(h * h, kNmfEps));
         y[i] = nmf_rcp(fmax(h, kNmfEps));
+#endif
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -375,10 +467,11 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
     }
   };
   if (fb < fe) load(fb, 0);
-  for (int ft = fb; ft < fe; ++ft) {
-    load(min(ft + 1, fe - 1), 1);
-    __builtin_amdgcn_sched_barrier(0);
+  for (int ft = fb; ft < (NMF_ABLATE == 4 ? fb : fe); ++ft) {
+    if (NMF_ABLATE != 1) load(min(ft + 1, fe - 1), 1);
+    if (!NMF_SPREAD) __builtin_amdgcn_sched_barrier(0);
     compute(0);
+    nmf_spread_loads<NKC>();
     __builtin_amdgcn_sched_barrier(0);  // the moves wait for the prefetch
     rotate();
   }
