@@ -9,6 +9,12 @@
 //   hat = W H; X, Y as above
 //   num = W^T X, den = W^T Y       (one GEMM launch, shared W operand)
 //   H *= num/max(den, eps)
+// (the unfused GEMM path below).  The fused path (K % 16 == 0, K <= 64) runs
+// an iteration in four launches: k_nmf_wnum (hat, ratios and the W
+// contraction in registers), k_nmf_w_upd (W *= num / max(den, eps) and
+// partial column sums), k_nmf_hnum (the H contraction on the un-renormalised
+// W: the column scale cancels in the model), k_nmf_h_part (H *= s num /
+// max(den, eps), W /= s).
 #include "fasst_gemm.h"
 #include "fasst_fft.h"
 
@@ -156,6 +162,9 @@ __device__ __forceinline__ constexpr int nmf_con_k(int kc, int fl) {
 #endif
 #ifndef NMF_FOLD4
 #define NMF_FOLD4 1
+#endif
+#ifndef NMF_PAIR
+#define NMF_PAIR 1
 #endif
 // interleave a tile's prefetch (NL 16-byte loads) with the first MFMAs of
 // the tile in flight, one load per two MFMAs: issued all at once, the four
@@ -353,6 +362,24 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
     }
   };
   if (tb < te) load(tb, 0);
+#if NMF_PAIR
+  // two tiles per trip, slots alternating (no register moves); every load
+  // is consumed on every path out of its trip, so none is sunk or waited
+  // for early
+  int tt = tb;
+  for (; tt + 1 < te; tt += 2) {
+    load(tt + 1, 1);
+    compute(0);
+    nmf_spread_loads<NKC>();
+    __builtin_amdgcn_sched_barrier(0);
+    load(min(tt + 2, te - 1), 0);
+    compute(1);
+    nmf_spread_loads<NKC>();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (tt < te) compute(0);
+  if (false)
+#endif
   for (int tt = tb; tt < (NMF_ABLATE == 4 ? tb : te); ++tt) {
     if (NMF_ABLATE != 1) load(min(tt + 1, te - 1), 1);
     if (!NMF_SPREAD) __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
@@ -467,6 +494,24 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
     }
   };
   if (fb < fe) load(fb, 0);
+#if NMF_PAIR
+  // two tiles per trip, slots alternating (no register moves); every load
+  // is consumed on every path out of its trip, so none is sunk or waited
+  // for early
+  int ft = fb;
+  for (; ft + 1 < fe; ft += 2) {
+    load(ft + 1, 1);
+    compute(0);
+    nmf_spread_loads<NKC>();
+    __builtin_amdgcn_sched_barrier(0);
+    load(min(ft + 2, fe - 1), 0);
+    compute(1);
+    nmf_spread_loads<NKC>();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (ft < fe) compute(0);
+  if (false)
+#endif
   for (int ft = fb; ft < (NMF_ABLATE == 4 ? fb : fe); ++ft) {
     if (NMF_ABLATE != 1) load(min(ft + 1, fe - 1), 1);
     if (!NMF_SPREAD) __builtin_amdgcn_sched_barrier(0);
@@ -480,17 +525,21 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
   nmf_fold_store<NKC, true>(num, den, pn, pn + slab, t0g, N, wv, lane);
 }
 
-// k_nmf_w over the fused path's group partials ([g][num / den][K][F])
-__global__ __launch_bounds__(1024) void k_nmf_w_part(double *__restrict__ W,
-                                                    const double *__restrict__ part, int ng,
-                                                    double *__restrict__ s_out, int F, int K) {
-  // 1024 threads: one or two bins each, the ng group partials of a bin
-  // loaded 8 at a time (a per-group loop was a chain of global round trips)
-  __shared__ double s_red[1024];
-  const int k = blockIdx.x;
+// k_nmf_w over the fused path's group partials ([g][num / den][K][F]), in
+// two launches so that the update spreads over K x kNmfWS workgroups: the
+// multiplicative update of a bin range with its partial column sum, then the
+// renormalisation by the summed columns
+constexpr int kNmfWS = 4;
+__global__ __launch_bounds__(256) void k_nmf_w_upd(double *__restrict__ W,
+                                                   const double *__restrict__ part, int ng,
+                                                   double *__restrict__ wsum, int F, int K) {
+  __shared__ double s_red[256];
+  const int k = blockIdx.x, fs = blockIdx.y;
   const size_t slab = (size_t)K * F;
   double acc = 0.0;
-  for (int f = threadIdx.x; f < F; f += blockDim.x) {
+  for (int f = fs * 256 + threadIdx.x; f < F; f += kNmfWS * 256) {
+    // the ng group partials of a bin loaded 8 at a time (a per-group loop
+    // was a chain of global round trips)
     const double *q = part + (size_t)k * F + f;
     double n = 0.0, d = 0.0;
     for (int g = 0; g < ng; g += 8) {
@@ -512,39 +561,75 @@ __global__ __launch_bounds__(1024) void k_nmf_w_part(double *__restrict__ W,
   }
   s_red[threadIdx.x] = acc;
   __syncthreads();
-  for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+  for (int w = 128; w > 0; w >>= 1) {
     if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
     __syncthreads();
   }
-  double s = s_red[0];
-  if (s == 0) s = 1.0;  // sumW[sumW==0] = 1. (nmf.py:46)
-  for (int f = threadIdx.x; f < F; f += blockDim.x) W[(size_t)f * K + k] /= s;
-  if (threadIdx.x == 0) s_out[k] = s;
+  if (threadIdx.x == 0) wsum[k * kNmfWS + fs] = s_red[0];
 }
 
-// k_nmf_hscale + k_nmf_h on the frame-major Ht over the group partials
-// ([g][num / den][N][K])
+// column sum of the updated W from its kNmfWS partials (nmf.py:45-46:
+// sumW[sumW==0] = 1)
+__device__ __forceinline__ double nmf_colsum(const double *__restrict__ wsum, int k) {
+  double s = 0.0;
+#pragma unroll
+  for (int u = 0; u < kNmfWS; ++u) s += wsum[k * kNmfWS + u];
+  return s == 0 ? 1.0 : s;
+}
+
+// The H update's tail over the group partials ([g][num / den][N][K]) on the
+// frame-major Ht, and the W update's renormalisation (nmf.py:45-48), which
+// the fused path defers to here: k_nmf_hnum forms hat = W' H from the not
+// yet renormalised W' and the not yet rescaled H (the same model: the
+// column scale s cancels in W' H = (W' / s)(s H)), so its numerator and
+// denominator both carry the factor s and their ratio is the reference's.
+// Then Ht = (Ht s) num / max(den, eps) and W = W' / s, s_out = s.  wsum is
+// null when W is frozen (no rescale).
 __global__ void k_nmf_h_part(double *__restrict__ Ht, const double *__restrict__ part, int ng,
-                             const double *__restrict__ hs, int K, int N) {
+                             const double *__restrict__ wsum, double *__restrict__ W,
+                             double *__restrict__ s_out, int F, int K, int N) {
   const size_t slab = (size_t)K * N;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slab;
        i += (size_t)gridDim.x * blockDim.x) {
-    double n = part[i], d = part[slab + i];
-    for (int g = 1; g < ng; ++g) {
-      n += part[(size_t)g * 2 * slab + i];
-      d += part[(size_t)g * 2 * slab + slab + i];
+    double n = 0.0, d = 0.0;
+    for (int g = 0; g < ng; g += 8) {  // 8 groups' loads in flight at once
+      double vn[8], vd[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        vn[u] = g + u < ng ? part[(size_t)(g + u) * 2 * slab + i] : 0.0;
+        vd[u] = g + u < ng ? part[(size_t)(g + u) * 2 * slab + slab + i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        n += vn[u];
+        d += vd[u];
+      }
     }
-    const double h = hs ? Ht[i] * hs[i % K] : Ht[i];
+    const double h = wsum ? Ht[i] * nmf_colsum(wsum, (int)(i % K)) : Ht[i];
     Ht[i] = h * (n / fmax(d, kNmfEps));
   }
+  if (wsum)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)F * K;
+         i += (size_t)gridDim.x * blockDim.x) {
+      const double sk = nmf_colsum(wsum, (int)(i % K));
+      W[i] /= sk;
+      if (i < (size_t)K) s_out[i] = sk;
+    }
 }
 
-// Ht *= s per component (the W update's renormalisation when H is frozen)
-__global__ void k_nmf_hscale_t(double *__restrict__ Ht, const double *__restrict__ s, int K,
+// the W update's renormalisation when H is frozen: Ht *= s, W /= s
+__global__ void k_nmf_hscale_t(double *__restrict__ Ht, const double *__restrict__ wsum,
+                               double *__restrict__ W, double *__restrict__ s_out, int F, int K,
                                int N) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)K * N;
        i += (size_t)gridDim.x * blockDim.x)
-    Ht[i] *= s[i % K];
+    Ht[i] *= nmf_colsum(wsum, (int)(i % K));
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)F * K;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const double sk = nmf_colsum(wsum, (int)(i % K));
+    W[i] /= sk;
+    if (i < (size_t)K) s_out[i] = sk;
+  }
 }
 
 // out[c][r] = in[r][c] for an R x C matrix (row-major), 16 x 16 LDS tiles
@@ -709,7 +794,7 @@ struct nmf_ctx {
   // fused path (K % 16 == 0, K <= 64): transposed copies and chunk partials
   // (H lives frame-major in Ht there; H is its staging copy for set / get)
   int fused = 0, ng_w = 1, tpc_w = 1, ng_h = 1, fpc_h = 1;
-  DBuf<double> SXt, Ht, part;
+  DBuf<double> SXt, Ht, part, wsum;
 };
 
 namespace {
@@ -736,16 +821,20 @@ static void nmf_fused(nmf_ctx *c, int update_w, int update_h) {
   if (update_w) {
     k_nmf_wnum<NKC><<<dim3(gw, c->ng_w), 256, 0, c->stream>>>(c->W.p, c->Ht.p, c->SXt.p, c->part.p,
                                                               F, N, c->tpc_w);
-    k_nmf_w_part<<<K, 1024, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->s.p, F, K);
+    k_nmf_w_upd<<<dim3(K, kNmfWS), 256, 0, c->stream>>>(c->W.p, c->part.p, c->ng_w, c->wsum.p, F,
+                                                       K);
   }
-  const double *hs = update_w ? c->s.p : nullptr;
+  // the W update leaves W un-renormalised and H un-rescaled: the H update
+  // (or k_nmf_hscale_t) applies both (k_nmf_h_part)
+  const double *ws = update_w ? c->wsum.p : nullptr;
+  const int eg = egrid_n((size_t)K * std::max(N, F));
   if (update_h) {
-    k_nmf_hnum<NKC><<<dim3(gh, c->ng_h), 256, 0, c->stream>>>(c->W.p, c->Ht.p, hs, c->SX.p,
+    k_nmf_hnum<NKC><<<dim3(gh, c->ng_h), 256, 0, c->stream>>>(c->W.p, c->Ht.p, nullptr, c->SX.p,
                                                               c->part.p, F, N, c->fpc_h);
-    k_nmf_h_part<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->Ht.p, c->part.p, c->ng_h, hs,
-                                                                K, N);
+    k_nmf_h_part<<<eg, 256, 0, c->stream>>>(c->Ht.p, c->part.p, c->ng_h, ws, c->W.p, c->s.p, F, K,
+                                            N);
   } else if (update_w) {
-    k_nmf_hscale_t<<<egrid_n((size_t)K * N), 256, 0, c->stream>>>(c->Ht.p, c->s.p, K, N);
+    k_nmf_hscale_t<<<eg, 256, 0, c->stream>>>(c->Ht.p, ws, c->W.p, c->s.p, F, K, N);
   }
 }
 
@@ -844,6 +933,7 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
     if (!st) st = c->SXt.alloc((size_t)(N + 16) * F + 64);
     if (!st) st = c->Ht.alloc((size_t)(N + 32) * K);
     if (!st) st = c->part.alloc(np);
+    if (!st) st = c->wsum.alloc((size_t)K * kNmfWS);
   }
   if (st) {
     nmf_destroy(c);
