@@ -2,7 +2,7 @@
 # NMF fused-kernel geometry sweep (timing only): per-kernel averages per (build, FASST_NMF_WAVES)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-for cfg in abl3:1024 abl4:1024 abl3:512 abl4:512; do
+for cfg in pair:1024 abl5:1024; do
   lib=${cfg%%:*}; wv=${cfg##*:}; d=gpurun_out/sweep_${lib}_$wv
   mkdir -p $d
   FASST_NMF_WAVES=$wv FASST_HIP_LIB=$PWD/build/ab/$lib.so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
