@@ -1276,6 +1276,9 @@ struct BArgs {
 #ifndef FB_REVERSE
 #define FB_REVERSE 0
 #endif
+#ifndef FB_RAWBUF
+#define FB_RAWBUF 1
+#endif
 template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
@@ -1313,6 +1316,24 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       // per load instruction instead of 4 x 16
       const int fp = ft0 * 16 + FPW * fl;
       double r[FPW][4];
+#if FB_RAWBUF
+      // raw-buffer loads off the tile's (wave-uniform) row base: frames past
+      // T / bins past Fp take an offset outside the resource and read 0, so
+      // the loads carry no exec branches
+      const __amdgpu_buffer_rsrc_t rr = es_rsrc(rhoj + (size_t)t0 * a.Fp);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = t0 + tq + 4 * i < a.T && fp < a.Fp;
+        const unsigned vo = ok ? (unsigned)(((tq + 4 * i) * a.Fp + fp) * 8) : 0x80000000u;
+#pragma unroll
+        for (int h = 0; h < FPW; h += 2) {
+          typedef unsigned u4 __attribute__((ext_vector_type(4)));
+          const u4 x = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(vo + 8u * h), 0, 0);
+          r[h][i] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 0, 1));
+          r[h + 1][i] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 2, 3));
+        }
+      }
+#else
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool ok = t0 + tq + 4 * i < a.T && fp < a.Fp;
@@ -1324,6 +1345,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
           r[h + 1][i] = v.y;
         }
       }
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
