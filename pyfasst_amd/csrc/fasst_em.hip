@@ -1277,7 +1277,7 @@ struct BArgs {
 #define FB_REVERSE 0
 #endif
 #ifndef FB_RAWBUF
-#define FB_RAWBUF 1
+#define FB_RAWBUF 0
 #endif
 template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
