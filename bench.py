@@ -4,17 +4,19 @@ Workload (BASELINE.json configs[2] / [3]): synthetic stereo STFT-domain clip,
 F=2049 bins x T=10000 frames, J=4 convolutive sources of spatial rank 2,
 K=32 NMF components (MultiChanNMFConv + makeItConvolutive).  One clip per
 GPU (config 4 = 8 independent clips): weak scaling, no collective in the
-data path; torch.distributed only provides the start/stop barrier and the
-max-over-ranks time, on the gloo backend (host-side, nothing on the GPUs)
-unless FASST_BENCH_BACKEND=nccl selects RCCL: measured on one MI355X, an
-RCCL process group alone costs the timed GEM loop ~2.5% (925-930 vs 945-949
-EM it/s at one rank, profiles/r3_dist_backend.txt), and the path has no
-exchange step that would need it.
+data path; torch.distributed (RCCL when every rank has its own GPU, gloo
+when ranks share one) provides the start/stop barrier, the max-over-ranks
+time and the final allgather of the per-clip logliks / times.
+
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts the
+N ranks itself (launch_local: one worker process per GPU, started before
+anything in the parent touches a GPU); under torchrun WORLD_SIZE must equal
+N.
 
 A "step" is one GEM iteration (audioModel.py:384-428) on the GPU, inputs
 resident in HBM.  Prints ONE JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--dry-run]
 """
 import argparse
 import json
@@ -147,14 +149,69 @@ def cpu_baseline(T_sample=T_FRAMES):
     return out
 
 
-def rank_setup(env=None):
+def rank_setup(env=None, ndev=None):
     """(world, rank, local_rank, data_seed, device) of this process: one clip per
-    GPU, data seed = global rank, device = local rank (torchrun env vars)."""
+    GPU, data seed = global rank, device = local rank (torchrun env vars).  With
+    fewer visible GPUs than local ranks (the one-GPU rehearsal box) the ranks
+    share the cards round-robin."""
     env = os.environ if env is None else env
     world = int(env.get("WORLD_SIZE", "1"))
     rank = int(env.get("RANK", "0"))
     local = int(env.get("LOCAL_RANK", "0"))
-    return world, rank, local, rank, local
+    device = local if not ndev else local % ndev
+    return world, rank, local, rank, device
+
+
+def choose_backend(world, ndev, env=None):
+    """Control-plane backend: RCCL ('nccl') when every rank has a GPU of its
+    own, as north_star names it; gloo when ranks share a card (RCCL refuses two
+    ranks on one device).  FASST_BENCH_BACKEND overrides; forcing nccl onto
+    shared cards is refused."""
+    env = os.environ if env is None else env
+    forced = env.get("FASST_BENCH_BACKEND")
+    if forced:
+        if forced == "nccl" and ndev < world:
+            raise SystemExit("bench.py: FASST_BENCH_BACKEND=nccl needs one GPU per rank "
+                             "(%d ranks, %d GPUs)" % (world, ndev))
+        return forced
+    return "nccl" if ndev >= world else "gloo"
+
+
+def launch_local(n, argv, env=None):
+    """`python bench.py --gpus N` without a launcher: start N worker processes
+    of this script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, a
+    rendezvous on 127.0.0.1), before anything in this process touches a GPU;
+    rank 0's stdout (the JSON line) passes through.  A failing worker stops
+    the others (by their own handles).  Returns the job's exit code."""
+    import signal
+    import socket
+    import subprocess
+    env = dict(os.environ if env is None else env)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        e = dict(env, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=e, stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
 
 
 def max_over_ranks(dt, dist=None, device="cpu"):
@@ -167,12 +224,63 @@ def max_over_ranks(dt, dist=None, device="cpu"):
     return float(t.item())
 
 
+def gather_clips(rec, dist=None, device="cpu"):
+    """SURVEY.md §8(e)1's final allgather: every rank's (rank, data seed,
+    device, last loglik, own timed seconds) -> list over ranks."""
+    if dist is None:
+        return [list(rec)]
+    import torch
+    t = torch.tensor(rec, dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
+def check_clips(clips):
+    """Distinct ranks must have run distinct clips (distinct data seeds and
+    logliks); raises otherwise."""
+    ranks = [int(c[0]) for c in clips]
+    seeds = [int(c[1]) for c in clips]
+    lls = [c[3] for c in clips]
+    if sorted(ranks) != list(range(len(clips))):
+        raise RuntimeError("clip records from ranks %s" % ranks)
+    if len(set(seeds)) != len(seeds) or len(set(lls)) != len(lls):
+        raise RuntimeError("ranks did not run distinct clips: seeds %s, logliks %s" % (seeds, lls))
+
+
+def dry_run(args, world, rank, seed):
+    """--dry-run: the multi-rank control plane of main() on the CPU (gloo),
+    around a host stand-in for one clip (the mean log power of a small
+    synthetic mixture drawn from the rank's data seed); rank 0 prints the
+    JSON line."""
+    import torch.distributed as dist
+    from pyfasst_amd import synthetic
+    dist.init_process_group("gloo")
+    dist.barrier()
+    t0 = time.perf_counter()
+    X = synthetic.stereo_mixture(65, 32 * max(args.steps, 1), J=2, K_true=2, rank=2, seed=seed)
+    ll = float(np.mean(np.log(np.abs(X) ** 2 + 1e-300)))
+    dist.barrier()
+    dt_own = time.perf_counter() - t0
+    dt = max_over_ranks(dt_own, dist, "cpu")
+    clips = gather_clips([rank, seed, -1, ll, dt_own], dist, "cpu")
+    check_clips(clips)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (control plane only)", "value": job_value(world, args.steps, dt),
+                          "n_gpus": world, "steps": args.steps, "control_plane": "gloo",
+                          "ms_per_step": dt / max(args.steps, 1) * 1e3,
+                          "clips": [{"rank": int(c[0]), "data_seed": int(c[1]), "loglik": c[3]}
+                                    for c in clips]}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
 def job_value(world, steps, dt_max):
     """Whole-job throughput: iterations of all clips / slowest rank's time."""
     return world * steps / dt_max
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -188,23 +296,43 @@ def main():
     ap.add_argument("--K", type=int, default=K_NMF)
     ap.add_argument("--cpu-T", type=int, default=T_FRAMES,
                     help="frames of the CPU-baseline sample (default: the full T)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control plane only, on the CPU: launcher, gloo barrier, max-over-ranks "
+                         "and the clips' allgather around a tiny host stand-in for the clip "
+                         "(tests/test_distributed.py); no GPU is touched")
+    args = ap.parse_args(argv)
 
-    world, rank, local, seed, device = rank_setup()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: this process only starts the ranks (no GPU call here)
+        return launch_local(args.gpus, sys.argv[1:] if argv is None else argv)
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.stderr.write("bench.py: WORLD_SIZE=%s but --gpus %d\n" % (env_world, args.gpus))
+        return 2
+
+    import torch
+    ndev = 0 if args.dry_run else torch.cuda.device_count()   # does not initialise the GPU
+    world, rank, local, seed, device = rank_setup(ndev=ndev)
+    if args.dry_run:
+        return dry_run(args, world, rank, seed)
     dist = None
-    # control plane only (barrier + max): gloo by default, RCCL with
-    # FASST_BENCH_BACKEND=nccl (rank r on GPU LOCAL_RANK either way; with gloo
-    # more ranks than GPUs share the cards round-robin)
-    backend = os.environ.get("FASST_BENCH_BACKEND", "gloo")
+    backend = None
+    # control plane only (start/stop barrier, max-over-ranks time, the clips'
+    # allgather): RCCL when each rank has its own GPU (choose_backend).
     # FASST_BENCH_DIST=1 initialises the process group even for one rank (the
     # barrier / max-over-ranks path exercised on a one-GPU box)
     if world > 1 or os.environ.get("FASST_BENCH_DIST") == "1":
-        import torch
         import torch.distributed as dist
-        if backend != "nccl":
-            device = local % max(1, torch.cuda.device_count())
+        backend = choose_backend(world, ndev)
         torch.cuda.set_device(device)
-        dist.init_process_group(backend)
+        if backend == "nccl":
+            # eager communicator (device_id), then one barrier: RCCL's setup
+            # finishes before the engine exists and long before the timed loop
+            dist.init_process_group(backend, device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+        dist.barrier()
+    coll_dev = "cuda:%d" % device if backend == "nccl" else "cpu"
 
     m = build_model(seed=seed, device=device, T=args.T, J=args.J, K=args.K)
     eng = m._engine
@@ -214,15 +342,19 @@ def main():
 
     def run_rows(rows):
         """GEM iterations over the PSD rows; a random TW restart (host RNG)
-        is performed and the run resumed, as the product does"""
-        done = 0
+        is performed and the run resumed, as the product does.  Returns the
+        last iteration's loglik."""
+        done, last = 0, float("nan")
         while done < len(rows):
-            _, n, mask = eng.run(rows[done:], m.nmfUpdateCoeff)
+            ll, n, mask = eng.run(rows[done:], m.nmfUpdateCoeff)
             done += n
+            if n:
+                last = float(ll[n - 1])
             if mask:
                 m._download(*state["upl"])
                 m._restart_tw(mask, state["upl"][0])
                 state["upl"] = m._upload()
+        return last
 
     # clock ramp: the first ~20 iterations of a process run while the GPU
     # clock rises (tools/ramp_probe.py); iterate untimed until it has settled,
@@ -245,10 +377,13 @@ def main():
     rows = psd_schedule(m, args.steps)
     barrier_sync()
     t0 = time.perf_counter()
-    run_rows(rows)
+    ll_last = run_rows(rows)
     barrier_sync()
-    dt = max_over_ranks(time.perf_counter() - t0, dist,
-                        "cuda:%d" % device if backend == "nccl" else "cpu")
+    dt_own = time.perf_counter() - t0
+    dt = max_over_ranks(dt_own, dist, coll_dev)
+    clips = gather_clips([rank, seed, device, ll_last, dt_own], dist, coll_dev)
+    if world > 1:
+        check_clips(clips)
 
     # per-kernel HIP-event timing on the engine's stream (separate, untimed pass)
     eng.set_profiling(True)
@@ -339,6 +474,9 @@ def main():
                                    "K=%d, one clip per GPU" % (m.nbFreqsSigRepr, m.nbFramesSigRepr,
                                                               args.J, RANK, args.K),
                        "parallelism": "clip-per-GPU x%d" % world},
+            "control_plane": backend or "none (one process)",
+            "clips": [{"rank": int(c[0]), "data_seed": int(c[1]), "device": int(c[2]),
+                       "loglik": c[3], "timed_s": round(c[4], 6)} for c in clips],
             "roofline": rl,
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(times.items())},
         }
@@ -347,7 +485,8 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -126,16 +126,7 @@ class SeparateLeadProcess(object):
         if inputAudioFilename[-4:] != ".wav":
             raise ValueError("File not WAV file? Only WAV format support, for now...")
         # output files (:352-373)
-        self.files['outputDirSuffix'] = outputDirSuffix
-        self.files['outputDir'] = ('/'.join(self.files['inputAudioFilename'].split('/')[:-1]) +
-                                   '/' + self.files['outputDirSuffix'] + '/')
-        if not os.path.isdir(self.files['outputDir']):
-            os.mkdir(self.files['outputDir'])
-        self.files['pathBaseName'] = (self.files['outputDir'] +
-                                      self.files['inputAudioFilename'].split('/')[-1][:-4])
-        self.files['mus_output_file'] = str(self.files['pathBaseName'] + '_acc.wav')
-        self.files['voc_output_file'] = str(self.files['pathBaseName'] + '_lead.wav')
-        self.files['pitch_output_file'] = str(self.files['pathBaseName'] + '_pitches.txt')
+        self._output_files(outputDirSuffix)
         # data scaling (:392-410)
         self.fs, data = wav.read(self.files['inputAudioFilename'])
         self.scaleData = 1.2 * np.abs(data).max()
@@ -184,6 +175,28 @@ class SeparateLeadProcess(object):
         self.freeMemory = freeMemory
 
     # ---------------------------------------------------------------- setup
+    def _output_files(self, outputDirSuffix):
+        """Output directory <input dir>/<suffix>/ and the lead / accompaniment
+        / pitch file names (:352-373, :551-570)."""
+        import os
+        self.files['outputDirSuffix'] = outputDirSuffix
+        self.files['outputDir'] = ('/'.join(self.files['inputAudioFilename'].split('/')[:-1]) +
+                                   '/' + self.files['outputDirSuffix'] + '/')
+        if not os.path.isdir(self.files['outputDir']):
+            os.mkdir(self.files['outputDir'])
+        self.files['pathBaseName'] = (self.files['outputDir'] +
+                                      self.files['inputAudioFilename'].split('/')[-1][:-4])
+        self.files['mus_output_file'] = str(self.files['pathBaseName'] + '_acc.wav')
+        self.files['voc_output_file'] = str(self.files['pathBaseName'] + '_lead.wav')
+        self.files['pitch_output_file'] = str(self.files['pathBaseName'] + '_pitches.txt')
+
+    def setOutputFileNames(self, outputDirSuffix):
+        """Redefine where the output files are written, e.g. between the first
+        estimation and the re-estimation of the parameters (:540-585)."""
+        if self.verbose:
+            print("Redefining the Output Filenames !")
+        self._output_files(outputDirSuffix)
+
     def computeWF0(self):
         """Source dictionary on the GPU and the transform object
         (SeparateLeadStereoTF.py:587-700, the transform-registry branch
@@ -353,6 +366,82 @@ class SeparateLeadProcess(object):
                 P['HF0'][:, start:stop] = np.copy(HF0[:, startincqt:startincqt + stop - start])
             del SX
 
+    def estimSIMMParams(self, R=1):
+        """Mono SIMM on the mean of the channels over the whole excerpt
+        (:919-957); the parameters go to SIMMParams."""
+        from .SIMM import SIMM
+        P = self.SIMMParams
+        SX = self.computeMonoX()
+        HGAMMA, HPHI, HF0, HM, WM, recoError1 = SIMM.SIMM(
+            SX, WF0=P['WF0'], WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
+            numberOfAccompanimentSpectralShapes=R, HGAMMA0=None, HPHI0=None, HF00=None,
+            WM0=None, HM0=None, numberOfIterations=P['niter'], updateRulePower=1.,
+            stepNotes=P['stepNotes'], lambdaHF0=0.0 / (1.0 * SX.max()), alphaHF0=0.9,
+            verbose=self.verbose, F0Table=P['F0Table'], chirpPerF0=P['chirpPerF0'],
+            device=self.device)
+        P['HGAMMA'], P['HPHI'], P['HF0'], P['HM'], P['WM'] = HGAMMA, HPHI, HF0, HM, WM
+        del SX
+
+    def _store_stereo(self, res, hf0_key='HF0'):
+        """SIMMParams from a Stereo_SIMM result tuple (SIMM.py:943 order)."""
+        P = self.SIMMParams
+        (P['alphaR'], P['alphaL'], P['HGAMMA'], P['HPHI'], P[hf0_key], P['betaR'], P['betaL'],
+         P['HM'], P['WM'], _) = res
+
+    def estimStereoSIMMParams(self):
+        """Stereo SIMM over the whole excerpt from HF00 (:1677-1713); note the
+        power spectrograms here are |X|^2 without the 1e-8 floor of the
+        chunked path, as in the reference."""
+        from .SIMM import SIMM
+        P = self.SIMMParams
+        self.computeStereoX()
+        SXR = np.abs(self.XR) ** 2
+        SXL = np.abs(self.XL) ** 2
+        self._store_stereo(SIMM.Stereo_SIMM(
+            SXR, SXL, WF0=P['WF0'], WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
+            numberOfAccompanimentSpectralShapes=P['R'], HGAMMA0=None, HPHI0=None,
+            HF00=P['HF00'], WM0=None, HM0=None, numberOfIterations=P['niter'],
+            updateRulePower=1.0, stepNotes=P['stepNotes'], lambdaHF0=0.0 / (1.0 * SXR.max()),
+            alphaHF0=0.9, verbose=self.verbose, displayEvolution=False, device=self.device))
+        del SXR, SXL
+
+    @staticmethod
+    def _unvoiced_basis(WF0):
+        """WUF0: the source dictionary with a flat (all-ones) unvoiced atom
+        appended (:1594-1596, :1720-1721)."""
+        return np.hstack([WF0, np.ones([WF0.shape[0], 1])])
+
+    def estimStereoSUIMMParams(self):
+        """Stereo SIMM with the unvoiced atom (:1715-1760): WUF0 = [WF0 | 1],
+        HUF0 = [HF0 ; 1], HGAMMA and HPHI from the voiced estimate, HGAMMA
+        held fixed (updateHGAMMA=False).  Reads the XR / XL of the previous
+        estimStereoSIMMParams, as the reference does."""
+        from .SIMM import SIMM
+        P = self.SIMMParams
+        SXR = np.abs(self.XR) ** 2
+        SXL = np.abs(self.XL) ** 2
+        WUF0 = self._unvoiced_basis(P['WF0'])
+        HUF0 = np.vstack([P['HF0'], np.ones([1, P['HF0'].shape[1]])])
+        self._store_stereo(SIMM.Stereo_SIMM(
+            SXR, SXL, WUF0, WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
+            numberOfAccompanimentSpectralShapes=P['R'], HGAMMA0=P['HGAMMA'], HPHI0=P['HPHI'],
+            HF00=HUF0, WM0=None, HM0=None, numberOfIterations=P['niter'], updateRulePower=1.0,
+            stepNotes=P['stepNotes'], lambdaHF0=0.0 / (1.0 * SXR.max()), alphaHF0=0.9,
+            verbose=self.verbose, displayEvolution=False, updateHGAMMA=False,
+            device=self.device), hf0_key='HUF0')
+        P['WUF0'] = WUF0
+
+    def automaticMelodyAndSeparation(self):
+        """(:1130-1140) The reference disables this un-chunked sequence: its
+        `raise warnings.warn(...)` emits the warning and then raises (the
+        warning call returns None), so nothing after it runs.  Kept with that
+        behaviour; the steps (runViterbi, initiateHF0WithIndexBestPath,
+        estimStereoSIMMParams, writeSeparatedSignals, estimStereoSUIMMParams,
+        writeSeparatedSignalsWithUnvoice) are callable one by one."""
+        import warnings
+        warnings.warn("This function does not work well with framed estimation.")
+        raise TypeError("exceptions must derive from BaseException")
+
     def initiateHF0WithIndexBestPath(self):
         """HF00: the melody's neighbourhood set to max HF0 (:1321-1368)."""
         NF0 = self.SIMMParams['NF0']
@@ -413,6 +502,44 @@ class SeparateLeadProcess(object):
                 for key in ('HM', 'HF0', 'HPHI', 'alphaR', 'alphaL', 'betaR', 'betaL'):
                     del P[key]
         self.overlapAddChunks(nChunks=nChunks, suffixIsSUIMM='.wav')
+
+    def estimStereoSUIMMParamsWriteSeps(self, maxFrames=1000):
+        """estimStereoSIMMParamsWriteSeps with the unvoiced atom (:1585-1675):
+        per chunk, stereo SIMM on WUF0 = [WF0 | 1] from HUF0 = [HF00 chunk ;
+        1] with the current HGAMMA held fixed, the chunk's '_VUIMM'
+        separation, then the overlap-add into <lead|acc>_VUIMM.wav."""
+        from .SIMM import SIMM
+        totFrames, nChunks, maxFrames = self.checkChunkSize(maxFrames)
+        P = self.SIMMParams
+        WUF0 = self._unvoiced_basis(P['WF0'])
+        P['WUF0'] = WUF0
+        for n in range(nChunks):
+            start = n * maxFrames
+            stop = np.minimum((n + 1) * maxFrames, totFrames)
+            SXR, SXL = self.computeStereoSX(start=start, stop=stop)
+            HUF0 = np.zeros([P['NF0'] * P['chirpPerF0'] + 1, SXR.shape[1]])
+            if self.tfrepresentation == 'stft':
+                startinHF00, stopinHF00 = 0, stop - start
+            else:                                            # :1610-1612
+                startinHF00 = np.sort(np.where(self.mqt.time_stamps > 0)[0])[0]
+                stopinHF00 = startinHF00 + stop - start
+            HUF0[:-1, startinHF00:stopinHF00] = P['HF00'][:, start:stop]
+            HUF0[-1] = 1
+            self._store_stereo(SIMM.Stereo_SIMM(
+                SXR, SXL, WUF0, WGAMMA=P['WGAMMA'], numberOfFilters=P['K'],
+                numberOfAccompanimentSpectralShapes=P['R'], HGAMMA0=P['HGAMMA'], HPHI0=None,
+                HF00=HUF0, WM0=None, HM0=None, numberOfIterations=P['niter'],
+                updateRulePower=1.0, stepNotes=P['stepNotes'],
+                lambdaHF0=0.0 / (1.0 * SXR.max()), alphaHF0=0.9, verbose=self.verbose,
+                displayEvolution=False, updateHGAMMA=False, device=self.device),
+                hf0_key='HUF0')
+            del SXR, SXL, HUF0
+            self.computeStereoX(start=start, stop=stop)
+            self.writeSeparatedSignals(suffix='%05d_VUIMM.wav' % n)
+            del self.XR, self.XL
+            for key in ('HM', 'HUF0', 'HPHI', 'alphaR', 'alphaL', 'betaR', 'betaL'):
+                del P[key]
+        self.overlapAddChunks(nChunks=nChunks, suffixIsSUIMM='_VUIMM.wav')
 
     def overlapAddChunks(self, nChunks, suffixIsSUIMM='.wav'):
         """Concatenate the chunk WAVs with their overlaps (:1469-1583): for the

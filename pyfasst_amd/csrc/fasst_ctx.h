@@ -26,8 +26,6 @@ struct fasst_ctx {
   // consumer, so they overlap the E-step instead of serialising before it
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  int nofork = 0;  // FASST_NOFORK (A/B measurements only)
-  int estep_split = 0;  // FASST_ESTEP_SPLIT: round-1 two-pass E-step (A/B measurements only)
   // observation
   int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
   fasst::DBuf<double> cx;        // 4*Tp*Fp
@@ -71,10 +69,6 @@ struct fasst_ctx {
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
   int nsplit_t = 1, fpc_t = 1;  // TW contraction bin chunks
-  int eb_split = 1;             // E-step / FB numerator interleaved over frame ranges
-  int nce_run = 1, ncb_run = 1; // partial-sum chunks the current iteration wrote
-  int tw_fused = 1;             // TW update applied in the TW contraction's last arrivers
-  fasst::DBuf<int> tcnt;        // their arrival counters [J][TW contraction x blocks]
   fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rpmax, rpe, rtpart;
   fasst::DBuf<double> gden, TWt, pnum, pden;  // FW update (free FW)
   int nchunk_r = 1;
@@ -86,9 +80,8 @@ struct fasst_ctx {
   double *h_ll = nullptr;        // pinned host mirror (one value)
   int psd_cap = 0, ll_cap = 0;
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
-  static constexpr int kNK = 15;
+  static constexpr int kNK = 13;
   int prof = 0;
-  int ablate = 0;  // FASST_ABLATE (profiling builds of the E-step; never in the product)
   hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};
   int used[kNK] = {0};
   double prof_ms[kNK] = {0};

@@ -58,9 +58,6 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
 // v_rcp_f64 + two Newton steps (<= 1 ulp) instead of the ~10-instruction
 // IEEE division sequence.
 __device__ __forceinline__ double rcp_nr(double x) {
-#ifdef FASST_EXACT_DIV  // A/B builds only
-  return 1.0 / x;
-#endif
   double r = __builtin_amdgcn_rcp(x);
   r = fma(fma(-x, r, 1.0), r, r);
   return fma(fma(-x, r, 1.0), r, r);
@@ -164,312 +161,8 @@ struct EArgs {
   int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
   int ybase, tbase;  // this launch's chunks start at partial ybase, frame tile tbase (ntt = end)
   int roff[kMaxJ + 1];
-  int store_hat;  // 1: hatW holds hat_W itself (general structures), 0: rho = hat_W / max(V, eps)
   const int *halt;
 };
-
-// Block: 4 waves on one 16-bin tile; wave w walks frame tiles w, w+4, ... of
-// the block's chunk.  Each lane owns ONE bin (f = f0 + lane%16) and 4 frames
-// per tile, so all per-bin statistics stay in registers across the t-loop.
-// The E-step is split in two launches so that each keeps half of the per-bin
-// accumulators live (occupancy):
-//   PART 1: pair statistics sum_t V_j1 V_j2 N (4 per pair), loglik, hat_W
-//   PART 2: cross statistics sum_t V_j Cx S (8 per source)
-// NKS = KP/4 MFMA k-steps; RKU = 1 or 2: every source has that rank (no
-// predication), 0: general ranks <= kMaxR.  AB = ablation bits (profiling
-// builds only, 0 in the product).
-#ifndef ESTEP_MINB1
-#define ESTEP_MINB1 2
-#endif
-#ifndef ESTEP_MINB2
-#define ESTEP_MINB2 2
-#endif
-#ifndef ESTEP_IB1
-#define ESTEP_IB1 2
-#endif
-#ifndef ESTEP_IB2
-#define ESTEP_IB2 4
-#endif
-template <int J, int NKS, int RKU, int PART, int AB>
-__global__ __launch_bounds__(256, PART == 1 ? ESTEP_MINB1 : ESTEP_MINB2) void k_estep(const EArgs a) {
-  HALT_GUARD(a.halt);
-  constexpr int NP = J * (J + 1) / 2;
-  constexpr int NACC = PART == 1 ? 4 * NP : 8 * J;
-  constexpr int UOFF = PART == 1 ? 0 : 4 * NP;   // column offset in the partial rows
-  constexpr int NTOT = 4 * NP + 8 * J;
-  constexpr int KP = 4 * NKS;
-  constexpr int RK = RKU ? RKU : kMaxR;
-  constexpr int IB = PART == 1 ? ESTEP_IB1 : ESTEP_IB2;  // frames per LDS coefficient read
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  double *s_cr = smem;                     // [kMaxR][4][16]
-  double *s_cj = s_cr + kMaxR * 4 * 16;    // [J][4][16]
-  double *s_ll = s_cj + J * 4 * 16;        // [4]
-  double *s_w = s_ll + 4;                  // [J][KP][16]   (t-loop)
-  double *s_red = s_w;                     // [4][NACC][16] (epilogue, aliases s_w)
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int fl = lane & 15, tq = lane >> 4;
-  const int f0 = blockIdx.x * 16;
-  const int f = f0 + fl;
-
-  for (int idx = tid; idx < J * KP * 16; idx += 256) {
-    const int ff = idx & 15, jk = idx >> 4;
-    s_w[idx] = a.Wkf[(size_t)jk * a.Fp + f0 + ff];
-  }
-  if (tid < 16) {
-    const int ff = f0 + tid;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      double al = 0, be = 0, gr = 0, gi = 0;
-      for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
-        const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + ff];
-        const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + ff];
-        const double aa = a0.x * a0.x + a0.y * a0.y;
-        const double bb = a1.x * a1.x + a1.y * a1.y;
-        const double cr = a0.x * a1.x + a0.y * a1.y;  // Re a0 conj(a1)
-        const double ci = a0.y * a1.x - a0.x * a1.y;  // Im a0 conj(a1)
-        s_cr[(r * 4 + 0) * 16 + tid] = aa;
-        s_cr[(r * 4 + 1) * 16 + tid] = bb;
-        s_cr[(r * 4 + 2) * 16 + tid] = 2.0 * cr;
-        s_cr[(r * 4 + 3) * 16 + tid] = 2.0 * ci;
-        al += aa;
-        be += bb;
-        gr += cr;
-        gi += ci;
-      }
-      s_cj[(j * 4 + 0) * 16 + tid] = al;
-      s_cj[(j * 4 + 1) * 16 + tid] = be;
-      s_cj[(j * 4 + 2) * 16 + tid] = gr;
-      s_cj[(j * 4 + 3) * 16 + tid] = gi;
-    }
-  }
-  __syncthreads();
-
-  int rk[J], r0[J];
-  double inv_rk[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    r0[j] = RKU ? RKU * j : a.roff[j];
-    rk[j] = RKU ? RKU : a.roff[j + 1] - a.roff[j];
-    inv_rk[j] = 1.0 / (double)rk[j];
-  }
-  const double psd = a.psd[f];
-  const bool fvalid = f < a.F;
-
-  double acc[NACC];
-#pragma unroll
-  for (int u = 0; u < NACC; ++u) acc[u] = 0.0;
-  // loglik: sum log(det*pi) is accumulated as a mantissa product lm in [0.5,1)
-  // times 2^lev (one log() per lane at the end instead of one per point);
-  // non-positive / non-finite terms map to -inf / NaN / inf like log().
-  double ll = 0.0, lm = 1.0, lev = 0.0, lspec = 0.0;
-
-  const int tb = a.tbase + blockIdx.y * a.tpc;
-  const int te = min(tb + a.tpc, a.ntt);
-  // V^T tile of frame tile tt (all sources) on the MFMA pipe
-  auto tile_v = [&](int tt, d4 *v, int lofs) {
-    const int t0 = tt * 16;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      v[j] = d4{0.0, 0.0, 0.0, 0.0};
-      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
-      const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
-#pragma unroll
-      for (int s = 0; s < NKS; ++s)
-        v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], sw[4 * s * 16], v[j]);
-    }
-  };
-  for (int tt = tb + wv; tt < te; tt += 4) {
-    const int t0 = tt * 16;
-    // the W tile and mixing coefficients are loop-invariant LDS data: launder
-    // the offset so they are re-read per tile instead of pinning ~96 VGPRs
-    int lofs = 0;
-    asm volatile("" : "+v"(lofs));
-    double c00[4], c11[4], cre[4], cim[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
-      // streamed planes (Cx, rho: 655 MB each at C3, larger than the 256 MB
-      // Infinity Cache) use non-temporal loads / stores: -1.5% per iteration
-      c00[i] = __builtin_nontemporal_load(a.cx00 + off);
-      c11[i] = __builtin_nontemporal_load(a.cx11 + off);
-      cre[i] = __builtin_nontemporal_load(a.cxr + off);
-      cim[i] = __builtin_nontemporal_load(a.cxi + off);
-    }
-    d4 v[J];
-    tile_v(tt, v, lofs);
-    const double *cj = s_cj + lofs + fl;
-    // frames are taken IB at a time so that every per-bin LDS coefficient is
-    // read once per IB frames (LDS bandwidth, not VALU, bounded part 1 with
-    // one read per frame); the per-frame arithmetic and its order are unchanged
-#pragma unroll
-    for (int ib = 0; ib < 4; ib += IB) {
-    double sx[IB][4];
-#pragma unroll
-    for (int ii = 0; ii < IB; ++ii) {
-      sx[ii][0] = psd;
-      sx[ii][1] = psd;
-      sx[ii][2] = 0.0;
-      sx[ii][3] = 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const double q = cj[(j * 4 + c) * 16];
-#pragma unroll
-        for (int ii = 0; ii < IB; ++ii) sx[ii][c] += q * v[j][ib + ii];
-      }
-    double nn[IB][4];
-#pragma unroll
-    for (int ii = 0; ii < IB; ++ii) {
-      const int i = ib + ii;
-      const int t = t0 + tq + 4 * i;
-      double V[J];
-#pragma unroll
-      for (int j = 0; j < J; ++j) V[j] = v[j][i];
-      const double d0 = sx[ii][0], d1 = sx[ii][1], ore = sx[ii][2], oim = sx[ii][3];
-      // inv_herm_mat_2d (signalTools.py:177-194)
-      double det = d0 * d1 - (ore * ore + oim * oim);
-      const double dg = det + kEps;
-      const double sg = dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0);
-      det = sg * fmax(fabs(det), kEps);
-      const double rd = rcp_nr(det);
-      const double i0 = d1 * rd, i1 = d0 * rd, ior = -ore * rd, ioi = -oim * rd;
-      const double x00 = c00[i], x11 = c11[i], xr = cre[i], xi = cim[i];
-      // P = Cx S
-      const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
-      const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
-      const double p10r = xr * i0 + x11 * ior, p10i = -xi * i0 - x11 * ioi;
-      const double p11r = xr * ior + xi * ioi + x11 * i1, p11i = xr * ioi - xi * ior;
-      if (PART == 2) {
-        if (!(AB & 4)) {
-#pragma unroll
-          for (int j = 0; j < J; ++j) {
-            acc[8 * j + 0] += V[j] * p00r;
-            acc[8 * j + 1] += V[j] * p00i;
-            acc[8 * j + 2] += V[j] * p01r;
-            acc[8 * j + 3] += V[j] * p01i;
-            acc[8 * j + 4] += V[j] * p10r;
-            acc[8 * j + 5] += V[j] * p10i;
-            acc[8 * j + 6] += V[j] * p11r;
-            acc[8 * j + 7] += V[j] * p11i;
-          }
-        }
-        continue;
-      }
-      if (fvalid && t < a.T) {
-        const double x = det * M_PI;
-        if (AB & 1) {
-          ll += x;
-        } else if (x > 0.0 && x < INFINITY) {
-          const unsigned long long b = __double_as_longlong(x);
-          lev += (double)((int)((b >> 52) & 0x7ff) - 1022);
-          lm *= __longlong_as_double((b & 0x800fffffffffffffULL) | 0x3fe0000000000000ULL);
-        } else {
-          lspec += x == 0.0 ? -INFINITY : (x == INFINITY ? INFINITY : NAN);
-        }
-        ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
-      }
-      // N = S Cx S - S = P^H S - S
-      const double n00 = p00r * i0 + (p10r * ior - p10i * ioi) - i0;
-      const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
-      const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
-      const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
-      if (!(AB & 4)) {
-        int p = 0;
-#pragma unroll
-        for (int j1 = 0; j1 < J; ++j1) {
-#pragma unroll
-          for (int j2 = j1; j2 < J; ++j2, ++p) {
-            const double vv = V[j1] * V[j2];
-            acc[4 * p + 0] += vv * n00;
-            acc[4 * p + 1] += vv * n11;
-            acc[4 * p + 2] += vv * n01r;
-            acc[4 * p + 3] += vv * n01i;
-          }
-        }
-      }
-      nn[ii][0] = n00;
-      nn[ii][1] = n11;
-      nn[ii][2] = n01r;
-      nn[ii][3] = n01i;
-      if (AB & 2) {
-        double sum = 0.0;
-#pragma unroll
-        for (int j = 0; j < J; ++j) sum += V[j] * n00;
-        a.hatW[(size_t)t * a.Fp + f] = sum;
-      }
-    }
-    // hat_W[j] = mean over the ranks of j of |V^2 a^H N a + V| (:727-729, :413-414),
-    // stored as rho = (hat_W / vm^2) * vm with vm = max(V, eps): the FB ratio
-    // of update_spectral_components (:1521-1575, N1) formed here, where V is
-    // already in registers, so the FB contraction needs no V recompute; the
-    // TW contraction recovers hat_W as rho * max(V_old, eps)
-    if (PART == 1 && !(AB & 2)) {
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        double hw[IB];
-#pragma unroll
-        for (int ii = 0; ii < IB; ++ii) hw[ii] = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < RK; ++qq) {
-          if (RKU || qq < rk[j]) {
-            const double *cr = s_cr + lofs + (r0[j] + qq) * 64 + fl;
-            const double c0 = cr[0], c1 = cr[16], c2 = cr[32], c3 = cr[48];
-#pragma unroll
-            for (int ii = 0; ii < IB; ++ii) {
-              const double Vj = v[j][ib + ii];
-              const double qa = c0 * nn[ii][0] + c1 * nn[ii][1] + (c2 * nn[ii][2] + c3 * nn[ii][3]);
-              hw[ii] += fabs((Vj * Vj) * qa + Vj);
-            }
-          }
-        }
-#pragma unroll
-        for (int ii = 0; ii < IB; ++ii) {
-          const double Vj = v[j][ib + ii];
-          const double hwm = RKU == 1 ? hw[ii] : hw[ii] * inv_rk[j];
-          const double vm = fmax(Vj, kEps);
-          const double rv = rcp_nr(vm);
-          __builtin_nontemporal_store((hwm * (rv * rv)) * vm,
-                                      a.hatW + ((size_t)j * a.Tp + t0 + tq + 4 * (ib + ii)) * a.Fp + f);
-        }
-      }
-    }
-    }
-    if (PART == 1) {  // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
-      const unsigned long long b = __double_as_longlong(lm);
-      lev += (double)((int)((b >> 52) & 0x7ff) - 1022);
-      lm = __longlong_as_double((b & 0x800fffffffffffffULL) | 0x3fe0000000000000ULL);
-    }
-  }
-  if (PART == 1) ll += (log(lm) + lev * M_LN2) + lspec;
-
-  // reduce the 4 lanes sharing a bin, then the 4 waves, then write the chunk partial
-  __syncthreads();  // s_red aliases s_w: every wave must be done with its last tile
-  double *red = s_red + wv * NACC * 16;
-#pragma unroll
-  for (int u = 0; u < NACC; ++u) {
-    double x = acc[u];
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    if (tq == 0) red[u * 16 + fl] = x;
-  }
-  if (PART == 1) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) ll += __shfl_xor(ll, m, 64);
-    if (lane == 0) s_ll[wv] = ll;
-  }
-  __syncthreads();
-  for (int idx = tid; idx < NACC * 16; idx += 256) {
-    const int u = idx >> 4, ff = idx & 15;
-    const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
-                     s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
-    a.part[((size_t)(a.ybase + blockIdx.y) * a.Fp + f0 + ff) * NTOT + UOFF + u] = x;
-  }
-  if (PART == 1 && tid == 0)
-    a.llpart[(a.ybase + blockIdx.y) * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
-}
 
 // Single-pass E-step with the per-bin t-reductions on the matrix cores.
 //
@@ -543,17 +236,11 @@ __device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsign
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(es_u2, v), r, (int)vo, (int)so, AUX);
 }
 
-#ifndef ESTEP_LL_SELECT
-#define ESTEP_LL_SELECT 0
+#ifndef ESTEP_PF
+#define ESTEP_PF 0
 #endif
-#ifndef ESTEP_NO_STOREHAT
-#define ESTEP_NO_STOREHAT 1
-#endif
-#ifndef ESTEP_SADDR
-#define ESTEP_SADDR 1
-#endif
-#ifndef ESTEP_TRIM
-#define ESTEP_TRIM 0
+#ifndef ESTEP_RHO_AUX
+#define ESTEP_RHO_AUX 2
 #endif
 template <int J, int NKS, int RKU>
 __global__ __launch_bounds__(256, J > 4 ? 1 : 2)
@@ -627,13 +314,7 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
     for (int h = 0; h < NPG; ++h) pacc[g][h] = 0.0;
   }
-#if ESTEP_TRIM
-  // exponent sum in an integer, negative-det flag as the OR of the sign words
-  double ll = 0.0, lm = 1.0;
-  int ilev = 0, sgn = 0;
-#else
   double ll = 0.0, lm = 1.0, lev = 0.0, xmin = 1.0;
-#endif
 
   const int tb = a.tbase + blockIdx.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
@@ -641,11 +322,38 @@ void k_estep_mx(const EArgs a) {
   // 32-bit per-lane byte offsets instead of one 64-bit VALU address
   // computation per access (J <= 4: the J = 8, K = 64 instantiation trips a
   // compiler crash in ROCm 7.2's AGPR-copy rewrite with it)
-  constexpr bool SA = ESTEP_SADDR && J <= 4;
+  constexpr bool SA = J <= 4;
   int wvu = wv;
   if constexpr (SA) wvu = __builtin_amdgcn_readfirstlane(wv);
   const unsigned vo_tw = (unsigned)(tq * a.Tp + fl) * 8u;   // TW[j][k = tq + 4s][t0 + fl]
   const unsigned vo_cx = (unsigned)(tq * a.Fp + f) * 8u;    // plane[t0 + tq + 4i][f]
+  // Cx of frame tile tt (raw-buffer form; the flat form without SA)
+  auto load_cx = [&](int tt, double (&c)[4][4]) {
+    const int t0 = tt * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (SA) {
+        const size_t ro = (size_t)t0 * a.Fp;
+        const unsigned so = (unsigned)(4 * i * a.Fp) * 8u;
+        c[0][i] = es_ld<2>(es_rsrc(a.cx00 + ro), vo_cx, so);
+        c[1][i] = es_ld<2>(es_rsrc(a.cx11 + ro), vo_cx, so);
+        c[2][i] = es_ld<2>(es_rsrc(a.cxr + ro), vo_cx, so);
+        c[3][i] = es_ld<2>(es_rsrc(a.cxi + ro), vo_cx, so);
+      } else {
+        const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
+        c[0][i] = __builtin_nontemporal_load(a.cx00 + off);
+        c[1][i] = __builtin_nontemporal_load(a.cx11 + off);
+        c[2][i] = __builtin_nontemporal_load(a.cxr + off);
+        c[3][i] = __builtin_nontemporal_load(a.cxi + off);
+      }
+    }
+  };
+  // ESTEP_PF: the next tile's Cx is loaded while this tile computes (HBM
+  // latency off the tile's critical path); a wave's last tile re-loads
+  // itself (clamped index: no branch around the loads)
+  constexpr bool PF = ESTEP_PF && SA;
+  double cxn[4][4];
+  if constexpr (PF) load_cx(min(tb + wvu, te - 1), cxn);
   for (int tt = tb + wvu; tt < te; tt += 4) {
     const int t0 = tt * 16;
     int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
@@ -664,23 +372,15 @@ void k_estep_mx(const EArgs a) {
         twv[j][s] = SA ? es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u)
                        : tw[(size_t)(4 * s) * a.Tp];
     }
-    double cxv[4][4];  // this tile's Cx, in flight with the TW operands
+    double cxv[4][4];  // this tile's Cx (in flight with the TW operands without PF)
+    if constexpr (PF) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if constexpr (SA) {
-        const size_t ro = (size_t)t0 * a.Fp;
-        const unsigned so = (unsigned)(4 * i * a.Fp) * 8u;
-        cxv[0][i] = es_ld<2>(es_rsrc(a.cx00 + ro), vo_cx, so);
-        cxv[1][i] = es_ld<2>(es_rsrc(a.cx11 + ro), vo_cx, so);
-        cxv[2][i] = es_ld<2>(es_rsrc(a.cxr + ro), vo_cx, so);
-        cxv[3][i] = es_ld<2>(es_rsrc(a.cxi + ro), vo_cx, so);
-      } else {
-        const size_t off = (size_t)(t0 + tq + 4 * i) * a.Fp + f;
-        cxv[0][i] = __builtin_nontemporal_load(a.cx00 + off);
-        cxv[1][i] = __builtin_nontemporal_load(a.cx11 + off);
-        cxv[2][i] = __builtin_nontemporal_load(a.cxr + off);
-        cxv[3][i] = __builtin_nontemporal_load(a.cxi + off);
-      }
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cxv[q][i] = cxn[q][i];
+      load_cx(min(tt + 4, te - 1), cxn);
+    } else {
+      load_cx(tt, cxv);
     }
     __builtin_amdgcn_sched_barrier(0);
     d4 v[J];
@@ -719,35 +419,17 @@ void k_estep_mx(const EArgs a) {
       det = sg * fmax(fabs(det), kEps);
       const double rdet = rcp_nr(det);
       const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
-#if ESTEP_LL_SELECT
-      {
-        // (branch-free form: padding points contribute x = 1, i.e. nothing)
-        const bool ok = fvalid && t < a.T;
-        const double x = ok ? det * M_PI : 1.0;
-        lev += (double)__builtin_amdgcn_frexp_exp(x);
-        lm *= __builtin_amdgcn_frexp_mant(x);
-        xmin = fmin(xmin, x);
-        ll += ok ? i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi) : 0.0;
-      }
-#else
       if (fvalid && t < a.T) {
         // log(det pi) as mantissa product x 2^exponent (v_frexp_*: 0, inf and
         // NaN pass through the mantissa, so log(lm) gives -inf / inf / NaN as
         // log() would; a negative det, which the guard only lets through for
         // a Sigma_x that is not positive semi-definite, is flagged in xmin)
         const double x = det * M_PI;
-#if ESTEP_TRIM
-        ilev += __builtin_amdgcn_frexp_exp(x);
-        lm *= __builtin_amdgcn_frexp_mant(x);
-        sgn |= (int)(__double_as_longlong(x) >> 32);
-#else
         lev += (double)__builtin_amdgcn_frexp_exp(x);
         lm *= __builtin_amdgcn_frexp_mant(x);
         xmin = fmin(xmin, x);
-#endif
         ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
       }
-#endif
       // P = Cx S, N = S Cx S - S = P^H S - S
       const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
       const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
@@ -757,10 +439,6 @@ void k_estep_mx(const EArgs a) {
       const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
       const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
       const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
-#if ESTEP_TRIM
-      constexpr double sr = RKU == 2 ? 0.5 : 1.0;
-      const double m00 = n00 * sr, m11 = n11 * sr, m01r = n01r * (2.0 * sr), m01i = n01i * (2.0 * sr);
-#endif
       // this point's MFMA operands -> the wave's slab (reader layout)
 #pragma unroll
       for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
@@ -796,28 +474,13 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const double Vj = V[j];
-#if ESTEP_TRIM
-        // (the factors 2 and 1 / rank folded into the N components once per
-        // point: exact scalings by powers of two for ranks 1 and 2)
-        const double q = RKU == 1 || RKU == 2
-                              ? (cj[(j * 4 + 0) * 16] * m00 + cj[(j * 4 + 1) * 16] * m11) +
-                                    (cj[(j * 4 + 2) * 16] * m01r + cj[(j * 4 + 3) * 16] * m01i)
-                              : ((cj[(j * 4 + 0) * 16] * n00 + cj[(j * 4 + 1) * 16] * n11) +
-                                 2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i)) *
-                                    inv_rk[j];
-#else
         const double qa = (cj[(j * 4 + 0) * 16] * n00 + cj[(j * 4 + 1) * 16] * n11) +
                           2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i);
         const double q = RKU == 1 ? qa : qa * inv_rk[j];
-#endif
-        double val;
-        if (!ESTEP_NO_STOREHAT && a.store_hat)
-          val = fabs((Vj * Vj) * q + Vj);
-        else
-          val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
+        const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
         if constexpr (SA)
-          es_st<2>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
-                   (unsigned)(4 * i * a.Fp) * 8u);
+          es_st<ESTEP_RHO_AUX>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
+                               (unsigned)(4 * i * a.Fp) * 8u);
         else
           __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
       }
@@ -855,18 +518,10 @@ void k_estep_mx(const EArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
-#if ESTEP_TRIM
-    ilev += __builtin_amdgcn_frexp_exp(lm);
-#else
     lev += (double)__builtin_amdgcn_frexp_exp(lm);
-#endif
     lm = __builtin_amdgcn_frexp_mant(lm);
   }
-#if ESTEP_TRIM
-  ll += (log(lm) + (double)ilev * M_LN2) + (sgn < 0 ? NAN : 0.0);
-#else
   ll += (log(lm) + lev * M_LN2) + (xmin < 0.0 ? NAN : 0.0);
-#endif
 
   // epilogue: lane (X = m, b, Y = n) holds, per bin group g, the 4x4 blocks
   // D[m][n] of bin f0 + 4g + b: cross (j = m, c = 4h + n), pairs (p = 4h + m, c = n)
@@ -1273,12 +928,6 @@ struct BArgs {
 // Without DEN and FPW even the tiles are interleaved (bin f in tile f mod
 // FPW), so each lane's rho values arrive as 16-byte loads (C3: 0.166 ->
 // 0.155 ms at FPW = 2, same-box A/B).
-#ifndef FB_REVERSE
-#define FB_REVERSE 0
-#endif
-#ifndef FB_RAWBUF
-#define FB_RAWBUF 0
-#endif
 template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
@@ -1294,9 +943,9 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   for (int p = 0; p < (DEN ? FPW : 1); ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
-  // FB_REVERSE: frame chunks taken last-first, so the chunks the E-step wrote
-  // last are read while they may still sit in the 256 MB infinity cache (the
-  // chunk's partial slot is its own index either way: same sums, same order)
+#ifndef FB_REVERSE
+#define FB_REVERSE 0
+#endif
   const int zc = FB_REVERSE ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
   const int tb = a.tbase + zc * a.tpc, te = min(tb + a.tpc, a.ntt);
   const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
@@ -1316,24 +965,6 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       // per load instruction instead of 4 x 16
       const int fp = ft0 * 16 + FPW * fl;
       double r[FPW][4];
-#if FB_RAWBUF
-      // raw-buffer loads off the tile's (wave-uniform) row base: frames past
-      // T / bins past Fp take an offset outside the resource and read 0, so
-      // the loads carry no exec branches
-      const __amdgpu_buffer_rsrc_t rr = es_rsrc(rhoj + (size_t)t0 * a.Fp);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = t0 + tq + 4 * i < a.T && fp < a.Fp;
-        const unsigned vo = ok ? (unsigned)(((tq + 4 * i) * a.Fp + fp) * 8) : 0x80000000u;
-#pragma unroll
-        for (int h = 0; h < FPW; h += 2) {
-          typedef unsigned u4 __attribute__((ext_vector_type(4)));
-          const u4 x = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(vo + 8u * h), 0, 0);
-          r[h][i] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 0, 1));
-          r[h + 1][i] = __builtin_bit_cast(double, __builtin_shufflevector(x, x, 2, 3));
-        }
-      }
-#else
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool ok = t0 + tq + 4 * i < a.T && fp < a.Fp;
@@ -1345,7 +976,6 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
           r[h + 1][i] = v.y;
         }
       }
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1644,75 +1274,9 @@ struct TArgs {
   int kb0[kMaxJ], kb1[kMaxJ];  // BLK: the V tiles sum the columns [kb0, kb1) only
   const double *cp, *pw;       // LAM: corrPen / powers planes of k_multi_prep
   const double *oth;           // TBQ: max(V_c, eps) plane of k_multi_prep
-  // !BLK with cnt set: the last of a frame tile's gridDim.z bin-chunk blocks
-  // sums their partials and applies the TW update itself (k_tw_update's work,
-  // in launch); cnt[j][blockIdx.x] are its arrival counters (zero between
-  // launches: the last arriver resets them)
-  int *cnt;
   double omega;
   const int *halt;
 };
-
-// write-through (sc1) 8-byte buffer accesses: a hand-off that needs no
-// agent-scope release / acquire fence (cdna_hip_programming.md split-K recipe)
-typedef unsigned tw_u2 __attribute__((ext_vector_type(2)));
-constexpr int kSc1 = 16;
-__device__ __forceinline__ void sc1_store(__amdgpu_buffer_rsrc_t r, size_t i, double v) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  tw_u2 x;
-  x.x = (unsigned)b;
-  x.y = (unsigned)(b >> 32);
-  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)(i * sizeof(double)), 0, kSc1);
-}
-__device__ __forceinline__ double sc1_load(__amdgpu_buffer_rsrc_t r, size_t i) {
-  const tw_u2 x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * sizeof(double)), 0, kSc1);
-  return __longlong_as_double((long long)(((unsigned long long)x.y << 32) | x.x));
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const double *p, size_t n) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, (int)(n * sizeof(double)),
-                                           0x00020000);
-}
-
-// TW *= (sum_chunks num / max(sum_chunks den, eps))^omega for the frames of
-// the TPW tiles at tt0 of source j (k_tw_update's arithmetic, chunk order
-// kept): one wave, loads coalesced over k
-template <int TPW>
-__device__ void tw_apply_tiles(const TArgs &a, int j, int tt0, int lane) {
-  const int n = 16 * a.KP;
-  const size_t cs = (size_t)a.J * a.Tp * a.KP;
-  const __amdgpu_buffer_rsrc_t rn = buf_rsrc(a.tnum, cs * gridDim.z);
-  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(a.tden, cs * gridDim.z);
-  for (int p = 0; p < TPW; ++p) {
-    if (tt0 + p >= a.ntt) break;
-    const int t0 = (tt0 + p) * 16;
-    for (int base = 0; base < n; base += 4 * 64) {
-      double num[4], den[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) num[u] = den[u] = 0.0;
-      for (int c = 0; c < (int)gridDim.z; ++c) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int idx = base + u * 64 + lane;
-          if (idx < n) {
-            const size_t o = c * cs + ((size_t)j * a.Tp + t0 + idx / a.KP) * a.KP + idx % a.KP;
-            num[u] += sc1_load(rn, o);
-            den[u] += sc1_load(rd, o);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int idx = base + u * 64 + lane;
-        const int t = t0 + idx / a.KP, k = idx % a.KP;
-        if (idx < n && t < a.T && k >= a.kb0[j] && k < a.kb1[j]) {
-          const double ratio = num[u] / fmax(den[u], kEps);
-          const_cast<double *>(a.TW)[((size_t)j * a.KP + k) * a.Tp + t] *=
-              a.omega == 1.0 ? ratio : pow(ratio, a.omega);
-        }
-      }
-    }
-  }
-}
 
 // TW numerator / denominator over f (:1694-1726), one wave per (TPW frame
 // tiles, source, bin chunk):
@@ -1728,12 +1292,6 @@ __device__ void tw_apply_tiles(const TArgs &a, int j, int tt0, int lane) {
 // TBQ (the TB step of a component with time blobs, :1931-1978): H has moved
 // since the step's start, so other = max(V_c_old, eps) comes from a plane,
 // hatW is hat_W_j itself, and num's ratio is hat_W / max(V_new^2, eps).
-#ifndef TW_1CHAIN
-#define TW_1CHAIN 0
-#endif
-#ifndef TW_EDGE_SPLIT
-#define TW_EDGE_SPLIT 0
-#endif
 template <int NKC, int TPW, bool BLK = false, bool LAM = false, bool TBQ = false>
 __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
@@ -1797,15 +1355,6 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
         h[3] = h23.y;
       }
       d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
-#if TW_1CHAIN
-      // one accumulation chain per product (vo and vn interleaved): no
-      // partial-sum adds
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        if constexpr (!TBQ) vo = mfma4(ao[s], bt[p][s], vo);
-        vn = mfma4(an[s], bt[p][s], vn);
-      }
-#else
       d4 vo2 = vo, vn2 = vo;
 #pragma unroll
       for (int s = 0; s < NKS; s += 2) {
@@ -1818,18 +1367,14 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       }
       vo += vo2;
       vn += vn2;
-#endif
-      // EDGE = false for interior tiles (every bin < F and frame < T: all but
-      // the last bin and frame tiles): no per-point padding masks there
-      auto form = [&](auto edge_c) {
-        constexpr bool EDGE = decltype(edge_c)::value;
-        const bool tok = !EDGE || t < a.T;
+      {
+        const bool tok = t < a.T;
         double r3[4], r4[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const double vm = fmax(vn[i], kEps);
           const double rv = rcp_nr(vm);
-          const bool ok = !EDGE || (tok && f0 + bq + bs * i < a.F);
+          const bool ok = tok && f0 + bq + bs * i < a.F;
           const size_t o = (size_t)j * a.Tp * a.Fp + (size_t)t * a.Fp + f0 + bq + bs * i;
           double other, q;
           if constexpr (TBQ) {
@@ -1855,45 +1400,10 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
             num[p][kc] = mfma4(r3[i], bw[i][kc], num[p][kc]);
             den[p][kc] = mfma4(r4[i], bw[i][kc], den[p][kc]);
           }
-      };
-      if (TW_EDGE_SPLIT && f0 + 16 <= a.F && (tt0 + p) * 16 + 16 <= a.T)
-        form(std::false_type{});
-      else
-        form(std::true_type{});
+      }
     }
   }
   const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Tp;
-  bool fused = false;
-  if constexpr (!BLK && !TBQ) fused = a.cnt != nullptr;
-  if (fused) {
-    // in-launch split-K reduction: the partials go out write-through (sc1),
-    // drained before the ticket; the last arriver reads them with sc1 loads
-    // (no agent fences: cdna_hip_programming.md split-K recipe, sc1 form)
-    const size_t nall = (size_t)gridDim.z * a.J * a.Tp * a.KP;
-    const __amdgpu_buffer_rsrc_t rn = buf_rsrc(a.tnum, nall), rd = buf_rsrc(a.tden, nall);
-#pragma unroll
-    for (int p = 0; p < TPW; ++p) {
-      if (tt0 + p >= a.ntt) break;
-#pragma unroll
-      for (int kc = 0; kc < NKC; ++kc)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const size_t o = (base + (tt0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl;
-          sc1_store(rn, o, num[p][kc][m]);
-          sc1_store(rd, o, den[p][kc][m]);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int last = 0;
-    if (lane == 0) {
-      int *ct = a.cnt + (size_t)j * gridDim.x + blockIdx.x;
-      const int old = __hip_atomic_fetch_add(ct, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = old == (int)gridDim.z - 1;
-      if (last) __hip_atomic_store(ct, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (__builtin_amdgcn_readfirstlane(last)) tw_apply_tiles<TPW>(a, j, tt0, lane);
-    return;
-  }
 #pragma unroll
   for (int p = 0; p < TPW; ++p) {
     if (tt0 + p >= a.ntt) break;
@@ -2503,13 +2013,12 @@ __global__ __launch_bounds__(256) void k_tb_renorm(const TBRArgs a) {
 
 // ---------------------------------------------------------------- host side
 enum KernelId {
-  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KESTEP2, KESTEP1,
-  KFWU
+  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KFWU
 };
 static const char *kKernelNames[fasst_ctx::kNK] = {
     "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep", "k_loglik", "k_mix",
     "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm", "k_tw_update",
-    "k_estep_part2", "k_estep_part1", "k_fw_update"};
+    "k_fw_update"};
 
 static inline void prof_begin(fasst_ctx *c, int id) {
   if (c->prof) {
@@ -2652,16 +2161,6 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
   c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
-  c->eb_split = 1;
-  if (const char *v = getenv("FASST_EB_SPLIT")) c->eb_split = std::max(1, std::min(atoi(v), 8));
-  // FASST_TW_FUSED=1: the TW update in the TW contraction's last arrivers
-  // (A/B knob, default off: C3 1.144 ms per iteration fused with the sc1
-  // hand-off vs 1.139 separate; 1.358 with agent release / acquire fences);
-  // the fused form addresses the partials with 32-bit buffer offsets
-  c->tw_fused = 0;
-  if (const char *v = getenv("FASST_TW_FUSED"))
-    c->tw_fused = atoi(v) != 0 &&
-                  (size_t)c->nsplit_t * J * c->Tp * c->KP * sizeof(double) < (1ull << 31);
   if (getenv("FASST_VERBOSE"))
     fprintf(stderr,
             "fasst: %d CUs; estep %d chunks (cap %ld blocks); fb %d chunks (cap %ld); tw %d "
@@ -2692,7 +2191,6 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(pnum, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(pden, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
   ALLOC(tnum, (size_t)c->nsplit_t * J * Tp * KP);
-  if ((st = c->tcnt.alloc((size_t)J * ((c->ntt + tpw_of(c) - 1) / tpw_of(c))))) return st;
   ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
   ALLOC(rxs, conv ? 0 : (size_t)Fp * 2 * R);
@@ -2866,18 +2364,10 @@ static int launch_renorm(fasst_ctx *c, int iter) {
 
 // E-step instantiation chosen from the model structure; `f` receives an
 // ETag carrying the template parameters (used for launches and occupancy).
-template <int J_, int NKS_, int RKU_, int AB_>
+template <int J_, int NKS_, int RKU_>
 struct ETag {
-  static constexpr int J = J_, NKS = NKS_, RKU = RKU_, AB = AB_;
+  static constexpr int J = J_, NKS = NKS_, RKU = RKU_;
 };
-
-template <class T>
-static size_t estep_smem(int part) {
-  constexpr int NP = T::J * (T::J + 1) / 2;
-  const size_t base = (size_t)(kMaxR * 4 * 16 + T::J * 4 * 16 + 4);
-  const size_t red = part == 1 ? 4 * (4 * NP) * 16 : 4 * (8 * T::J) * 16;
-  return (base + std::max((size_t)(T::J * 4 * T::NKS * 16), red)) * sizeof(double);
-}
 
 template <int J, int NKS, class F>
 static void estep_dispatch_r(const fasst_ctx *c, F &&f) {
@@ -2887,33 +2377,22 @@ static void estep_dispatch_r(const fasst_ctx *c, F &&f) {
     all2 &= c->rank[j] == 2;
   }
   if (all1)
-    f(ETag<J, NKS, 1, 0>{});
+    f(ETag<J, NKS, 1>{});
   else if (all2)
-    f(ETag<J, NKS, 2, 0>{});
+    f(ETag<J, NKS, 2>{});
   else
-    f(ETag<J, NKS, 0, 0>{});
+    f(ETag<J, NKS, 0>{});
 }
 
 template <int J, class F>
 static void estep_dispatch_j(const fasst_ctx *c, F &&f) {
-  bool all2 = true;
-  for (int j = 0; j < J; ++j) all2 &= c->rank[j] == 2;
-  if (J == 4 && c->KP == 32 && all2 && c->ablate) {  // profiling builds only
-    switch (c->ablate) {
-      case 1: f(ETag<4, 8, 2, 1>{}); return;
-      case 2: f(ETag<4, 8, 2, 2>{}); return;
-      case 4: f(ETag<4, 8, 2, 4>{}); return;
-      case 7: f(ETag<4, 8, 2, 7>{}); return;
-      default: break;
-    }
-  }
   switch (c->KP) {
     case 16: estep_dispatch_r<J, 4>(c, f); break;
     case 32: estep_dispatch_r<J, 8>(c, f); break;
     case 64: estep_dispatch_r<J, 16>(c, f); break;
     default:   // K up to 128: general ranks only, J <= 4 (gem_iteration refuses more)
-      if constexpr (J <= 4) f(ETag<J, 32, 0, 0>{});
-      else f(ETag<J, 16, 0, 0>{});
+      if constexpr (J <= 4) f(ETag<J, 32, 0>{});
+      else f(ETag<J, 16, 0>{});
       break;
   }
 }
@@ -2935,49 +2414,26 @@ static void estep_dispatch(const fasst_ctx *c, F &&f) {
 static void launch_estep(fasst_ctx *c, const EArgs &e, int ny) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
-    dim3 grid(c->nft, ny);
-    if ((!c->estep_split || T::J > 4) && !T::AB) {
-      prof_begin(c, KESTEP);
-      k_estep_mx<T::J, T::NKS, T::RKU>
-          <<<grid, 256, estep_mx_smem<T::J, T::NKS>(), c->stream>>>(e);
-      prof_end(c, KESTEP);
-      return;
-    }
-    if constexpr (T::J <= 4 && T::NKS <= 16) {  // round-1 two-pass E-step (A/B only)
-      prof_begin(c, KESTEP1);
-      k_estep<T::J, T::NKS, T::RKU, 1, T::AB><<<grid, 256, estep_smem<T>(1), c->stream>>>(e);
-      prof_end(c, KESTEP1);
-      prof_begin(c, KESTEP2);
-      k_estep<T::J, T::NKS, T::RKU, 2, T::AB><<<grid, 256, estep_smem<T>(2), c->stream>>>(e);
-      prof_end(c, KESTEP2);
-    }
+    prof_begin(c, KESTEP);
+    k_estep_mx<T::J, T::NKS, T::RKU>
+        <<<dim3(c->nft, ny), 256, estep_mx_smem<T::J, T::NKS>(), c->stream>>>(e);
+    prof_end(c, KESTEP);
   });
 }
 
-// resident blocks per CU of the E-step pair (the lower of the two parts)
+// resident E-step blocks per CU
 static int estep_occupancy(const fasst_ctx *c) {
   int occ = 1;
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
-    int n1 = 0, n2 = 0;
-    if ((!c->estep_split || T::J > 4) && !T::AB) {
-      constexpr size_t smem = estep_mx_smem<T::J, T::NKS>();
-      (void)hipFuncSetAttribute((const void *)k_estep_mx<T::J, T::NKS, T::RKU>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n1, k_estep_mx<T::J, T::NKS, T::RKU>, 256,
-                                                       smem) != hipSuccess)
-        n1 = 1;
-      occ = std::max(1, n1);
-      return;
-    }
-    if constexpr (T::J <= 4 && T::NKS <= 16) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &n1, k_estep<T::J, T::NKS, T::RKU, 1, T::AB>, 256, estep_smem<T>(1)) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &n2, k_estep<T::J, T::NKS, T::RKU, 2, T::AB>, 256, estep_smem<T>(2)) != hipSuccess)
-        n1 = n2 = 1;
-    }
-    occ = std::max(1, std::min(n1, n2));
+    constexpr size_t smem = estep_mx_smem<T::J, T::NKS>();
+    (void)hipFuncSetAttribute((const void *)k_estep_mx<T::J, T::NKS, T::RKU>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_estep_mx<T::J, T::NKS, T::RKU>, 256,
+                                                     smem) != hipSuccess)
+      n = 1;
+    occ = std::max(1, n);
   });
   return occ;
 }
@@ -3127,7 +2583,6 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     t.cp = mp.rcp;
     t.pw = mp.rpow;
     t.oth = nullptr;
-    t.cnt = nullptr;
     t.omega = omega;
     const TBArgs tbw = tb_args(c, b, only_j, 1, omega), tbb = tb_args(c, b, only_j, 2, omega);
     int lmax, kwmax;
@@ -3313,7 +2768,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   // (FW.TW)^T and the TW row sums depend only on the previous iteration's
   // parameters: fork them onto the side stream (kept on the main stream
   // while per-kernel event timing is on)
-  const bool fork = !c->prof && !c->nofork;
+  const bool fork = !c->prof;
   hipStream_t side = fork ? c->aux : c->stream;
   if (fork) {
     FASST_HIP(hipEventRecord(c->ev_fork, c->stream));
@@ -3357,7 +2812,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.tpc = c->tpc_e;
   e.nft = c->nft;
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
-  e.store_hat = 0;
   e.ybase = e.tbase = 0;
   BArgs b;
   b.TW = c->TW.p;
@@ -3380,48 +2834,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   b.zbase = b.tbase = 0;
   for (int j = 0; j < kMaxJ; ++j) b.fb_free[j] = j < J ? c->fb_free[j] : 0;
   const int nkc = c->KP / 16;
-  // E-step and FB numerator interleaved over eb_split frame ranges: each
-  // range's rho is contracted right after it is written, while it is still in
-  // the 256 MB infinity cache (FASST_EB_SPLIT)
-  const int S = c->multi ? 1 : c->eb_split;
-  bool fb_done = false;
-  c->nce_run = c->nchunk_e;
-  c->ncb_run = c->nchunk_b;
-  if (S > 1) {
-    int ye = 0, zb = 0;
-    for (int sc = 0; sc < S; ++sc) {
-      const int T0 = (int)((long)sc * c->ntt / S), T1 = (int)((long)(sc + 1) * c->ntt / S);
-      if (T1 <= T0) continue;
-      const int ne = (T1 - T0 + c->tpc_e - 1) / c->tpc_e, nb = (T1 - T0 + c->tpc_b - 1) / c->tpc_b;
-      e.ybase = ye;
-      e.tbase = T0;
-      e.ntt = T1;
-      launch_estep(c, e, ne);
-      FASST_LAUNCH_CHECK();
-      if (fork && sc == 0) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // FWHt
-      b.zbase = zb;
-      b.tbase = T0;
-      b.ntt = T1;
-      switch (nkc) {
-        case 1: launch_contract<1>(c, b, TArgs(), true, nb); break;
-        case 2: launch_contract<2>(c, b, TArgs(), true, nb); break;
-        case 4: launch_contract<4>(c, b, TArgs(), true, nb); break;
-        default: launch_contract<8>(c, b, TArgs(), true, nb); break;
-      }
-      FASST_LAUNCH_CHECK();
-      ye += ne;
-      zb += nb;
-    }
-    c->nce_run = ye;
-    c->ncb_run = zb;
-    fb_done = true;
-  } else {
-    launch_estep(c, e, c->nchunk_e);
-    FASST_LAUNCH_CHECK();
-    if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
-  }
+  launch_estep(c, e, c->nchunk_e);
+  FASST_LAUNCH_CHECK();
+  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
   prof_begin(c, KLL);
-  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nce_run * c->nft, ll_dev,
+  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
                                      1.0 / ((double)c->F * (double)c->T), c->halt);
   prof_end(c, KLL);
   FASST_LAUNCH_CHECK();
@@ -3446,7 +2863,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     m.Fp = c->Fp;
     m.J = J;
     m.R = c->R;
-    m.nchunk = c->nce_run;
+    m.nchunk = c->nchunk_e;
     m.nacc = c->nacc;
     m.conv_update = c->conv ? 1 : 0;
     m.invT = 1.0 / (double)c->T;
@@ -3507,7 +2924,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   t.ntt = c->ntt;
   t.fpc = c->fpc_t;
   t.cp = t.pw = t.oth = nullptr;
-  t.cnt = c->tw_fused ? c->tcnt.p : nullptr;
   t.omega = omega;
   TUArgs tu;
   tu.TW = c->TW.p;
@@ -3532,7 +2948,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   u.Fp = c->Fp;
   u.KP = c->KP;
   u.J = J;
-  u.nchunk = c->ncb_run;
+  u.nchunk = c->nchunk_b;
   u.omega = omega;
   u.bden = nullptr;
   for (int j = 0; j < kMaxJ; ++j) {
@@ -3542,15 +2958,13 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     t.tw_free[j] = tu.tw_free[j] = in ? c->tw_free[j] : 0;
     u.fb_free[j] = in ? c->fb_free[j] : 0;
   }
-  if (!fb_done) {
-    switch (nkc) {
-      case 1: launch_contract<1>(c, b, t, true); break;
-      case 2: launch_contract<2>(c, b, t, true); break;
-      case 4: launch_contract<4>(c, b, t, true); break;
-      default: launch_contract<8>(c, b, t, true); break;
-    }
-    FASST_LAUNCH_CHECK();
+  switch (nkc) {
+    case 1: launch_contract<1>(c, b, t, true); break;
+    case 2: launch_contract<2>(c, b, t, true); break;
+    case 4: launch_contract<4>(c, b, t, true); break;
+    default: launch_contract<8>(c, b, t, true); break;
   }
+  FASST_LAUNCH_CHECK();
   prof_begin(c, KFBU);
   (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
                 fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
@@ -3613,12 +3027,10 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     default: launch_contract<8>(c, b, t, false); break;
   }
   FASST_LAUNCH_CHECK();
-  if (!c->tw_fused) {   // else applied by the contraction's last arrivers
-    prof_begin(c, KTWU);
-    k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
-    prof_end(c, KTWU);
-    FASST_LAUNCH_CHECK();
-  }
+  prof_begin(c, KTWU);
+  k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
+  prof_end(c, KTWU);
+  FASST_LAUNCH_CHECK();
   return launch_renorm(c, iter);
 }
 
@@ -3657,9 +3069,6 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->nft = c->Fp / kTile;
   c->ntt = c->Tp / kTile;
   int st = FASST_OK;
-  if (const char *ab = getenv("FASST_ABLATE")) c->ablate = atoi(ab);  // profiling only
-  if (const char *nf = getenv("FASST_NOFORK")) c->nofork = atoi(nf);  // A/B only
-  if (const char *es = getenv("FASST_ESTEP_SPLIT")) c->estep_split = atoi(es);  // A/B only
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -4067,7 +3476,7 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   // iteration i halts every later kernel on the device (HALT_GUARD), and the
   // host reads the flags once at the end.  Profiling keeps one sync per
   // iteration so the per-kernel events can be folded.
-  c->halt = c->ablate ? nullptr : c->flags.p + kFlagHalt;
+  c->halt = c->flags.p + kFlagHalt;
   const int sync_every = c->prof ? 1 : n_iter;
   int done = 0;
   for (int it = 0; it < n_iter; ++it) {
@@ -4085,7 +3494,7 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
     if (c->h_flags[kFlagHalt] || c->h_flags[0]) break;
   }
   c->halt = nullptr;
-  if (c->h_flags[0] && !c->ablate) {
+  if (c->h_flags[0]) {
     set_error("Singular Matrix");
     return FASST_ERR_SINGULAR;
   }

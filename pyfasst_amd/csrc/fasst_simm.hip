@@ -1013,7 +1013,6 @@ static SkinnySplit wmt_split(int F, int N, long slots) {
   const int lo = std::max(std::max(1, (F + kWmtMaxChunk - 1) / kWmtMaxChunk),
                           (int)std::min<long>(16, (2 * slots + bx - 1) / bx));
   int nz = round_split(bx, lo, std::max(lo, std::min(16, F / 64)), slots);
-  if (const char *v = getenv("FASST_WMT_NZ")) nz = std::max(1, atoi(v));   // A/B knob
   nz = std::max(nz, (F + kWmtMaxChunk - 1) / kWmtMaxChunk);
   const int kchunk = ((F + nz - 1) / nz + 15) / 16 * 16;
   return {(F + kchunk - 1) / kchunk, kchunk};
@@ -1021,8 +1020,7 @@ static SkinnySplit wmt_split(int F, int N, long slots) {
 static SkinnySplit hmt_split(int F, int N, long slots) {
   const long by = (F + 63) / 64;
   const int hi = std::max(1, std::min(32, N / 256));
-  int nz = round_split(by, std::min(hi, (int)std::max<long>(1, slots / (2 * by))), hi, slots);
-  if (const char *v = getenv("FASST_HMT_NZ")) nz = std::max(1, atoi(v));   // A/B knob
+  const int nz = round_split(by, std::min(hi, (int)std::max<long>(1, slots / (2 * by))), hi, slots);
   const int kchunk = ((N + nz - 1) / nz + 31) / 32 * 32;
   return {(N + kchunk - 1) / kchunk, kchunk};
 }

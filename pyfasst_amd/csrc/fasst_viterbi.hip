@@ -583,8 +583,7 @@ int viterbi_tracking(int device, int n_states, int n_frames, const double *log_d
   int spw = 0, wpt = 1, nu = 0;
   {
     const int lo_spw = (S + 239) / 240;
-    int want = std::max(lo_spw, (S + 95) / 96);
-    if (const char *v = getenv("FASST_VT_SPW")) want = std::max(lo_spw, atoi(v));   // A/B only
+    const int want = std::max(lo_spw, (S + 95) / 96);
     for (int c = std::min(want, kVtPersistThreads / 64); c >= lo_spw && c >= 1; --c) {
       const int cw = std::max(1, (kVtPersistThreads / 64) / c);
       const int cn = (((S + cw - 1) / cw + 127) / 128) * 2;
@@ -620,8 +619,6 @@ int viterbi_tracking(int device, int n_states, int n_frames, const double *log_d
     // workgroups store (S = 1092: 43.5 ms per track without the wait, 38.5
     // with it, 39-44 ms with 10 / 16 / 19 / 22)
     int sleep0 = 13, sleepr = 1;   // in s_sleep(1) units of 64 clocks
-    if (const char *v = getenv("FASST_VT_SLEEP0")) sleep0 = atoi(v);   // A/B only
-    if (const char *v = getenv("FASST_VT_SLEEPR")) sleepr = atoi(v);   // A/B only
     void *args[] = {&pTT, &ldt, &pDT, &ldd, &ppr, &nS, &nN, &nspw, &nwpt,
                     &pante, &lda, &pcl, &pg, &pab, &pprobe, &sleep0, &sleepr};
     // the cooperative launch checks that the whole grid is co-resident

@@ -674,6 +674,66 @@ def run_pipeline_mqt():
     print("pipeline_mqt", {k: np.shape(v) for k, v in out.items()})
 
 
+def run_pipeline_suimm():
+    """The unvoiced-lead (SUIMM) stages of SeparateLeadProcess on the signal
+    and settings of run_pipeline: after autoMelSepAndWrite(maxFrames=60),
+    estimStereoSUIMMParamsWriteSeps(maxFrames=60) (SeparateLeadStereoTF.py:
+    1585-1675: per chunk Stereo_SIMM on WUF0 = [WF0 | 1] with HGAMMA fixed,
+    the '_VUIMM' masks, the overlap-add); then, into a second output
+    directory (setOutputFileNames, :540-585), the un-chunked
+    estimStereoSIMMParams (:1677-1713) + writeSeparatedSignals and
+    estimStereoSUIMMParams (:1715-1760) + writeSeparatedSignalsWithUnvoice."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import shutil
+    import numpy as np
+    import scipy.io.wavfile as wf
+    from pyfasst.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    from pyfasst.SeparateLeadStereo.tracking import tracking as TR
+
+    def tracker(S_, N_, logD, prior, logT, verbose=False):
+        return TR.viterbiTrackingArray(logD[:S_, :N_], prior[:S_], logT[:S_, :S_])
+    SL.viterbiTrackingArray = tracker
+    work = "/tmp/golden_pipeline_suimm"
+    shutil.rmtree(work, ignore_errors=True)
+    os.makedirs(work)
+    os.chdir(work)
+    fs = 8000
+    x = pipeline_signal(fs, 9000)
+    wav = os.path.join(work, "mix.wav")
+    wf.write(wav, fs, x)
+    np.random.seed(3)
+    proc = SL.SeparateLeadProcess(wav, windowSize=0.0464, nbIter=3, numCompAccomp=6, minF0=100,
+                                  maxF0=800, stepNotes=4, K_numFilters=3, P_numAtomFilters=10,
+                                  verbose=False, outputDirSuffix='out')
+    proc.autoMelSepAndWrite(maxFrames=60)
+    hg0 = np.array(proc.SIMMParams['HGAMMA'])
+    proc.estimStereoSUIMMParamsWriteSeps(maxFrames=60)
+    out = {'wav': x, 'fs': np.array(fs), 'HGAMMA_in': hg0,
+           'HGAMMA_suimm': np.array(proc.SIMMParams['HGAMMA']),
+           'WM_suimm': np.array(proc.SIMMParams['WM']),
+           'lead': wf.read(proc.files['voc_output_file'])[1],
+           'lead_vuimm': wf.read(proc.files['voc_output_file'][:-4] + '_VUIMM.wav')[1],
+           'acc_vuimm': wf.read(proc.files['mus_output_file'][:-4] + '_VUIMM.wav')[1]}
+    proc.setOutputFileNames('out2')
+    proc.estimStereoSIMMParams()
+    proc.writeSeparatedSignals()
+    P = proc.SIMMParams
+    out.update({'whole_HF0': np.array(P['HF0']), 'whole_HGAMMA': np.array(P['HGAMMA']),
+                'whole_alphaR': np.array(P['alphaR']), 'whole_alphaL': np.array(P['alphaL']),
+                'whole_lead': wf.read(proc.files['voc_output_file'])[1],
+                'whole_acc': wf.read(proc.files['mus_output_file'])[1]})
+    proc.estimStereoSUIMMParams()
+    proc.writeSeparatedSignalsWithUnvoice()
+    out.update({'whole_HUF0': np.array(P['HUF0']), 'whole_HGAMMA_u': np.array(P['HGAMMA']),
+                'whole_alphaR_u': np.array(P['alphaR']), 'whole_betaR_u': np.array(P['betaR']),
+                'whole_lead_vuimm': wf.read(proc.files['voc_output_file'][:-4] + '_VUIMM.wav')[1],
+                'whole_acc_vuimm': wf.read(proc.files['mus_output_file'][:-4] + '_VUIMM.wav')[1]})
+    np.savez_compressed(os.path.join(HERE, "pipeline_suimm.npz"), **out)
+    print("pipeline_suimm", {k: np.shape(v) for k, v in out.items()})
+
+
 def run_inv_herm():
     """Known-answer data of pyfasst_tests/pyfasst/tools/test_signalTools.py:27-64."""
     import numpy as np
@@ -700,7 +760,7 @@ if __name__ == "__main__":
          "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0, "nmfinit_same": lambda: run_nmfinit(True),
          "nmfinit_indiv": lambda: run_nmfinit(False), "pipeline": run_pipeline,
          "wf0_cqt": run_wf0_cqt, "pipeline_mqt": run_pipeline_mqt,
-         "pipeline_nnls": run_pipeline_nnls}.get(
+         "pipeline_nnls": run_pipeline_nnls, "pipeline_suimm": run_pipeline_suimm}.get(
             name, lambda: run_case(name))()
         sys.exit(0)
     import make_scratch_ref
@@ -708,6 +768,6 @@ if __name__ == "__main__":
         make_scratch_ref.build(SCRATCH)
     names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0", "nmfinit_same",
                               "nmfinit_indiv", "pipeline", "wf0_cqt", "pipeline_mqt",
-                              "pipeline_nnls"] + list(CASES))
+                              "pipeline_nnls", "pipeline_suimm"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

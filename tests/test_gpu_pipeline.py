@@ -121,3 +121,56 @@ def test_auto_melody_separation_nnls_init_vs_reference(tmp_path, monkeypatch):
         y = wf.read(proc.files[key])[1].astype(np.int64)
         assert y.shape == ref.shape
         assert np.max(np.abs(y - ref.astype(np.int64))) <= 2
+
+
+def test_unvoiced_suimm_stages_vs_reference(tmp_path, monkeypatch):
+    """The unvoiced-lead (SUIMM) stages (tests/golden/pipeline_suimm.npz):
+    after autoMelSepAndWrite, estimStereoSUIMMParamsWriteSeps
+    (SeparateLeadStereoTF.py:1585-1675: Stereo_SIMM per chunk on WUF0 = [WF0 |
+    1], NF0 + 1 = 145 columns -- the odd-width path of the NF0-sized
+    products -- with HGAMMA held fixed, '_VUIMM' masks, overlap-add); then
+    setOutputFileNames and the un-chunked estimStereoSIMMParams /
+    estimStereoSUIMMParams with their WAVs (:1677-1760).  WAVs within 2 LSB,
+    parameters to 1e-8 of the reference run."""
+    from pyfasst_amd.SeparateLeadStereo import SeparateLeadStereoTF as SL
+    monkeypatch.chdir(tmp_path)
+    g = load("pipeline_suimm")
+    wav = os.path.join(str(tmp_path), "mix.wav")
+    wf.write(wav, int(g['fs']), g['wav'])
+    np.random.seed(3)
+    proc = SL.SeparateLeadProcess(wav, windowSize=0.0464, nbIter=3, numCompAccomp=6, minF0=100,
+                                  maxF0=800, stepNotes=4, K_numFilters=3, P_numAtomFilters=10,
+                                  verbose=False, outputDirSuffix='out')
+    proc.autoMelSepAndWrite(maxFrames=60)
+    assert rel(proc.SIMMParams['HGAMMA'], g['HGAMMA_in']) < 1e-8
+    proc.estimStereoSUIMMParamsWriteSeps(maxFrames=60)
+    P = proc.SIMMParams
+    assert P['WUF0'].shape[1] == P['WF0'].shape[1] + 1
+    np.testing.assert_array_equal(P['WUF0'][:, -1], 1.0)
+    assert rel(P['HGAMMA'], g['HGAMMA_suimm']) < 1e-8     # updateHGAMMA=False
+    assert rel(P['WM'], g['WM_suimm']) < 1e-8
+
+    def check_wav(path, ref):
+        y = wf.read(path)[1].astype(np.int64)
+        assert y.shape == ref.shape
+        assert np.max(np.abs(y - ref.astype(np.int64))) <= 2, path
+    check_wav(proc.files['voc_output_file'], g['lead'])
+    check_wav(proc.files['voc_output_file'][:-4] + '_VUIMM.wav', g['lead_vuimm'])
+    check_wav(proc.files['mus_output_file'][:-4] + '_VUIMM.wav', g['acc_vuimm'])
+    proc.setOutputFileNames('out2')
+    assert proc.files['outputDir'].endswith('/out2/') and os.path.isdir(proc.files['outputDir'])
+    proc.estimStereoSIMMParams()
+    assert rel(P['HF0'], g['whole_HF0']) < 1e-8
+    assert rel(P['HGAMMA'], g['whole_HGAMMA']) < 1e-8
+    assert abs(P['alphaR'] - g['whole_alphaR']) <= 1e-8 * abs(g['whole_alphaR'])
+    proc.writeSeparatedSignals()
+    check_wav(proc.files['voc_output_file'], g['whole_lead'])
+    check_wav(proc.files['mus_output_file'], g['whole_acc'])
+    proc.estimStereoSUIMMParams()
+    assert rel(P['HUF0'], g['whole_HUF0']) < 1e-8
+    assert rel(P['HGAMMA'], g['whole_HGAMMA_u']) < 1e-8
+    assert rel(P['betaR'], g['whole_betaR_u']) < 1e-8
+    proc.writeSeparatedSignalsWithUnvoice()
+    check_wav(proc.files['voc_output_file'][:-4] + '_VUIMM.wav', g['whole_lead_vuimm'])
+    check_wav(proc.files['mus_output_file'][:-4] + '_VUIMM.wav', g['whole_acc_vuimm'])
+
