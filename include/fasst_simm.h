@@ -69,6 +69,12 @@ int simm_separate(simm_ctx *ctx, const double *XR, const double *XL, double *VR,
 int simm_get_params(simm_ctx *ctx, double *HGAMMA, double *HPHI, double *HF0, double *HM,
                     double *WM, double *alpha, double *betaR, double *betaL);
 
+/* NF0-sized products (SF0 = WF0 HF0 and WF0^T [num | den], SIMM.py:623-674,
+ * :799) dispatched since the library was loaded, per kernel: the
+ * hand-written k_dgemm2 (the default) and the generic k_gemm
+ * (FASST_SIMM_GEMM=2); either pointer may be NULL */
+int simm_nf0_product_counts(long *dgemm2_launches, long *kgemm_launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,8 @@ SIGNATURES = {
     "simm_reco_error": (ctypes.c_int, [_vp, _dp]),
     "simm_separate": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp]),
     "simm_get_params": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    "simm_nf0_product_counts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_long),
+                                               ctypes.POINTER(ctypes.c_long)]),
     # include/fasst_nmf.h
     "nmf_create": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(_vp)]),
     "nmf_destroy": (ctypes.c_int, [_vp]),

@@ -97,6 +97,14 @@ struct DBuf {
     FASST_HIP(hipDeviceSynchronize());
     return FASST_OK;
   }
+  // scratch that every reader writes before it reads: no zero-fill, no sync
+  int alloc_uninit(size_t count) {
+    release();
+    if (count == 0) return FASST_OK;
+    FASST_HIP(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+    return FASST_OK;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;

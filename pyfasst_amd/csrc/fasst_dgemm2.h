@@ -73,7 +73,14 @@ __device__ __forceinline__ double d2_mfma(double a, double b, double c) {
 
 // (FASST_NO_LDS_PAIRING: keep the operand reads as ds_read_b64, 2 LDS cycles
 // each, not paired into ds_read2_b64 at 8)
-template <class CF, bool A4 = false, bool B4 = false>
+// BUF (16-byte pieces only): the pieces as raw-buffer LDS-DMA loads
+// (buffer_load_dwordx4 ... lds) off one wave-uniform resource per operand whose
+// size is exactly its K rows, so rows k >= K read 0 without a test; a piece's
+// per-lane byte offset is loop-invariant (columns past M / N: an offset past
+// the resource, 0 as well) and the chunk's row offset rides in an SGPR.  The
+// global_load_lds form selects the zero buffer per lane, which hipcc turns
+// into exec-masked branches around every load.
+template <class CF, bool A4 = false, bool B4 = false, bool BUF = false>
 __global__ __launch_bounds__(CF::NT, CF::OCC) FASST_NO_LDS_PAIRING
 void k_dgemm2(const Dgemm2Args g) {
   constexpr int NS = CF::NS, BK = CF::BK, BM = CF::BM, BN = CF::BN, NW = CF::NW;
@@ -110,9 +117,43 @@ void k_dgemm2(const Dgemm2Args g) {
       }
     }
   };
+  // BUF: per-piece lane offsets and LDS destinations (pieces r < PCA / NW of
+  // a wave are A pieces: p = wv + NW r < PCA)
+  constexpr int RPB = (CF::PCA + CF::PCB) / NW;
+  static_assert(!BUF || (CF::PCA % NW == 0 && !A4 && !B4), "BUF: 16-byte pieces, whole A rows per wave");
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(g.A), 0, BUF ? (int)((size_t)g.K * g.lda * sizeof(double)) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(g.B), 0, BUF ? (int)((size_t)g.K * g.ldb * sizeof(double)) : 0, 0x00020000);
+  unsigned voff[BUF ? RPB : 1];
+  int ldso[BUF ? RPB : 1];
+  if constexpr (BUF) {
+#pragma unroll
+    for (int r = 0; r < RPB; ++r) {
+      const int p = wv + NW * r;
+      const bool isA = r < CF::PCA / NW;
+      const int q = isA ? p : p - CF::PCA;
+      const int per = isA ? BM / 128 : BN / 128;
+      const int kr = q / per, sg = q % per;
+      const int col = (isA ? m0 : n0) + 128 * sg + 2 * lane;
+      const int lim = isA ? g.M : g.N, ld = isA ? g.lda : g.ldb;
+      voff[r] = col < lim ? (unsigned)((kr * ld + col) * (int)sizeof(double)) : 0x80000000u;
+      ldso[r] = isA ? kr * PA + 128 * sg : BK * PA + kr * PB + 128 * sg;
+    }
+  }
   // chunk c: pieces wv, wv + NW, ... of the PCA A pieces then the PCB B pieces
   auto issue = [&](int c) {
     double *st = smem + (c % NS) * SS;
+    if constexpr (BUF) {
+#pragma unroll
+      for (int r = 0; r < RPB; ++r) {
+        const bool isA = r < CF::PCA / NW;
+        const int so = c * BK * (isA ? g.lda : g.ldb) * (int)sizeof(double);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (d2_lds_t *)(st + ldso[r]), 16,
+                                                 (int)voff[r], so, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < (CF::PCA + CF::PCB) / NW; ++r) {
       const int p = wv + NW * r;

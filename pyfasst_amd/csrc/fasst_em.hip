@@ -50,6 +50,26 @@ void set_error(const char *fmt, ...) {
     if ((h) && *(volatile const int *)(h)) return;      \
   } while (0)
 
+// XCD-aware logical block (FASST_XCD): workgroups b, b + 8, ... of a launch
+// share an XCD (dispatch is round-robin over the 8 XCDs, for speed only,
+// never correctness); the bijective remap of cdna_hip_programming.md gives
+// each XCD a contiguous run of the logical (x fastest, z slowest) sequence,
+// so the blocks that re-read one operand slice (the E-step's TW chunk, the
+// contractions' W / (FW H)^T slices) meet in one 4 MB L2
+#ifndef FASST_XCD
+#define FASST_XCD 0
+#endif
+__device__ __forceinline__ dim3 xcd_block() {
+  const int nx = gridDim.x, ny = gridDim.y, n = nx * ny * gridDim.z;
+  const int b = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  int L = b;
+  if (FASST_XCD) {
+    const int q = n / 8, r = n % 8, x = b % 8;
+    L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+  }
+  return dim3(L % nx, (L / nx) % ny, L / (nx * ny));
+}
+
 __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -239,6 +259,9 @@ __device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsign
 #ifndef ESTEP_PF
 #define ESTEP_PF 0
 #endif
+#ifndef ESTEP_SWP
+#define ESTEP_SWP 0
+#endif
 #ifndef ESTEP_RHO_AUX
 #define ESTEP_RHO_AUX 2
 #endif
@@ -263,7 +286,8 @@ void k_estep_mx(const EArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fl = lane & 15, tq = lane >> 4;
-  const int f0 = blockIdx.x * 16;
+  const dim3 bi = xcd_block();   // x: 16-bin tile, y: frame chunk
+  const int f0 = bi.x * 16;
   const int f = f0 + fl;
   double *slab = s_slab + wv * S::SLAB;
 
@@ -316,7 +340,7 @@ void k_estep_mx(const EArgs a) {
   }
   double ll = 0.0, lm = 1.0, lev = 0.0, xmin = 1.0;
 
-  const int tb = a.tbase + blockIdx.y * a.tpc;
+  const int tb = a.tbase + bi.y * a.tpc;
   const int te = min(tb + a.tpc, a.ntt);
   // SA: wave-uniform buffer resources (SGPRs, formed on the scalar unit) +
   // 32-bit per-lane byte offsets instead of one 64-bit VALU address
@@ -396,8 +420,9 @@ void k_estep_mx(const EArgs a) {
                      WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
     }
     const double *cj = s_cj + lofs + fl;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    // point i of the lane's four (frame t0 + tq + 4 i): Sigma_x, its guarded
+    // inverse, loglik, P = Cx S, N = S Cx S - S, and rho stored; no LDS
+    auto pt_valu = [&](int i, double (&P)[8], double (&N)[4]) {
       const int t = t0 + tq + 4 * i;
       const double x00 = cxv[0][i], x11 = cxv[1][i], xr = cxv[2][i], xi = cxv[3][i];
       double V[J];
@@ -431,37 +456,18 @@ void k_estep_mx(const EArgs a) {
         ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
       }
       // P = Cx S, N = S Cx S - S = P^H S - S
-      const double p00r = x00 * i0 + xr * ior + xi * ioi, p00i = xi * ior - xr * ioi;
-      const double p01r = x00 * ior + xr * i1, p01i = x00 * ioi + xi * i1;
-      const double p10r = xr * i0 + x11 * ior, p10i = -xi * i0 - x11 * ioi;
-      const double p11r = xr * ior + xi * ioi + x11 * i1, p11i = xr * ioi - xi * ior;
-      const double n00 = p00r * i0 + (p10r * ior - p10i * ioi) - i0;
-      const double n11 = (p01r * ior + p01i * ioi) + p11r * i1 - i1;
-      const double n01r = p00r * ior + p00i * ioi + p10r * i1 - ior;
-      const double n01i = p00r * ioi - p00i * ior - p10i * i1 - ioi;
-      // this point's MFMA operands -> the wave's slab (reader layout)
-#pragma unroll
-      for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
-      wr[(S::SP + 0) * 64 + 0] = p00r;
-      wr[(S::SP + 0) * 64 + 1] = p00i;
-      wr[(S::SP + 0) * 64 + 2] = p01r;
-      wr[(S::SP + 0) * 64 + 3] = p01i;
-      wr[(S::SP + 1) * 64 + 0] = p10r;
-      wr[(S::SP + 1) * 64 + 1] = p10i;
-      wr[(S::SP + 1) * 64 + 2] = p11r;
-      wr[(S::SP + 1) * 64 + 3] = p11i;
-      wr[S::SN * 64 + 0] = n00;
-      wr[S::SN * 64 + 1] = n11;
-      wr[S::SN * 64 + 2] = n01r;
-      wr[S::SN * 64 + 3] = n01i;
-      {
-        int p = 0;
-#pragma unroll
-        for (int j1 = 0; j1 < J; ++j1)
-#pragma unroll
-          for (int j2 = j1; j2 < J; ++j2, ++p)
-            wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
-      }
+      P[0] = x00 * i0 + xr * ior + xi * ioi;   // p00r
+      P[1] = xi * ior - xr * ioi;              // p00i
+      P[2] = x00 * ior + xr * i1;              // p01r
+      P[3] = x00 * ioi + xi * i1;              // p01i
+      P[4] = xr * i0 + x11 * ior;              // p10r
+      P[5] = -xi * i0 - x11 * ioi;             // p10i
+      P[6] = xr * ior + xi * ioi + x11 * i1;   // p11r
+      P[7] = xr * ioi - xi * ior;              // p11i
+      N[0] = P[0] * i0 + (P[4] * ior - P[5] * ioi) - i0;          // n00
+      N[1] = (P[2] * ior + P[3] * ioi) + P[6] * i1 - i1;          // n11
+      N[2] = P[0] * ior + P[1] * ioi + P[4] * i1 - ior;           // n01r
+      N[3] = P[0] * ioi - P[1] * ior - P[5] * i1 - ioi;           // n01i
       // hat_W[j] = mean over the ranks of j of |V^2 a_r^H N a_r + V| (:727-729,
       // :413-414) in the rank-merged form |V^2 (sum_r a_r^H N a_r) / rk + V|
       // (each rank's term is a posterior second moment, >= 0: the two forms
@@ -474,8 +480,8 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const double Vj = V[j];
-        const double qa = (cj[(j * 4 + 0) * 16] * n00 + cj[(j * 4 + 1) * 16] * n11) +
-                          2.0 * (cj[(j * 4 + 2) * 16] * n01r + cj[(j * 4 + 3) * 16] * n01i);
+        const double qa = (cj[(j * 4 + 0) * 16] * N[0] + cj[(j * 4 + 1) * 16] * N[1]) +
+                          2.0 * (cj[(j * 4 + 2) * 16] * N[2] + cj[(j * 4 + 3) * 16] * N[3]);
         const double q = RKU == 1 ? qa : qa * inv_rk[j];
         const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
         if constexpr (SA)
@@ -484,21 +490,50 @@ void k_estep_mx(const EArgs a) {
         else
           __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
       }
-      // the slab writes above must land before the cross-lane reads below
-      // (LDS is in order within a wave; this keeps the compiler in order too)
+    };
+    // point i's MFMA operands -> the wave's slab (reader layout)
+    auto pt_write = [&](int i, const double (&P)[8], const double (&N)[4]) {
+      double V[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) V[j] = v[j][i];
+#pragma unroll
+      for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        wr[(S::SP + 0) * 64 + c] = P[c];
+        wr[(S::SP + 1) * 64 + c] = P[4 + c];
+        wr[S::SN * 64 + c] = N[c];
+      }
+      int p = 0;
+#pragma unroll
+      for (int j1 = 0; j1 < J; ++j1)
+#pragma unroll
+        for (int j2 = j1; j2 < J; ++j2, ++p)
+          wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
+    };
+    // (J > 4 always pipelines: the other form trips ROCm 7.2's AGPR-copy
+    // rewrite pass at J = 8, K = 64)
+    constexpr bool SWP = ESTEP_SWP || J > 4;
+    auto slab_fence = [&]() {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // all operands of the 4 bin groups in flight at once, then the MFMAs
-      // (read -> wait -> MFMA one at a time left the LDS latency exposed)
-      {
-      const int g2 = 0;
+    };
+    // the slab's operands of the 4 bin groups in flight at once, then the
+    // MFMAs (read -> wait -> MFMA one at a time left the LDS latency exposed);
+    // ESTEP_SWP: the next point's VALU work sits between the reads and the
+    // MFMAs (its slab writes after them)
+    auto mfma_pass = [&](auto between) {
       double opd[4][S::NSET];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int q = 0; q < S::NSET; ++q) opd[g][q] = rd[g * S::GS + q * 64];
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SWP) {
+        between();
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
 #pragma unroll
@@ -510,12 +545,31 @@ void k_estep_mx(const EArgs a) {
         for (int h = 0; h < NPG; ++h)
           pacc[g][h] = mfma44(opd[g][S::SV2 + h], opd[g][S::SN], pacc[g][h]);
       }
-      (void)g2;
+    };
+    if constexpr (SWP) {
+      double Pc[8], Nc[4];
+      pt_valu(0, Pc, Nc);
+      pt_write(0, Pc, Nc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        slab_fence();   // point i's slab writes land before the cross-lane reads
+        double Pn[8], Nn[4];
+        mfma_pass([&]() {
+          if (i < 3) pt_valu(i + 1, Pn, Nn);
+        });
+        slab_fence();   // point i + 1's writes must not overtake point i's reads
+        if (i < 3) pt_write(i + 1, Pn, Nn);
       }
-      // the next point's slab writes must not overtake these reads
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double P[8], N[4];
+        pt_valu(i, P, N);
+        pt_write(i, P, N);
+        slab_fence();   // the slab writes land before the cross-lane reads
+        mfma_pass([]() {});
+        slab_fence();   // the next point's writes must not overtake these reads
+      }
     }
     // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
     lev += (double)__builtin_amdgcn_frexp_exp(lm);
@@ -553,10 +607,10 @@ void k_estep_mx(const EArgs a) {
     const int u = idx >> 4, ff = idx & 15;
     const double x = s_red[(0 * NACC + u) * 16 + ff] + s_red[(1 * NACC + u) * 16 + ff] +
                      s_red[(2 * NACC + u) * 16 + ff] + s_red[(3 * NACC + u) * 16 + ff];
-    a.part[((size_t)(a.ybase + blockIdx.y) * a.Fp + f0 + ff) * NACC + u] = x;
+    a.part[((size_t)(a.ybase + bi.y) * a.Fp + f0 + ff) * NACC + u] = x;
   }
   if (tid == 0)
-    a.llpart[(a.ybase + blockIdx.y) * a.nft + blockIdx.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+    a.llpart[(a.ybase + bi.y) * a.nft + bi.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
 }
 
 // sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
@@ -932,7 +986,8 @@ template <int NKC, int FPW, bool DEN = false>
 __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   HALT_GUARD(a.halt);
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
-  const int ft0 = blockIdx.x * FPW, j = blockIdx.y;
+  const dim3 bi = xcd_block();   // x: bin-tile group, y: source, z: frame chunk
+  const int ft0 = bi.x * FPW, j = bi.y;
   if (!a.fb_free[j]) return;
   d4 num[FPW][NKC], den[DEN ? FPW : 1][NKC];
 #pragma unroll
@@ -946,7 +1001,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
 #ifndef FB_REVERSE
 #define FB_REVERSE 0
 #endif
-  const int zc = FB_REVERSE ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
+  const int zc = FB_REVERSE ? (int)gridDim.z - 1 - (int)bi.z : (int)bi.z;
   const int tb = a.tbase + zc * a.tpc, te = min(tb + a.tpc, a.ntt);
   const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
   const double *rdj = DEN ? a.hatW2 + (size_t)j * a.Tp * a.Fp : nullptr;
@@ -1297,7 +1352,8 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   HALT_GUARD(a.halt);
   constexpr int NKS = 4 * NKC;
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
-  const int tt0 = blockIdx.x * TPW, j = blockIdx.y;
+  const dim3 bi = xcd_block();   // x: frame-tile group, y: source, z: bin chunk
+  const int tt0 = bi.x * TPW, j = bi.y;
   if (!a.tw_free[j]) return;
   double bt[TPW][NKS];
 #pragma unroll
@@ -1312,7 +1368,7 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   for (int p = 0; p < TPW; ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
-  const int fb = blockIdx.z * a.fpc, fe = min(fb + a.fpc, a.nft);
+  const int fb = bi.z * a.fpc, fe = min(fb + a.fpc, a.nft);
   // the V tiles' bin rows are permuted (lane fl's A row is bin
   // 4 (fl & 3) + (fl >> 2)) so that a lane's four D values are the four
   // consecutive bins 4 tq .. 4 tq + 3: its rho values arrive as two 16-byte
@@ -1403,7 +1459,7 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
       }
     }
   }
-  const size_t base = ((size_t)blockIdx.z * a.J + j) * a.Tp;
+  const size_t base = ((size_t)bi.z * a.J + j) * a.Tp;
 #pragma unroll
   for (int p = 0; p < TPW; ++p) {
     if (tt0 + p >= a.ntt) break;
@@ -2103,6 +2159,16 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   // update runs over the free 'inst' sources with the rest held fixed
   const int conv = c->convm == (1u << J) - 1u ? 1 : 0;
   c->conv = conv;
+  // the E-step addresses TW through a raw buffer resource with 32-bit byte
+  // offsets (j KP + 4 s) Tp 8 (J <= 4, k_estep_mx's SA form)
+  {
+    const int KPc = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : (kmax <= 64 ? 64 : 128));
+    if (J <= 4 && (size_t)J * KPc * c->Tp * sizeof(double) >= (1ull << 31)) {
+      set_error("J %d x K %d x T %d: the TW plane passes the E-step's 2 GB buffer offsets", J,
+                KPc, c->T);
+      return FASST_ERR_UNSUPPORTED;
+    }
+  }
   c->KP = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : (kmax <= 64 ? 64 : 128));
   c->roff[0] = 0;
   for (int j = 0; j < J; ++j) {
@@ -2764,6 +2830,18 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
                 "and no time blobs");
       return FASST_ERR_UNSUPPORTED;
     }
+  }
+  if (!c->conv) {
+    // a free 'conv' component next to other components: the reference's conv
+    // solve (audioModel.py:856-857) passes the full hat_Rss[f].T against the
+    // free components' right-hand side only, and np.linalg.solve raises
+    for (int j = 0; j < J; ++j)
+      if ((c->convm >> j & 1u) && c->spat_free[j]) {
+        set_error("spatial component %d is 'conv' and free next to other components: the "
+                  "reference's mixing solve (audioModel.py:856-857) raises for this structure",
+                  j);
+        return FASST_ERR_UNSUPPORTED;
+      }
   }
   // (FW.TW)^T and the TW row sums depend only on the previous iteration's
   // parameters: fork them onto the side stream (kept on the main stream

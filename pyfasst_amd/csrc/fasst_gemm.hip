@@ -140,13 +140,13 @@ int gemm(hipStream_t s, const double *A, int lda, const double *const *B, int ld
 // Large plain products on k_dgemm2 (fasst_dgemm2.h) in its product shapes
 // (D2Prod, D2Odd).  The dynamic-LDS limit is a per-device attribute: set
 // before every launch.
-template <class CF, bool A4, bool B4>
+template <class CF, bool A4, bool B4, bool BUF = false>
 static int launch_dgemm2(hipStream_t s, Dgemm2Args g) {
   g.mt = (g.M + CF::BM - 1) / CF::BM;
   g.nt = (g.N + CF::BN - 1) / CF::BN;
-  FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm2<CF, A4, B4>,
+  FASST_HIP(hipFuncSetAttribute((const void *)k_dgemm2<CF, A4, B4, BUF>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)CF::smem));
-  k_dgemm2<CF, A4, B4><<<g.mt * g.nt, CF::NT, CF::smem, s>>>(g);
+  k_dgemm2<CF, A4, B4, BUF><<<g.mt * g.nt, CF::NT, CF::smem, s>>>(g);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
 }
@@ -169,6 +169,13 @@ int dgemm2(hipStream_t s, int M, int N, int K, const double *A, int lda, const d
   g.K = K;
   const bool a16 = lda % 2 == 0 && ((uintptr_t)A & 15) == 0;
   const bool b16 = ldb % 2 == 0 && ((uintptr_t)B & 15) == 0;
+#ifndef FASST_D2BUF
+#define FASST_D2BUF 0
+#endif
+  // raw-buffer pieces: operands within 2 GB (32-bit byte offsets)
+  const bool fits = (size_t)K * lda * sizeof(double) < (1ull << 31) &&
+                    (size_t)K * ldb * sizeof(double) < (1ull << 31);
+  if (FASST_D2BUF && a16 && b16 && fits) return launch_dgemm2<D2Prod, false, false, true>(s, g);
   if (a16 && b16) return launch_dgemm2<D2Prod, false, false>(s, g);
   if (a16) return launch_dgemm2<D2Odd, false, true>(s, g);
   if (b16) return launch_dgemm2<D2Odd, true, false>(s, g);

@@ -38,7 +38,7 @@ struct NnlsArgs {
   const double *Ct;   // [nf][n]
   double *X;          // [n][nf]
   double *L, *Lt;     // [slots][n][n] scratch
-  int *info;          // [nf]: outer iterations, or -1 when maxiter was reached
+  int *info;          // [nf]: iterations (outer + inner steps), or -1 at maxiter
   int n, nf, maxiter;
   double tol, add_eps;   // tol: relative to max |c| of the frame
 };
@@ -172,29 +172,45 @@ __global__ __launch_bounds__(64) void k_nnls(const NnlsArgs a) {
         if (st[i] == 2) st[i] = 0;
       if (lane == 0) s_p = p + 1;
       __syncthreads();
-      // inner loop: step towards z while a coefficient is not positive
+      // secondary loop (Lawson & Hanson's step E): every pass counts one
+      // iteration, the pass that finds z feasible included; scipy 1.15.3 fails
+      // once outer + inner passes reach maxiter (probed: the smallest maxiter
+      // that succeeds is outer + inner + 1)
       while (true) {
+        if (++it >= a.maxiter) break;
         const int pp = s_p;
         bool allpos = true;
         double al = INFINITY;
+        int aj = pp;   // position in P of the coefficient that sets alpha (first on ties)
         for (int i = lane; i < pp; i += 64)
           if (!(t[i] > 0.0)) {
             allpos = false;
             const double xi = x[lst[i]];
-            al = fmin(al, xi / (xi - t[i]));
+            const double ti = xi / (xi - t[i]);
+            if (ti < al) {
+              al = ti;
+              aj = i;
+            }
           }
         allpos = __all(allpos);
         if (allpos) break;
-        if (++it > a.maxiter) break;
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) al = fmin(al, __shfl_xor(al, m, 64));
+        for (int m = 32; m >= 1; m >>= 1) {
+          const double oa = __shfl_xor(al, m, 64);
+          const int oj = __shfl_xor(aj, m, 64);
+          if (oa < al || (oa == al && oj < aj)) {
+            al = oa;
+            aj = oj;
+          }
+        }
         for (int i = lane; i < pp; i += 64) {
           const int k = lst[i];
-          x[k] = x[k] + al * (t[i] - x[k]);
+          x[k] = i == aj ? 0.0 : x[k] + al * (t[i] - x[k]);   // the alpha index lands on 0 exactly
         }
         __syncthreads();
-        // drop the indices that reached zero; rows from the first drop on are
-        // recomputed for the compacted list
+        // drop the indices at zero (the alpha index, and any others rounding
+        // left non-positive); rows from the first drop on are recomputed for
+        // the compacted list
         if (lane == 0) {
           int np_ = 0, r1 = pp;
           for (int i = 0; i < pp; ++i) {
@@ -215,7 +231,7 @@ __global__ __launch_bounds__(64) void k_nnls(const NnlsArgs a) {
         for (int r = s_j; r < np2; ++r) append_row(r, lst[r]);
         solve_z(np2);
       }
-      if (it > a.maxiter) break;
+      if (it >= a.maxiter) break;
       // x = z on P, 0 elsewhere; w = c - G x
       const int pp = s_p;
       for (int i = lane; i < pp; i += 64) x[lst[i]] = t[i];
@@ -226,11 +242,9 @@ __global__ __launch_bounds__(64) void k_nnls(const NnlsArgs a) {
         w[i] = s;
       }
       __syncthreads();
-      ++it;
-      if (it > a.maxiter) break;
     }
     for (int i = lane; i < n; i += 64) a.X[(size_t)i * a.nf + q] = x[i] + a.add_eps;
-    if (lane == 0) a.info[q] = it > a.maxiter ? -1 : it;
+    if (lane == 0) a.info[q] = it >= a.maxiter ? -1 : it;
     __syncthreads();
   }
 }
@@ -258,8 +272,8 @@ int nnls_columns(int device, int m, int n, const double *A, int nf, const double
   DBuf<int> dinfo;
   if ((st = dA.alloc((size_t)m * n)) || (st = dB.alloc((size_t)m * nf)) ||
       (st = dG.alloc((size_t)n * n)) || (st = dCt.alloc((size_t)nf * n)) ||
-      (st = dX.alloc((size_t)n * nf)) || (st = dL.alloc((size_t)slots * n * n)) ||
-      (st = dLt.alloc((size_t)slots * n * n)) || (st = dinfo.alloc(nf)))
+      (st = dX.alloc((size_t)n * nf)) || (st = dL.alloc_uninit((size_t)slots * n * n)) ||
+      (st = dLt.alloc_uninit((size_t)slots * n * n)) || (st = dinfo.alloc(nf)))
     return st;
   FASST_HIP(hipMemcpy(dA.p, A, (size_t)m * n * sizeof(double), hipMemcpyHostToDevice));
   FASST_HIP(hipMemcpy(dB.p, B, (size_t)m * nf * sizeof(double), hipMemcpyHostToDevice));

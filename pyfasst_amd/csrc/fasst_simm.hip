@@ -13,6 +13,7 @@
 // GEMM) -- it saves two F x NF0 x N GEMMs per iteration.
 #include "fasst_gemm.h"
 
+#include <atomic>
 #include <cmath>
 #include <type_traits>
 
@@ -374,7 +375,13 @@ __global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(const SPl p, const doubl
 //   registers, HPHI's chunk columns staged in LDS next to HM's), and a pending
 //   SF0 column scale (HGAMMA's renormalisation of HF0) is applied and written
 //   back here.
-template <bool ST, int KM>
+// V16 (N even: 16-byte aligned frame pairs): lane (fl, tq) loads frames
+//   kc + 8 j + 2 tq + h, h < 2, as one 16-byte load per plane and j < 4
+//   (every load instruction reads 64 contiguous bytes of 16 rows); MFMA
+//   2 j + h contracts them (k = tq).  The staged chunk columns are stored
+//   interleaved, column c at (c & 1) 16 + (c >> 1), so the B reads of one
+//   MFMA stay consecutive in tq (the pitch-34 rows keep them conflict-free).
+template <bool ST, int KM, bool V16 = false>
 __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const double *__restrict__ HM,
                                                         double *__restrict__ out, size_t slab,
                                                         int R, int kchunk) {
@@ -397,19 +404,44 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
   for (int q = 0; q < NO; ++q)
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
+  // chunk column of MFMA j's k = tq, and its staged position
+  auto kcol = [&](int j) { return V16 ? 8 * (j >> 1) + 2 * tq + (j & 1) : tq + 4 * j; };
+  auto kpos = [&](int k) { return V16 ? (k & 1) * 16 + (k >> 1) : k; };
   for (int kc = kb; kc < ke; kc += KC) {
     const size_t base = (size_t)f * N + kc + tq;
     double sfv[8], smv[NC][8], sv[NC][8];
+    if constexpr (V16) {
+      typedef double dv2 __attribute__((ext_vector_type(2)));
+      const size_t b2 = (size_t)f * N + kc + 2 * tq;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool ok = fin && kc + tq + 4 * j < ke;
-      // plain (cached) loads: a lane group reads 32 bytes of a row per
-      // instruction, the rest of the line arrives with the next j's
-      sfv[j] = ok ? p.SF0[base + 4 * j] : 0.0;
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = fin && kc + 8 * j + 2 * tq < ke;   // pairs never straddle ke (even)
+        const dv2 z = {0.0, 0.0};
+        const dv2 a0 = ok ? *(const dv2 *)(p.SF0 + b2 + 8 * j) : z;
+        sfv[2 * j] = a0.x;
+        sfv[2 * j + 1] = a0.y;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        smv[c][j] = ok ? sm[c][base + 4 * j] : 0.0;
-        sv[c][j] = ok ? ss[c][base + 4 * j] : 0.0;
+        for (int c = 0; c < NC; ++c) {
+          const dv2 a1 = ok ? *(const dv2 *)(sm[c] + b2 + 8 * j) : z;
+          const dv2 a2 = ok ? *(const dv2 *)(ss[c] + b2 + 8 * j) : z;
+          smv[c][2 * j] = a1.x;
+          smv[c][2 * j + 1] = a1.y;
+          sv[c][2 * j] = a2.x;
+          sv[c][2 * j + 1] = a2.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = fin && kc + tq + 4 * j < ke;
+        // plain (cached) loads: a lane group reads 32 bytes of a row per
+        // instruction, the rest of the line arrives with the next j's
+        sfv[j] = ok ? p.SF0[base + 4 * j] : 0.0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          smv[c][j] = ok ? sm[c][base + 4 * j] : 0.0;
+          sv[c][j] = ok ? ss[c][base + 4 * j] : 0.0;
+        }
       }
     }
     double hm[(NR * KC + 255) / 256];  // chunk of HM (48 rows), HPHI (8 rows), pend
@@ -428,26 +460,26 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
 #pragma unroll
     for (int t = 0; t < (NR * KC + 255) / 256; ++t) {
       const int e = tid + 256 * t;
-      if (e < NR * KC) sH[(e / KC) * PH + e % KC] = hm[t];
+      if (e < NR * KC) sH[(e / KC) * PH + kpos(e % KC)] = hm[t];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int kk = tq + 4 * j;
+      const int kk = kcol(j), kq = kpos(kk);
       const bool ok = fin && kc + kk < ke;
       if (p.SF0w) {   // (plain store: the line's four 32-byte pieces merge in L2)
-        sfv[j] *= sH[(NR - 1) * PH + kk];
-        if (ok) p.SF0w[base + 4 * j] = sfv[j];
+        sfv[j] *= sH[(NR - 1) * PH + kq];
+        if (ok) p.SF0w[(size_t)f * N + kc + kk] = sfv[j];
       }
       double h[KM];
 #pragma unroll
-      for (int k = 0; k < KM; ++k) h[k] = sH[(48 + k) * PH + kk];
+      for (int k = 0; k < KM; ++k) h[k] = sH[(48 + k) * PH + kq];
       const double sp = sphi_of<KM>(w, h, K);
       double hv[2];
       hat_of<ST>(sfv[j], sp, smv[0][j], ST ? smv[NC - 1][j] : 0.0, aR2, aL2, hv[0], hv[1]);
       double b[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) b[i] = sH[(i * 16 + fl) * PH + kk];
+      for (int i = 0; i < 3; ++i) b[i] = sH[(i * 16 + fl) * PH + kq];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double x, y;
@@ -968,6 +1000,10 @@ struct simm_ctx {
 
 namespace {
 
+// NF0-sized products dispatched per kernel since the library was loaded
+// (simm_nf0_product_counts): which path a run took is observable
+std::atomic<long> g_nf0_dgemm2{0}, g_nf0_kgemm{0};
+
 int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, double *C, int ldc,
             int M, int N, int K) {
   const double *Bs[1] = {B};
@@ -977,8 +1013,11 @@ int gemm_nn(simm_ctx *c, const double *A, int lda, const double *B, int ldb, dou
 
 // SF0 = WF0 HF0 (F x NF0)(NF0 x N)
 int sf0_gemm(simm_ctx *c) {
-  if (c->gemm_kind == 0)
+  if (c->gemm_kind == 0) {
+    ++g_nf0_dgemm2;
     return dgemm2(c->stream, c->F, c->N, c->NF0, c->WF0T.p, c->Fp, c->HF0.p, c->N, c->SF0.p, c->N);
+  }
+  ++g_nf0_kgemm;
   return gemm_nn(c, c->WF0.p, c->NF0, c->HF0.p, c->N, c->SF0.p, c->N, c->F, c->N, c->NF0);
 }
 
@@ -1138,12 +1177,23 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
   const size_t slab = (size_t)no * F * R;
   dim3 grid(1, (F + 63) / 64, sp.nz);
   const SPl p = planes(c, true);
+#ifndef FASST_HMT16
+#define FASST_HMT16 0
+#endif
+  // 16-byte frame pairs: even N (rows 16-byte aligned) and even chunks
+  const bool v16 = FASST_HMT16 && N % 2 == 0 && sp.kchunk % 2 == 0;
   kdispatch(c->K, [&](auto km) {
     constexpr int KM = decltype(km)::value;
     if (c->stereo)
-      k_simm_xy_hmt<true, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+      if (v16)
+        k_simm_xy_hmt<true, KM, true><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+      else
+        k_simm_xy_hmt<true, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
     else
-      k_simm_xy_hmt<false, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+      if (v16)
+        k_simm_xy_hmt<false, KM, true><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+      else
+        k_simm_xy_hmt<false, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
   });
   FASST_LAUNCH_CHECK();
   c->pend = nullptr;
@@ -1251,10 +1301,12 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
   }
   // WF0^T [num | den]: one (NF0 x F)(F x 2N) product
   if (c->gemm_kind == 0) {
+    ++g_nf0_dgemm2;
     if ((st = dgemm2(c->stream, NF0, 2 * N, F, c->WF0K.p, c->NF0p, c->TND.p, 2 * N, c->NPD.p,
                      2 * N)))
       return st;
   } else {   // FASST_SIMM_GEMM=2: k_gemm (no split-K: its outputs have ldc 2N)
+    ++g_nf0_kgemm;
     const double *Bs[2] = {c->TND.p, c->TND.p + N};
     double *Cs[2] = {c->NPD.p, c->NPD.p + N};
     if ((st = gemm<true, false, 2>(c->stream, c->WF0.p, NF0, Bs, 2 * N, Cs, 2 * N, NF0, N, F,
@@ -1586,6 +1638,12 @@ int simm_get_params(simm_ctx *c, double *HGAMMA, double *HPHI, double *HF0, doub
     if (betaL) FASST_HIP(hipMemcpyAsync(betaL, c->bL.p, R * 8, hipMemcpyDeviceToHost, c->stream));
   }
   FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int simm_nf0_product_counts(long *dgemm2_launches, long *kgemm_launches) {
+  if (dgemm2_launches) *dgemm2_launches = g_nf0_dgemm2.load();
+  if (kgemm_launches) *kgemm_launches = g_nf0_kgemm.load();
   return FASST_OK;
 }
 

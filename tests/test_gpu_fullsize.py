@@ -139,9 +139,24 @@ def test_config5_full_size_vs_oracle(monkeypatch, gemm, name):
     WF0 = rs.gamma(1.0, 1.0, size=(F, NF0))
     WG = rs.gamma(1.0, 1.0, size=(F, P))
     np.random.seed(c["init_seed"])
+    import ctypes
+    from pyfasst_amd import _lib
+
+    def counts():
+        d2, kg = ctypes.c_long(0), ctypes.c_long(0)
+        _lib.check(_lib.lib.simm_nf0_product_counts(ctypes.byref(d2), ctypes.byref(kg)),
+                   "simm_nf0_product_counts")
+        return d2.value, kg.value
+    before = counts()
     res = S.Stereo_SIMM(SXR, SXL, WF0, WG, numberOfFilters=K,
                         numberOfAccompanimentSpectralShapes=Rr, numberOfIterations=c["iters"],
                         computeError=True, verbose=False)
+    after = counts()
+    # the selected kernel ran, and only it: at least two NF0-sized products
+    # per iteration (SF0 and WF0^T [num | den]) plus the model rebuilds
+    ran = (after[0] - before[0], after[1] - before[1])
+    used, other = ran if gemm == "0" else ran[::-1]
+    assert used >= 2 * c["iters"] and other == 0, (gemm, ran)
     names = ['alphaR', 'alphaL', 'HGAMMA', 'HPHI', 'HF0', 'betaR', 'betaL', 'HM', 'WM',
              'recoError']
     fs, ts = sub_f(F), sub_t(N)

@@ -616,6 +616,19 @@ def test_mixed_types_free_conv_raises_as_reference(tmp_path):
         o.estim_param_a_post_model()
 
 
+def test_mixed_types_free_conv_refused_at_the_abi(tmp_path):
+    """The same structure straight through the C ABI (no Python-side
+    check): fasst_run refuses it (FASST_ERR_UNSUPPORTED) instead of
+    updating the 'inst' rows and leaving the free 'conv' filters stale."""
+    g = load("em_mixed")
+    m = _product_model("em_mixed", g, tmp_path)
+    m._upload()
+    eng = m._engine
+    eng.set_spatial(2, m.spat_comps[2]['params'], True)
+    with pytest.raises(NotImplementedError, match="conv"):
+        eng.run(np.ones((1, eng.F)), 1.0)
+
+
 def test_full_size_config3_invariants():
     """BASELINE config 3 at full size (F=2049, T=10000, J=4, r=2, K=32):
     size-independent properties after two GEM iterations on the GPU."""

@@ -174,3 +174,45 @@ def test_unvoiced_suimm_stages_vs_reference(tmp_path, monkeypatch):
     check_wav(proc.files['voc_output_file'][:-4] + '_VUIMM.wav', g['whole_lead_vuimm'])
     check_wav(proc.files['mus_output_file'][:-4] + '_VUIMM.wav', g['whole_acc_vuimm'])
 
+
+
+def test_nnls_drops_and_iteration_count_vs_scipy():
+    """Columns whose active-set path drops coefficients (Lawson & Hanson's
+    step E: the coefficient that sets alpha leaves the passive set at exactly
+    zero): the GPU solution matches scipy.optimize.nnls (the reference's
+    per-frame call, SeparateLeadStereoTF.py:988) and the iteration budget
+    behaves as scipy's -- a column whose count is c (outer + inner passes)
+    succeeds with maxiter c + 1 and fails with maxiter c, in both."""
+    import scipy.optimize
+    from pyfasst_amd.tools.nnls import nnls_columns
+    rs = np.random.RandomState(1)      # 4 of the 40 columns take inner (drop) steps
+    m, n = 15, 12
+    A = rs.rand(m, n)
+    B = rs.randn(m, 40)
+    X = nnls_columns(A, B)
+    for q in range(B.shape[1]):
+        xs = scipy.optimize.nnls(A, B[:, q])[0]
+        assert np.max(np.abs(X[:, q] - xs)) < 1e-10 * max(1.0, np.max(np.abs(xs)))
+    import ctypes
+    from pyfasst_amd import _lib
+    info = np.empty(B.shape[1], dtype=np.int32)
+    Xc = np.empty((n, B.shape[1]))
+    Ac, Bc = np.ascontiguousarray(A), np.ascontiguousarray(B)
+    _lib.check(_lib.lib.nnls_columns(_lib.default_device(), m, n, _lib.dptr(Ac), B.shape[1],
+                                     _lib.dptr(Bc), 10.0 * max(m, n) * np.finfo(float).eps, 0.0,
+                                     0, _lib.dptr(Xc), info.ctypes.data_as(_lib._ip)),
+               "nnls_columns")
+    drops = 0
+    for q in range(B.shape[1]):
+        c = int(info[q])
+        if c == 0:      # A^T b <= 0: x = 0 with no pass (maxiter 0 means scipy's default)
+            np.testing.assert_array_equal(Xc[:, q], 0.0)
+            continue
+        drops += c > int(np.sum(Xc[:, q] > 0))        # more passes than entries: a drop
+        scipy.optimize.nnls(A, B[:, q], maxiter=c + 1)
+        with pytest.raises(RuntimeError):
+            scipy.optimize.nnls(A, B[:, q], maxiter=c)
+        nnls_columns(A, B[:, q], maxiter=c + 1)
+        with pytest.raises(Exception):
+            nnls_columns(A, B[:, q], maxiter=c)
+    assert drops > 0
