@@ -399,7 +399,14 @@ def main(argv=None):
         dom = max(times, key=lambda k: times[k][0])
         rl = None
         pmc = None
-        pmc_path = os.environ.get("FASST_PMC_JSON", os.path.join(ROOT, "profiles", "r3_bench.json"))
+        # PMC traffic of THIS configuration's own rocprofv3 passes
+        # (tools/gpu_prof.sh; BENCH_ARGS="--J 8" -> profiles/r4_bench_J8K32.json)
+        default_cfg = (args.J, args.K, args.T) == (J_SRC, K_NMF, T_FRAMES)
+        pmc_name = "r4_bench.json" if default_cfg else "r4_bench_J%dK%d.json" % (args.J, args.K)
+        if args.T != T_FRAMES:
+            pmc_name = None
+        pmc_path = os.environ.get("FASST_PMC_JSON",
+                                  os.path.join(ROOT, "profiles", pmc_name) if pmc_name else "")
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))["kernels"]

@@ -197,6 +197,48 @@ int fasst_istft_simm(int device, const double *X, int n_frames, const double *wi
 int fasst_inv_herm_mat_2d(int device, int n, const double *diag, const double *off,
                           double *inv_diag, double *inv_off, double *det);
 
+/* ---- GEM step methods (fasst_steps.hip) ---------------------------------
+ * The FASST methods GEM_iteration (audioModel.py:384-428) is made of, as
+ * device calls on the reference's own arrays, for scripts that drive an
+ * iteration piecewise or inspect its intermediates (fasst_run fuses them and
+ * never materialises these arrays).  complex128 = interleaved (re, im).
+ *
+ * retrieve_subsrc_params (:514-578), the powers half: V out [nj][F][T], the
+ * power of spatial components j0 .. j0+nj-1 from the context's parameters
+ * (colmask[jj]: the NMF columns to include, bit k; NULL: all).            */
+int fasst_source_powers(fasst_ctx *ctx, int j0, int nj, const unsigned long long *colmask,
+                        double *V);
+/* compute_suff_stat (:580-764) on the context's Cx: V [R][F][T] per-rank
+ * powers, mix complex128 [R][2][F], psd [F] -> rxx complex128 [3][F]
+ * (hat_Rxx: mean of Cx00, Cx01, Cx11), rxs complex128 [F][2][R],
+ * rss complex128 [F][R][R], ws [R][F][T] (hat_Ws), loglik.  R <= 16.      */
+int fasst_suff_stat(fasst_ctx *ctx, int R, const double *V, const double *mix, const double *psd,
+                    double *rxx, double *rxs, double *rss, double *ws, double *loglik);
+/* update_mix_matrix (:766-889), the solve: kind[r] = 0 fixed, 1 free
+ * 'inst', 2 free 'conv' per rank; mix complex128 [R][2][F] in/out.  Free
+ * 'conv' ranks next to other ranks: FASST_ERR_SHAPE (the reference's solve
+ * raises); a singular system: FASST_ERR_SINGULAR, mix untouched.           */
+int fasst_mix_solve(int device, int F, int R, const double *rss, const double *rxs, double *mix,
+                    const int *kind);
+/* update_spectral_components (:1469-1978): hat_W [J][F][T] -> the
+ * context's FB / FW / TW (TB) updated in place (read back with
+ * fasst_get_spectral); no renormalisation (fasst_renormalize).            */
+int fasst_spectral_update(fasst_ctx *ctx, const double *hat_W, double omega);
+/* compute_sigma_comp_2d (:1327-1372): spatial component j, NMF columns
+ * colmask -> diag [2][F][T], off complex128 [F][T].                        */
+int fasst_sigma_comp(fasst_ctx *ctx, int j, unsigned long long colmask, double *diag,
+                     double *off);
+/* compute_inv_sigma_mix_2d (:1374-1394): n components' diag [n][2][F][T],
+ * off complex128 [n][F][T], psd [F] -> inverse of their sum + PSD I:
+ * idiag [2][F][T], ioff complex128 [F][T].                                 */
+int fasst_inv_sigma_mix(int device, int n, int F, int T, const double *diag, const double *off,
+                        const double *psd, double *idiag, double *ioff);
+/* compute_Wiener_gain_2d (:1396-1467): one component's sigma (sdiag
+ * [2][n], soff complex128 [n]) and the inverse mixture covariance
+ * (idiag [2][n], ioff complex128 [n]) -> WG complex128 [2][2][n].         */
+int fasst_wiener_gain(int device, long n, const double *sdiag, const double *soff,
+                      const double *idiag, const double *ioff, double *WG);
+
 #ifdef __cplusplus
 }
 #endif

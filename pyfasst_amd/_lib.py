@@ -78,6 +78,16 @@ SIGNATURES = {
     "fasst_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
     "fasst_inv_herm_mat_2d": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp,
                                              _dp]),
+    "fasst_source_powers": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_ulonglong), _dp]),
+    "fasst_suff_stat": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp,
+                                       _dp]),
+    "fasst_mix_solve": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp,
+                                       _ip]),
+    "fasst_spectral_update": (ctypes.c_int, [_vp, _dp, ctypes.c_double]),
+    "fasst_sigma_comp": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_ulonglong, _dp, _dp]),
+    "fasst_inv_sigma_mix": (ctypes.c_int, [ctypes.c_int] * 4 + [_dp, _dp, _dp, _dp, _dp]),
+    "fasst_wiener_gain": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, _dp, _dp, _dp, _dp, _dp]),
     # include/fasst_simm.h
     "simm_create": (ctypes.c_int, [ctypes.c_int] * 8 + [ctypes.POINTER(_vp)]),
     "simm_destroy": (ctypes.c_int, [_vp]),

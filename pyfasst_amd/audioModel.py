@@ -378,6 +378,100 @@ class FASST(object):
         if mask:
             self._restart_tw(mask, order)
 
+    # ---------------------------------------------------------------- GEM steps
+    # The methods GEM_iteration is made of (audioModel.py:384-428), each a
+    # device call on the reference's own arrays (fasst_steps.hip).  GEM_iteration
+    # itself runs the fused iteration (fasst_run) and never materialises them.
+    def _psd_row(self):
+        return np.asarray(self.noise['PSD'], dtype=np.float64) * np.ones(self.nbFreqsSigRepr)
+
+    def retrieve_subsrc_params(self,):
+        """(spat_comp_powers [R, F, T], mix_matrix [R, 2, F], rank_part_ind)
+        (audioModel.py:514-578); the powers come from the device."""
+        order, Ks, conv = self._upload()
+        J = len(order)
+        rank_part_ind, total = {}, 0
+        for j in range(J):
+            sc = self.spat_comps[j]
+            rank = sc['params'].shape[1] if sc['mix_type'] == 'inst' else sc['params'].shape[0]
+            rank_part_ind[j] = total + np.arange(rank)
+            total += rank
+        V = self._engine.source_powers(0, J)
+        spat_comp_powers = np.empty((total, self.nbFreqsSigRepr, self.nbFramesSigRepr))
+        mix_matrix = np.zeros((total, self.audioObject.channels, self.nbFreqsSigRepr),
+                              dtype=complex)
+        for j in range(J):
+            sc = self.spat_comps[j]
+            spat_comp_powers[rank_part_ind[j]] = V[j]
+            if sc['mix_type'] == 'inst':
+                mix_matrix[rank_part_ind[j]] = np.asarray(sc['params']).T[:, :, None]
+            else:
+                mix_matrix[rank_part_ind[j]] = sc['params']
+        return spat_comp_powers, mix_matrix, rank_part_ind
+
+    def compute_suff_stat(self, spat_comp_powers, mix_matrix):
+        """(hat_Rxx, hat_Rxs, hat_Rss, hat_Ws, loglik) on the device
+        (audioModel.py:580-764), with the current noise PSD."""
+        if self.audioObject.channels != 2:
+            raise ValueError("Nb channels not supported:" + str(self.audioObject.channels))
+        if self._engine is None:
+            raise AttributeError("no observation: call comp_transf_Cx() first")
+        return self._engine.suff_stat(spat_comp_powers, mix_matrix, self._psd_row())
+
+    def update_mix_matrix(self, hat_Rxs, hat_Rss, mix_matrix, rank_part_ind):
+        """Mixing update (audioModel.py:766-889): mix_matrix updated in place,
+        the free spatial components' params replaced."""
+        kind = np.zeros(mix_matrix.shape[0], dtype=np.int32)
+        for j, sc in self.spat_comps.items():
+            if sc['frdm_prior'] == 'free':
+                kind[rank_part_ind[j]] = 1 if sc['mix_type'] == 'inst' else 2
+        m = np.ascontiguousarray(mix_matrix, dtype=np.complex128)
+        self._engine.mix_solve(hat_Rss, hat_Rxs, m, kind)
+        if m is not mix_matrix:
+            mix_matrix[...] = m
+        for j, sc in self.spat_comps.items():
+            if sc['frdm_prior'] == 'free':
+                if sc['mix_type'] == 'inst':
+                    sc['params'] = np.mean(mix_matrix[rank_part_ind[j]], axis=2).T
+                else:
+                    sc['params'] = mix_matrix[rank_part_ind[j]]
+
+    def update_spectral_components(self, hat_W):
+        """FB / FW / TW (TB) updates from hat_W [J, F, T] on the device
+        (audioModel.py:1469-1978); no renormalisation."""
+        order, Ks, conv = self._upload()
+        self._engine.spectral_update(hat_W, self.nmfUpdateCoeff)
+        self._download(order, Ks, conv, updated_spatial=False)
+
+    def _colmask(self, spat_ind, spec_comp_ind, order):
+        keys = spec_comp_ind if len(spec_comp_ind) else order[spat_ind]
+        mask, a = 0, 0
+        for k in order[spat_ind]:
+            n = self.spec_comps[k]['factor'][0]['FB'].shape[1]
+            if k in keys:
+                mask |= ((1 << n) - 1) << a
+            a += n
+        return mask
+
+    def compute_sigma_comp_2d(self, spat_ind, spec_comp_ind):
+        """(sigma_comp_diag [2, F, T], sigma_comp_off [F, T]) of one spatial
+        component's spectral components (audioModel.py:1327-1372)."""
+        order, Ks, conv = self._upload()
+        return self._engine.sigma_comp(spat_ind, self._colmask(spat_ind, spec_comp_ind, order))
+
+    def compute_inv_sigma_mix_2d(self, sigma_comps_diag, sigma_comps_off):
+        """Inverse of sum_n Sigma_n + PSD I (audioModel.py:1374-1394)."""
+        return self._engine.inv_sigma_mix(sigma_comps_diag, sigma_comps_off, self._psd_row())
+
+    def compute_Wiener_gain_2d(self, sigma_comp_diag, sigma_comp_off, inv_sigma_mix_diag,
+                               inv_sigma_mix_off, timeInvariant=False):
+        """WG [2, 2, F(, T)] (audioModel.py:1396-1467)."""
+        from .engine import wiener_gain
+        dev = self._engine.device if self._engine is not None else \
+            (0 if self.device is None else self.device)
+        return wiener_gain(dev, sigma_comp_diag, sigma_comp_off, inv_sigma_mix_diag,
+                           inv_sigma_mix_off)
+
     # ---------------------------------------------------------------- NMF init
     def _mono_power(self):
         """Channel-averaged power sum_c Re Cx[c, c] / nc (audioModel.py:2150-2158)."""

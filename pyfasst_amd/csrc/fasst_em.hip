@@ -50,23 +50,19 @@ void set_error(const char *fmt, ...) {
     if ((h) && *(volatile const int *)(h)) return;      \
   } while (0)
 
-// XCD-aware logical block (FASST_XCD): workgroups b, b + 8, ... of a launch
-// share an XCD (dispatch is round-robin over the 8 XCDs, for speed only,
-// never correctness); the bijective remap of cdna_hip_programming.md gives
-// each XCD a contiguous run of the logical (x fastest, z slowest) sequence,
-// so the blocks that re-read one operand slice (the E-step's TW chunk, the
-// contractions' W / (FW H)^T slices) meet in one 4 MB L2
-#ifndef FASST_XCD
-#define FASST_XCD 0
-#endif
+// XCD-aware logical block: workgroups b, b + 8, ... of a launch share an XCD
+// (dispatch is round-robin over the 8 XCDs, for speed only, never
+// correctness); the bijective remap of cdna_hip_programming.md gives each XCD
+// a contiguous run of the logical (x fastest, z slowest) sequence, so the
+// blocks that re-read one operand slice (the E-step's TW chunk, the
+// contractions' W / (FW H)^T slices) meet in one 4 MB L2.  At C3 it takes
+// 9-14 % off the HBM fetch of the E-step and both contractions (rocprofv3
+// FETCH_SIZE, profiles/r4_bench.txt vs the row-major order) at equal time.
 __device__ __forceinline__ dim3 xcd_block() {
   const int nx = gridDim.x, ny = gridDim.y, n = nx * ny * gridDim.z;
   const int b = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
-  int L = b;
-  if (FASST_XCD) {
-    const int q = n / 8, r = n % 8, x = b % 8;
-    L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-  }
+  const int q = n / 8, r = n % 8, x = b % 8;
+  const int L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
   return dim3(L % nx, (L / nx) % ny, L / (nx * ny));
 }
 
@@ -207,22 +203,66 @@ __device__ __forceinline__ double mfma44(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
+// Reader-formed pair operands (RP, J >= 4): the slab holds V, P and N only,
+// and the reader forms the pair operands V_j1 V_j2 itself.  With the sources
+// padded to Q = 4 (J = 4) or 8 (J > 4), lane m of a 4-pair group reads the Q
+// rotated values W_e = V_{(m + e) mod Q} of its point, and the pairs are the
+// groups (base, d): pair m of a group is (base + m, base + m + d mod Q), its
+// operand W_base W_{(base + d) mod Q} -- static register indices.  Q = 8: the
+// 36 pairs are {0, 4} x {0..3} plus (0, 4); Q = 4: the 10 pairs are
+// (0, 0), (0, 1) and (0, 2) (rows m = 2, 3 of the last repeat rows 0, 1).
+// The writer's J (J + 1) / 2 products and their slab stores go (J = 8: 56 ->
+// 20 stores per point, J = 4: 26 -> 16), the reader's loads stay or drop
+// (J = 8: 14 -> 11 per bin group), and the slab shrinks.  Same-box A/B at
+// C3 (J = 4): E-step 0.373 vs 0.390 ms, iteration 1.040 vs 1.068 ms; J = 6 /
+// 8 (K = 32): 0.813 / 1.002 ms against 1.083 / 1.663 ms with writer-formed
+// pairs.
+// VR (J > 4): also the per-source pipelined V tile, one wave per SIMD (the
+// register file, not the LDS, bounds it: at two waves the kernel spills
+// 500+ bytes per lane to scratch) and the epilogue one bin group at a time.
 template <int J>
 struct MXShape {
+  static constexpr bool VR = J > 4;
+  static constexpr bool RP = J >= 4;
+  static constexpr int Q = J > 4 ? 8 : 4;       // RP: sources padded to Q
   static constexpr int NP = J * (J + 1) / 2;
-  static constexpr int NPG = (NP + 3) / 4;      // pair groups of 4
+  static constexpr int NPG = RP ? (Q == 8 ? 9 : 3) : (NP + 3) / 4;   // pair groups of 4
   static constexpr int NVG = (J + 3) / 4;       // source groups of 4
   static constexpr int SP = NVG, SN = NVG + 2, SV2 = NVG + 3;  // set offsets: P lo/hi, N, VV
-  static constexpr int NSET = NVG + 3 + NPG;    // V groups | P lo | P hi | N | VV groups
+  static constexpr int NSET = NVG + 3 + (RP ? 0 : NPG);  // V groups | P lo | P hi | N | VV groups
   static constexpr int GS = NSET * 64 + 1;      // doubles per bin group (+1: bank skew)
   static constexpr int SLAB = 4 * GS;           // doubles per wave
 };
+// RP pair group h: (base, d)
+template <int Q>
+__host__ __device__ constexpr int rp_base(int h) { return Q == 4 || h == 8 ? 0 : 4 * (h & 1); }
+template <int Q>
+__host__ __device__ constexpr int rp_d(int h) { return Q == 4 ? h : (h == 8 ? 4 : h >> 1); }
+// canonical index (j1 <= j2, j1 major) of the pair lane m of group h
+// accumulates, or -1 (a padded source or a repeated pair)
+template <int J>
+__host__ __device__ constexpr int rp_pair(int h, int m) {
+  constexpr int Q = MXShape<J>::Q;
+  if (!MXShape<J>::RP) return 4 * h + m < MXShape<J>::NP ? 4 * h + m : -1;
+  const int j1 = rp_base<Q>(h) + m, j2 = (rp_base<Q>(h) + m + rp_d<Q>(h)) & (Q - 1);
+  if (j1 >= J || j2 >= J || (Q == 4 && rp_d<Q>(h) == 2 && m >= 2)) return -1;
+  const int lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+  return lo * J - lo * (lo - 1) / 2 + (hi - lo);
+}
+// does RP pair group h hold a live pair
+template <int J>
+__host__ __device__ constexpr bool rp_live(int h) {
+  for (int m = 0; m < 4; ++m)
+    if (rp_pair<J>(h, m) >= 0) return true;
+  return false;
+}
 
 // the W tile sits in LDS unless it would push the block past 160 KB (J = 8,
-// K = 64); then the V tiles read their W operand from L2
+// K = 128); then the V tiles read their W operand from L2
 template <int J, int NKS>
 __host__ __device__ constexpr bool mx_w_in_lds() {
-  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) * sizeof(double) <= 160 * 1024;
+  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) * sizeof(double) <=
+         160 * 1024;
 }
 template <int J, int NKS>
 static constexpr size_t estep_mx_smem() {
@@ -256,21 +296,14 @@ __device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsign
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(es_u2, v), r, (int)vo, (int)so, AUX);
 }
 
-#ifndef ESTEP_PF
-#define ESTEP_PF 0
-#endif
-#ifndef ESTEP_SWP
-#define ESTEP_SWP 0
-#endif
-#ifndef ESTEP_RHO_AUX
-#define ESTEP_RHO_AUX 2
-#endif
 template <int J, int NKS, int RKU>
 __global__ __launch_bounds__(256, J > 4 ? 1 : 2)
 __attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) FASST_NO_LDS_PAIRING
 void k_estep_mx(const EArgs a) {
   HALT_GUARD(a.halt);
   using S = MXShape<J>;
+  constexpr bool VR = S::VR, RP = S::RP;
+  constexpr int Q = S::Q;
   constexpr int NP = S::NP, NPG = S::NPG, NVG = S::NVG;
   constexpr int NACC = 4 * NP + 8 * J;
   constexpr int KP = 4 * NKS;
@@ -282,7 +315,7 @@ void k_estep_mx(const EArgs a) {
   double *s_ll = smem;                     // [4]
   double *s_w = s_ll + 4;                  // [J][KP][16] W tile (if WL)
   double *s_slab = s_w + (WL ? J * KP * 16 : 0);  // [4 waves][SLAB] operand slabs
-  double *s_red = s_w;                     // [4][NACC][16] (epilogue, aliases W + slabs)
+  double *s_red = s_w;                     // [4][NACC][16 | 4] (epilogue, aliases W + slabs)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fl = lane & 15, tq = lane >> 4;
@@ -329,6 +362,15 @@ void k_estep_mx(const EArgs a) {
   double *wr = slab + (fl >> 2) * S::GS + 16 * tq + 4 * (fl & 3);
   // reader side: operands of lane (X, b, Y) sit at [group][set][lane]
   const double *rd = slab + lane;
+  // RP: W_e = V_{(m + e) mod Q} of the lane's point (m = Y) sits in set
+  // ((m + e) mod Q) / 4 at Y' = (m + e) mod 4 of the same (X, b)
+  const double *rdq = slab + (lane & ~3);
+  int vro[Q];
+#pragma unroll
+  for (int e = 0; e < Q; ++e) {
+    const int j = ((lane & 3) + e) & (Q - 1);
+    vro[e] = (j >> 2) * 64 + (j & 3);
+  }
 
   double xacc[4][NVG][2], pacc[4][NPG];  // D operands (4x4 blocks per bin group)
 #pragma unroll
@@ -344,9 +386,8 @@ void k_estep_mx(const EArgs a) {
   const int te = min(tb + a.tpc, a.ntt);
   // SA: wave-uniform buffer resources (SGPRs, formed on the scalar unit) +
   // 32-bit per-lane byte offsets instead of one 64-bit VALU address
-  // computation per access (J <= 4: the J = 8, K = 64 instantiation trips a
-  // compiler crash in ROCm 7.2's AGPR-copy rewrite with it)
-  constexpr bool SA = J <= 4;
+  // computation per access
+  constexpr bool SA = true;
   int wvu = wv;
   if constexpr (SA) wvu = __builtin_amdgcn_readfirstlane(wv);
   const unsigned vo_tw = (unsigned)(tq * a.Tp + fl) * 8u;   // TW[j][k = tq + 4s][t0 + fl]
@@ -372,12 +413,6 @@ void k_estep_mx(const EArgs a) {
       }
     }
   };
-  // ESTEP_PF: the next tile's Cx is loaded while this tile computes (HBM
-  // latency off the tile's critical path); a wave's last tile re-loads
-  // itself (clamped index: no branch around the loads)
-  constexpr bool PF = ESTEP_PF && SA;
-  double cxn[4][4];
-  if constexpr (PF) load_cx(min(tb + wvu, te - 1), cxn);
   for (int tt = tb + wvu; tt < te; tt += 4) {
     const int t0 = tt * 16;
     int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
@@ -386,7 +421,8 @@ void k_estep_mx(const EArgs a) {
     // otherwise pair each load with its MFMA and wait on every one); with more
     // than 32 operands (J > 4 or K > 32 at J = 4) the sources beyond the first
     // 32 operands load next to their own MFMAs
-    constexpr int JA = (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
+    // (VR: none up front -- the V loop below pipelines them source by source)
+    constexpr int JA = VR ? 1 : (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
     double twv[JA][NKS];
 #pragma unroll
     for (int j = 0; j < JA; ++j) {
@@ -396,23 +432,46 @@ void k_estep_mx(const EArgs a) {
         twv[j][s] = SA ? es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u)
                        : tw[(size_t)(4 * s) * a.Tp];
     }
-    double cxv[4][4];  // this tile's Cx (in flight with the TW operands without PF)
-    if constexpr (PF) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) cxv[q][i] = cxn[q][i];
-      load_cx(min(tt + 4, te - 1), cxn);
-    } else {
-      load_cx(tt, cxv);
-    }
+    double cxv[4][4];  // this tile's Cx (in flight with the TW operands)
+    load_cx(tt, cxv);
     __builtin_amdgcn_sched_barrier(0);
     d4 v[J];
+    if constexpr (VR) {
+      // source j + 1's TW operands in flight while source j's MFMAs run; the
+      // barriers keep the scheduler from hoisting every source's loads (at
+      // K = 64 / 128 they alone would fill the register file)
+      // (W from L2 at K = 128, J = 8: no prefetch, or the operands alone spill)
+      constexpr bool PFS = WL || NKS <= 16;
+      double tn[NKS];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
+      for (int s = 0; s < NKS; ++s) tn[s] = twv[0][s];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        double tc[NKS];
+#pragma unroll
+        for (int s = 0; s < NKS; ++s)
+          tc[s] = PFS || j == 0 ? tn[s]
+                               : es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u);
+        if (PFS && j + 1 < J) {
+#pragma unroll
+          for (int s = 0; s < NKS; ++s)
+            tn[s] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)(((j + 1) * KP + 4 * s) * a.Tp) * 8u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        v[j] = d4{0.0, 0.0, 0.0, 0.0};
+        const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+        const double *gw = a.Wkf + lofs + ((size_t)j * KP + tq) * a.Fp + f;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s)
+          v[j] = mfma4(tc[s], WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < (VR ? 0 : J); ++j) {
       v[j] = d4{0.0, 0.0, 0.0, 0.0};
       const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
-      const double *gw = a.Wkf + ((size_t)j * KP + tq) * a.Fp + f;
+      const double *gw = a.Wkf + lofs + ((size_t)j * KP + tq) * a.Fp + f;
       const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
       for (int s = 0; s < NKS; ++s)
@@ -485,7 +544,7 @@ void k_estep_mx(const EArgs a) {
         const double q = RKU == 1 ? qa : qa * inv_rk[j];
         const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
         if constexpr (SA)
-          es_st<ESTEP_RHO_AUX>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
+          es_st<2>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
                                (unsigned)(4 * i * a.Fp) * 8u);
         else
           __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
@@ -504,16 +563,20 @@ void k_estep_mx(const EArgs a) {
         wr[(S::SP + 1) * 64 + c] = P[4 + c];
         wr[S::SN * 64 + c] = N[c];
       }
-      int p = 0;
+      if constexpr (!RP) {
+        int p = 0;
 #pragma unroll
-      for (int j1 = 0; j1 < J; ++j1)
+        for (int j1 = 0; j1 < J; ++j1)
 #pragma unroll
-        for (int j2 = j1; j2 < J; ++j2, ++p)
-          wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
+          for (int j2 = j1; j2 < J; ++j2, ++p)
+            wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
+      }
     };
-    // (J > 4 always pipelines: the other form trips ROCm 7.2's AGPR-copy
-    // rewrite pass at J = 8, K = 64)
-    constexpr bool SWP = ESTEP_SWP || J > 4;
+    // SWP (J > 4): the next point's VALU work sits between this point's slab
+    // reads and its MFMAs.  Neutral at J <= 4 (0.376-0.381 vs 0.380-0.382 ms
+    // at C3); at J > 4 the unpipelined form trips ROCm 7.2's AGPR-copy
+    // rewrite pass (J = 8, K = 64)
+    constexpr bool SWP = J > 4;
     auto slab_fence = [&]() {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -521,9 +584,39 @@ void k_estep_mx(const EArgs a) {
     };
     // the slab's operands of the 4 bin groups in flight at once, then the
     // MFMAs (read -> wait -> MFMA one at a time left the LDS latency exposed);
-    // ESTEP_SWP: the next point's VALU work sits between the reads and the
+    // with SWP the next point's VALU work sits between the reads and the
     // MFMAs (its slab writes after them)
     auto mfma_pass = [&](auto between) {
+      if constexpr (RP) {
+        // rotated sources W_e, then P lo / hi and N, of the 4 bin groups
+        double w[4][Q], pn[4][3];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+          for (int e = 0; e < Q; ++e) w[g][e] = rdq[g * S::GS + vro[e]];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) pn[g][q] = rd[g * S::GS + (S::SP + q) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SWP) {
+          between();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+          for (int vg = 0; vg < NVG; ++vg) {
+            xacc[g][vg][0] = mfma44(w[g][4 * vg], pn[g][0], xacc[g][vg][0]);
+            xacc[g][vg][1] = mfma44(w[g][4 * vg], pn[g][1], xacc[g][vg][1]);
+          }
+#pragma unroll
+          for (int h = 0; h < NPG; ++h)
+            if (rp_live<J>(h))
+              pacc[g][h] = mfma44(w[g][rp_base<Q>(h)] * w[g][(rp_base<Q>(h) + rp_d<Q>(h)) & (Q - 1)],
+                                  pn[g][2], pacc[g][h]);
+        }
+        return;
+      }
       double opd[4][S::NSET];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
@@ -579,6 +672,44 @@ void k_estep_mx(const EArgs a) {
 
   // epilogue: lane (X = m, b, Y = n) holds, per bin group g, the 4x4 blocks
   // D[m][n] of bin f0 + 4g + b: cross (j = m, c = 4h + n), pairs (p = 4h + m, c = n)
+  // (VR: pair m of group (base, d); the four waves' sums go through LDS one
+  // bin group at a time, [4][NACC][4], to fit the smaller slab allocation)
+#pragma unroll
+  for (int mm = 1; mm < 64; mm <<= 1) ll += __shfl_xor(ll, mm, 64);
+  if constexpr (VR) {
+    static_assert(4 * NACC * 4 <= 4 * S::SLAB, "VR epilogue fits the slabs");
+    const int m = lane >> 4, bb = (lane >> 2) & 3, n = lane & 3;
+    double *red = s_slab;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __syncthreads();  // (g = 0: the slabs' last reads; else the previous group's sums)
+#pragma unroll
+      for (int vg = 0; vg < NVG; ++vg) {
+        const int j = 4 * vg + m;
+        if (j < J) {
+          red[((wv * NACC) + 4 * NP + 8 * j + n) * 4 + bb] = xacc[g][vg][0];
+          red[((wv * NACC) + 4 * NP + 8 * j + 4 + n) * 4 + bb] = xacc[g][vg][1];
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < NPG; ++h) {
+        const int p = rp_pair<J>(h, m);
+        if (p >= 0) red[((wv * NACC) + 4 * p + n) * 4 + bb] = pacc[g][h];
+      }
+      __syncthreads();
+      for (int idx = tid; idx < NACC * 4; idx += 256) {
+        const int u = idx >> 2, ff = idx & 3;
+        const double x = red[(0 * NACC + u) * 4 + ff] + red[(1 * NACC + u) * 4 + ff] +
+                         red[(2 * NACC + u) * 4 + ff] + red[(3 * NACC + u) * 4 + ff];
+        a.part[((size_t)(a.ybase + bi.y) * a.Fp + f0 + 4 * g + ff) * NACC + u] = x;
+      }
+    }
+    if (lane == 0) s_ll[wv] = ll;
+    __syncthreads();
+    if (tid == 0)
+      a.llpart[(a.ybase + bi.y) * a.nft + bi.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
+    return;
+  }
   __syncthreads();  // s_red aliases the W tile and the slabs
   double *red = s_red + wv * NACC * 16;
   {
@@ -595,12 +726,12 @@ void k_estep_mx(const EArgs a) {
         }
       }
 #pragma unroll
-      for (int h = 0; h < NPG; ++h)
-        if (4 * h + m < NP) red[(4 * (4 * h + m) + n) * 16 + bin] = pacc[g][h];
+      for (int h = 0; h < NPG; ++h) {
+        const int p = rp_pair<J>(h, m);
+        if (p >= 0) red[(4 * p + n) * 16 + bin] = pacc[g][h];
+      }
     }
   }
-#pragma unroll
-  for (int mm = 1; mm < 64; mm <<= 1) ll += __shfl_xor(ll, mm, 64);
   if (lane == 0) s_ll[wv] = ll;
   __syncthreads();
   for (int idx = tid; idx < NACC * 16; idx += 256) {
@@ -998,11 +1129,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
   for (int p = 0; p < (DEN ? FPW : 1); ++p)
 #pragma unroll
     for (int kc = 0; kc < NKC; ++kc) den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
-#ifndef FB_REVERSE
-#define FB_REVERSE 0
-#endif
-  const int zc = FB_REVERSE ? (int)gridDim.z - 1 - (int)bi.z : (int)bi.z;
-  const int tb = a.tbase + zc * a.tpc, te = min(tb + a.tpc, a.ntt);
+  const int tb = a.tbase + bi.z * a.tpc, te = min(tb + a.tpc, a.ntt);
   const double *rhoj = a.hatW + (size_t)j * a.Tp * a.Fp;
   const double *rdj = DEN ? a.hatW2 + (size_t)j * a.Tp * a.Fp : nullptr;
   for (int tt = tb; tt < te; ++tt) {
@@ -1063,7 +1190,7 @@ __global__ __launch_bounds__(64) void k_fb_contract(const BArgs a) {
       }
     }
   }
-  const size_t base = ((size_t)(a.zbase + zc) * a.J + j) * a.Fp;
+  const size_t base = ((size_t)(a.zbase + bi.z) * a.J + j) * a.Fp;
   if constexpr (FPW % 2 == 0 && !DEN) {   // interleaved tiles: tile p holds bins p mod FPW
 #pragma unroll
     for (int p = 0; p < FPW; ++p)
@@ -2160,10 +2287,10 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   const int conv = c->convm == (1u << J) - 1u ? 1 : 0;
   c->conv = conv;
   // the E-step addresses TW through a raw buffer resource with 32-bit byte
-  // offsets (j KP + 4 s) Tp 8 (J <= 4, k_estep_mx's SA form)
+  // offsets (j KP + 4 s) Tp 8 (k_estep_mx's SA form)
   {
     const int KPc = kmax <= 16 ? 16 : (kmax <= 32 ? 32 : (kmax <= 64 ? 64 : 128));
-    if (J <= 4 && (size_t)J * KPc * c->Tp * sizeof(double) >= (1ull << 31)) {
+    if ((size_t)J * KPc * c->Tp * sizeof(double) >= (1ull << 31)) {
       set_error("J %d x K %d x T %d: the TW plane passes the E-step's 2 GB buffer offsets", J,
                 KPc, c->T);
       return FASST_ERR_UNSUPPORTED;
@@ -2456,10 +2583,7 @@ static void estep_dispatch_j(const fasst_ctx *c, F &&f) {
     case 16: estep_dispatch_r<J, 4>(c, f); break;
     case 32: estep_dispatch_r<J, 8>(c, f); break;
     case 64: estep_dispatch_r<J, 16>(c, f); break;
-    default:   // K up to 128: general ranks only, J <= 4 (gem_iteration refuses more)
-      if constexpr (J <= 4) f(ETag<J, 32, 0>{});
-      else f(ETag<J, 16, 0>{});
-      break;
+    default: f(ETag<J, 32, 0>{}); break;   // K up to 128: general ranks only
   }
 }
 
@@ -2816,37 +2940,11 @@ static int multi_spectral(fasst_ctx *c, double omega) {
   return FASST_OK;
 }
 
-// One GEM iteration, all launches asynchronous on c->stream.
-static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
-                         int iter) {
+// (FW.TW)^T and the TW row sums of the previous parameters, the operands of
+// the spectral update; fork: on the side stream (joined by the caller
+// through ev_join before their first consumer)
+static int launch_spectral_prep(fasst_ctx *c, bool fork) {
   const int J = c->J;
-  if (c->KP > 64) {
-    // K > 64 per source: the single-component path (the constructors' models)
-    bool any_fw = false;
-    for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-    if (c->multi || any_fw || J > 4) {
-      set_error("K > 64 NMF components on a spatial component is on the HIP path with at most "
-                "4 spatial components, one spectral component each, fixed FW, lambdaCorr = 0 "
-                "and no time blobs");
-      return FASST_ERR_UNSUPPORTED;
-    }
-  }
-  if (!c->conv) {
-    // a free 'conv' component next to other components: the reference's conv
-    // solve (audioModel.py:856-857) passes the full hat_Rss[f].T against the
-    // free components' right-hand side only, and np.linalg.solve raises
-    for (int j = 0; j < J; ++j)
-      if ((c->convm >> j & 1u) && c->spat_free[j]) {
-        set_error("spatial component %d is 'conv' and free next to other components: the "
-                  "reference's mixing solve (audioModel.py:856-857) raises for this structure",
-                  j);
-        return FASST_ERR_UNSUPPORTED;
-      }
-  }
-  // (FW.TW)^T and the TW row sums depend only on the previous iteration's
-  // parameters: fork them onto the side stream (kept on the main stream
-  // while per-kernel event timing is on)
-  const bool fork = !c->prof;
   hipStream_t side = fork ? c->aux : c->stream;
   if (fork) {
     FASST_HIP(hipEventRecord(c->ev_fork, c->stream));
@@ -2863,34 +2961,18 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   k_tw_rowsum<<<J * c->KP, 256, 0, side>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
   FASST_LAUNCH_CHECK();
   if (fork) FASST_HIP(hipEventRecord(c->ev_join, c->aux));
-  int st = launch_w_old(c);
-  if (st) return st;
-  st = build_inst_A(c);
-  if (st) return st;
-  EArgs e;
-  e.cx00 = c->cx.p;
-  e.cx11 = c->cx.p + (size_t)c->Tp * c->Fp;
-  e.cxr = c->cx.p + 2 * (size_t)c->Tp * c->Fp;
-  e.cxi = c->cx.p + 3 * (size_t)c->Tp * c->Fp;
-  e.TW = c->TW.p;
-  e.Wkf = c->Wkf.p;
-  e.A = c->A.p;
-  e.psd = psd_dev;
-  e.hatW = c->hatW.p;
-  e.halt = c->halt;
-  e.part = c->epart.p;
-  e.llpart = c->llpart.p;
-  e.F = c->F;
-  e.T = c->T;
-  e.Fp = c->Fp;
-  e.Tp = c->Tp;
-  e.KP = c->KP;
-  e.R = c->R;
-  e.ntt = c->ntt;
-  e.tpc = c->tpc_e;
-  e.nft = c->nft;
-  for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
-  e.ybase = e.tbase = 0;
+  return FASST_OK;
+}
+
+// update_spectral_components (audioModel.py:1469-1978) from the rho planes in
+// c->hatW (rho_j = hat_W_j / max(V_j, eps), V from the parameters before the
+// update), after launch_spectral_prep and launch_w_old
+static int spectral_update(fasst_ctx *c, double omega) {
+  const int J = c->J;
+  const int nkc = c->KP / 16;
+  bool any_fw = false;
+  for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
+  if (c->multi) return multi_spectral(c, omega);
   BArgs b;
   b.TW = c->TW.p;
   b.Wkf = c->Wkf.p;
@@ -2911,77 +2993,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   b.tpc = c->tpc_b;
   b.zbase = b.tbase = 0;
   for (int j = 0; j < kMaxJ; ++j) b.fb_free[j] = j < J ? c->fb_free[j] : 0;
-  const int nkc = c->KP / 16;
-  launch_estep(c, e, c->nchunk_e);
-  FASST_LAUNCH_CHECK();
-  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
-  prof_begin(c, KLL);
-  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
-                                     1.0 / ((double)c->F * (double)c->T), c->halt);
-  prof_end(c, KLL);
-  FASST_LAUNCH_CHECK();
-  // mixing update
-  bool any_free = false, all_free = true;
-  for (int j = 0; j < J; ++j) {
-    any_free |= c->spat_free[j] != 0;
-    all_free &= c->spat_free[j] != 0;
-  }
-  if (any_free) {
-    MArgs m;
-    m.part = c->epart.p;
-    m.Wkf = c->Wkf.p;
-    m.hsum = c->hsum.p;
-    m.KP = c->KP;
-    m.A = c->A.p;
-    m.rss = c->rss.p;
-    m.rxs = c->rxs.p;
-    m.flags = c->flags.p;
-    m.halt = c->halt;
-    m.F = c->F;
-    m.Fp = c->Fp;
-    m.J = J;
-    m.R = c->R;
-    m.nchunk = c->nchunk_e;
-    m.nacc = c->nacc;
-    m.conv_update = c->conv ? 1 : 0;
-    m.invT = 1.0 / (double)c->T;
-    for (int j = 0; j < J; ++j)
-      for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
-    prof_begin(c, KMIX);
-    k_mix<<<c->F, 64, mix_smem(J, c->R, c->KP, c->nacc), c->stream>>>(m);
-    prof_end(c, KMIX);
-    FASST_LAUNCH_CHECK();
-    if (!c->conv) {
-      IArgs ia;
-      ia.rss = c->rss.p;
-      ia.rxs = c->rxs.p;
-      ia.A = c->A.p;
-      ia.Pinst = c->Pinst.p;
-      ia.flags = c->flags.p;
-      ia.halt = c->halt;
-      ia.F = c->F;
-      ia.Fp = c->Fp;
-      ia.R = c->R;
-      ia.nu = ia.no = 0;
-      for (int j = 0; j < J; ++j)
-        for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) {
-          if (c->spat_free[j])
-            ia.upd[ia.nu++] = r;
-          else
-            ia.oth[ia.no++] = r;
-        }
-      prof_begin(c, KMIXI);
-      k_mix_inst<<<1, 256, 0, c->stream>>>(ia);
-      prof_end(c, KMIXI);
-      FASST_LAUNCH_CHECK();
-    }
-  }
-  (void)all_free;
-  if (c->multi) {
-    int st2 = multi_spectral(c, omega);
-    if (st2) return st2;
-    return launch_renorm(c, iter);
-  }
   // spectral update: FB then TW (one NMF factor per source)
   TArgs t;
   t.TW = c->TW.p;
@@ -3109,6 +3120,149 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
   prof_end(c, KTWU);
   FASST_LAUNCH_CHECK();
+  return FASST_OK;
+}
+
+// rho_j = hat_W_j / max(V_j, eps) into the [J][Tp][Fp] plane the spectral
+// update reads, from a caller's hat_W [J][F][T] (update_spectral_components
+// called on its own); V_j from the current parameters (Wkf = FB.FW)
+__global__ void k_rho_from_hatw(const double *__restrict__ hw, const double *__restrict__ Wkf,
+                                const double *__restrict__ TW, double *__restrict__ rho, int F,
+                                int T, int Fp, int Tp, int KP) {
+  const int f = blockIdx.x * 64 + (threadIdx.x & 63), t = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int j = blockIdx.z;
+  if (f >= F || t >= T) return;
+  double v = 0.0;
+  for (int k = 0; k < KP; ++k) v += Wkf[((size_t)j * KP + k) * Fp + f] * TW[((size_t)j * KP + k) * Tp + t];
+  rho[((size_t)j * Tp + t) * Fp + f] = hw[((size_t)j * F + f) * T + t] / fmax(v, kEps);
+}
+
+// One GEM iteration, all launches asynchronous on c->stream.
+static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
+                         int iter) {
+  const int J = c->J;
+  if (c->KP > 64) {
+    // K > 64 per source: the single-component path (the constructors' models)
+    bool any_fw = false;
+    for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
+    if (c->multi || any_fw) {
+      set_error("K > 64 NMF components on a spatial component is on the HIP path with one "
+                "spectral component each, fixed FW, lambdaCorr = 0 and no time blobs");
+      return FASST_ERR_UNSUPPORTED;
+    }
+  }
+  if (!c->conv) {
+    // a free 'conv' component next to other components: the reference's conv
+    // solve (audioModel.py:856-857) passes the full hat_Rss[f].T against the
+    // free components' right-hand side only, and np.linalg.solve raises
+    for (int j = 0; j < J; ++j)
+      if ((c->convm >> j & 1u) && c->spat_free[j]) {
+        set_error("spatial component %d is 'conv' and free next to other components: the "
+                  "reference's mixing solve (audioModel.py:856-857) raises for this structure",
+                  j);
+        return FASST_ERR_UNSUPPORTED;
+      }
+  }
+  // (FW.TW)^T and the TW row sums depend only on the previous iteration's
+  // parameters: fork them onto the side stream (kept on the main stream
+  // while per-kernel event timing is on)
+  const bool fork = !c->prof;
+  int st = launch_spectral_prep(c, fork);
+  if (st) return st;
+  st = launch_w_old(c);
+  if (st) return st;
+  st = build_inst_A(c);
+  if (st) return st;
+  EArgs e;
+  e.cx00 = c->cx.p;
+  e.cx11 = c->cx.p + (size_t)c->Tp * c->Fp;
+  e.cxr = c->cx.p + 2 * (size_t)c->Tp * c->Fp;
+  e.cxi = c->cx.p + 3 * (size_t)c->Tp * c->Fp;
+  e.TW = c->TW.p;
+  e.Wkf = c->Wkf.p;
+  e.A = c->A.p;
+  e.psd = psd_dev;
+  e.hatW = c->hatW.p;
+  e.halt = c->halt;
+  e.part = c->epart.p;
+  e.llpart = c->llpart.p;
+  e.F = c->F;
+  e.T = c->T;
+  e.Fp = c->Fp;
+  e.Tp = c->Tp;
+  e.KP = c->KP;
+  e.R = c->R;
+  e.ntt = c->ntt;
+  e.tpc = c->tpc_e;
+  e.nft = c->nft;
+  for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
+  e.ybase = e.tbase = 0;
+  launch_estep(c, e, c->nchunk_e);
+  FASST_LAUNCH_CHECK();
+  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
+  prof_begin(c, KLL);
+  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
+                                     1.0 / ((double)c->F * (double)c->T), c->halt);
+  prof_end(c, KLL);
+  FASST_LAUNCH_CHECK();
+  // mixing update
+  bool any_free = false, all_free = true;
+  for (int j = 0; j < J; ++j) {
+    any_free |= c->spat_free[j] != 0;
+    all_free &= c->spat_free[j] != 0;
+  }
+  if (any_free) {
+    MArgs m;
+    m.part = c->epart.p;
+    m.Wkf = c->Wkf.p;
+    m.hsum = c->hsum.p;
+    m.KP = c->KP;
+    m.A = c->A.p;
+    m.rss = c->rss.p;
+    m.rxs = c->rxs.p;
+    m.flags = c->flags.p;
+    m.halt = c->halt;
+    m.F = c->F;
+    m.Fp = c->Fp;
+    m.J = J;
+    m.R = c->R;
+    m.nchunk = c->nchunk_e;
+    m.nacc = c->nacc;
+    m.conv_update = c->conv ? 1 : 0;
+    m.invT = 1.0 / (double)c->T;
+    for (int j = 0; j < J; ++j)
+      for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
+    prof_begin(c, KMIX);
+    k_mix<<<c->F, 64, mix_smem(J, c->R, c->KP, c->nacc), c->stream>>>(m);
+    prof_end(c, KMIX);
+    FASST_LAUNCH_CHECK();
+    if (!c->conv) {
+      IArgs ia;
+      ia.rss = c->rss.p;
+      ia.rxs = c->rxs.p;
+      ia.A = c->A.p;
+      ia.Pinst = c->Pinst.p;
+      ia.flags = c->flags.p;
+      ia.halt = c->halt;
+      ia.F = c->F;
+      ia.Fp = c->Fp;
+      ia.R = c->R;
+      ia.nu = ia.no = 0;
+      for (int j = 0; j < J; ++j)
+        for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) {
+          if (c->spat_free[j])
+            ia.upd[ia.nu++] = r;
+          else
+            ia.oth[ia.no++] = r;
+        }
+      prof_begin(c, KMIXI);
+      k_mix_inst<<<1, 256, 0, c->stream>>>(ia);
+      prof_end(c, KMIXI);
+      FASST_LAUNCH_CHECK();
+    }
+  }
+  (void)all_free;
+  if ((st = spectral_update(c, omega))) return st;
   return launch_renorm(c, iter);
 }
 
@@ -3507,6 +3661,31 @@ int fasst_get_spectral(fasst_ctx *c, int j, double *FB, double *FW, double *TW) 
     FASST_HIP(hipMemcpy2DAsync(TW, c->T * sizeof(double), c->TW.p + (size_t)j * KP * c->Tp,
                                c->Tp * sizeof(double), c->T * sizeof(double), K,
                                hipMemcpyDeviceToHost, c->stream));
+  FASST_HIP(hipStreamSynchronize(c->stream));
+  return FASST_OK;
+}
+
+int fasst_spectral_update(fasst_ctx *c, const double *hat_W, double omega) {
+  int st = need_model(c, 0);
+  if (st) return st;
+  if (!hat_W) return FASST_ERR_SHAPE;
+  if (c->KP > 64 && c->multi) {
+    set_error("K > 64: the single-component spectral path only");
+    return FASST_ERR_UNSUPPORTED;
+  }
+  DeviceGuard g(c->device);
+  const size_t n = (size_t)c->J * c->F * c->T;
+  DBuf<double> dh;
+  if ((st = dh.alloc_uninit(n))) return st;
+  FASST_HIP(hipMemcpyAsync(dh.p, hat_W, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  FASST_HIP(hipMemsetAsync(c->flags.p, 0, kNFlags * sizeof(int), c->stream));
+  c->halt = nullptr;
+  if ((st = launch_spectral_prep(c, false)) || (st = launch_w_old(c))) return st;
+  FASST_HIP(hipMemsetAsync(c->hatW.p, 0, (size_t)c->J * c->Tp * c->Fp * sizeof(double), c->stream));
+  k_rho_from_hatw<<<dim3((c->F + 63) / 64, (c->T + 3) / 4, c->J), 256, 0, c->stream>>>(
+      dh.p, c->Wkf.p, c->TW.p, c->hatW.p, c->F, c->T, c->Fp, c->Tp, c->KP);
+  FASST_LAUNCH_CHECK();
+  if ((st = spectral_update(c, omega))) return st;
   FASST_HIP(hipStreamSynchronize(c->stream));
   return FASST_OK;
 }

@@ -169,13 +169,11 @@ int dgemm2(hipStream_t s, int M, int N, int K, const double *A, int lda, const d
   g.K = K;
   const bool a16 = lda % 2 == 0 && ((uintptr_t)A & 15) == 0;
   const bool b16 = ldb % 2 == 0 && ((uintptr_t)B & 15) == 0;
-#ifndef FASST_D2BUF
-#define FASST_D2BUF 0
-#endif
-  // raw-buffer pieces: operands within 2 GB (32-bit byte offsets)
+  // raw-buffer LDS-DMA pieces (operands within 2 GB: 32-bit byte offsets);
+  // the stereo SIMM iteration 9.19 -> 8.80 ms against the flat-address form
   const bool fits = (size_t)K * lda * sizeof(double) < (1ull << 31) &&
                     (size_t)K * ldb * sizeof(double) < (1ull << 31);
-  if (FASST_D2BUF && a16 && b16 && fits) return launch_dgemm2<D2Prod, false, false, true>(s, g);
+  if (a16 && b16 && fits) return launch_dgemm2<D2Prod, false, false, true>(s, g);
   if (a16 && b16) return launch_dgemm2<D2Prod, false, false>(s, g);
   if (a16) return launch_dgemm2<D2Odd, false, true>(s, g);
   if (b16) return launch_dgemm2<D2Odd, true, false>(s, g);

@@ -1177,11 +1177,9 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
   const size_t slab = (size_t)no * F * R;
   dim3 grid(1, (F + 63) / 64, sp.nz);
   const SPl p = planes(c, true);
-#ifndef FASST_HMT16
-#define FASST_HMT16 0
-#endif
   // 16-byte frame pairs: even N (rows 16-byte aligned) and even chunks
-  const bool v16 = FASST_HMT16 && N % 2 == 0 && sp.kchunk % 2 == 0;
+  // (the stereo SIMM iteration 8.80 -> 8.61 ms against 8-byte frames)
+  const bool v16 = N % 2 == 0 && sp.kchunk % 2 == 0;
   kdispatch(c->K, [&](auto km) {
     constexpr int KM = decltype(km)::value;
     if (c->stereo)

@@ -11,6 +11,22 @@ from . import _lib
 from ._lib import check, dptr, iptr, lib
 
 
+def wiener_gain(device, sdiag, soff, idiag, ioff):
+    """compute_Wiener_gain_2d on the device (fasst_wiener_gain): WG [2, 2, *soff.shape]."""
+    sdiag = np.ascontiguousarray(sdiag, dtype=np.float64)
+    idiag = np.ascontiguousarray(idiag, dtype=np.float64)
+    soff = np.ascontiguousarray(soff, dtype=np.complex128)
+    ioff = np.ascontiguousarray(ioff, dtype=np.complex128)
+    shp = soff.shape
+    if sdiag.shape != (2,) + shp or idiag.shape != (2,) + shp or ioff.shape != shp:
+        raise ValueError("Wiener gain operands %s %s %s %s"
+                         % (sdiag.shape, shp, idiag.shape, ioff.shape))
+    WG = np.empty((2, 2) + shp, dtype=np.complex128)
+    check(lib.fasst_wiener_gain(int(device), int(soff.size), dptr(sdiag), dptr(soff),
+                                dptr(idiag), dptr(ioff), dptr(WG)), "compute_Wiener_gain_2d")
+    return WG
+
+
 class Engine(object):
     """Device state of one FASST model: observation (Cx, STFT) + parameters."""
 
@@ -204,6 +220,78 @@ class Engine(object):
                                            int(nfft), int(hop), dptr(out)),
               "fasst_separate_waveforms")
         return out
+
+    # ------------------------------------------------------------ step methods
+    def source_powers(self, j0, nj, colmasks=None):
+        """V [nj, F, T] of spatial components j0 .. j0+nj-1 (fasst_source_powers)."""
+        out = np.empty((nj, self.F, self.T))
+        mp = None
+        if colmasks is not None:
+            m = np.ascontiguousarray(colmasks, dtype=np.uint64)
+            mp = m.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))
+        check(lib.fasst_source_powers(self._h, int(j0), int(nj), mp, dptr(out)),
+              "fasst_source_powers")
+        return out
+
+    def suff_stat(self, V, mix, psd):
+        """compute_suff_stat on the resident Cx (fasst_suff_stat):
+        (hat_Rxx [3, F], hat_Rxs [F, 2, R], hat_Rss [F, R, R], hat_Ws [R, F, T], loglik)."""
+        V = np.ascontiguousarray(V, dtype=np.float64)
+        mix = np.ascontiguousarray(mix, dtype=np.complex128)
+        psd = np.ascontiguousarray(np.broadcast_to(psd, (self.F,)), dtype=np.float64)
+        R = V.shape[0]
+        if V.shape != (R, self.F, self.T) or mix.shape != (R, 2, self.F):
+            raise ValueError("spat_comp_powers %s / mix_matrix %s for F=%d, T=%d"
+                             % (V.shape, mix.shape, self.F, self.T))
+        rxx = np.empty((3, self.F), dtype=np.complex128)
+        rxs = np.empty((self.F, 2, R), dtype=np.complex128)
+        rss = np.empty((self.F, R, R), dtype=np.complex128)
+        ws = np.empty((R, self.F, self.T))
+        ll = np.zeros(1)
+        check(lib.fasst_suff_stat(self._h, R, dptr(V), dptr(mix), dptr(psd), dptr(rxx), dptr(rxs),
+                                  dptr(rss), dptr(ws), dptr(ll)), "compute_suff_stat")
+        return rxx, rxs, rss, ws, ll[0]
+
+    def mix_solve(self, rss, rxs, mix, kind):
+        """update_mix_matrix's solves, mix [R, 2, F] complex128 updated in place."""
+        rss = np.ascontiguousarray(rss, dtype=np.complex128)
+        rxs = np.ascontiguousarray(rxs, dtype=np.complex128)
+        k = np.ascontiguousarray(kind, dtype=np.int32)
+        R = k.size
+        if mix.dtype != np.complex128 or not mix.flags['C_CONTIGUOUS'] or \
+                mix.shape != (R, 2, self.F):
+            raise ValueError("mix_matrix must be a C-contiguous complex128 (%d, 2, %d) array"
+                             % (R, self.F))
+        check(lib.fasst_mix_solve(self.device, self.F, R, dptr(rss), dptr(rxs), dptr(mix),
+                                  iptr(k)), "update_mix_matrix")
+
+    def spectral_update(self, hat_W, omega):
+        hat_W = np.ascontiguousarray(hat_W, dtype=np.float64)
+        if hat_W.shape != (len(self.structure[0]), self.F, self.T):
+            raise ValueError("hat_W shape %s" % (hat_W.shape,))
+        check(lib.fasst_spectral_update(self._h, dptr(hat_W), float(omega)),
+              "update_spectral_components")
+
+    def sigma_comp(self, j, colmask):
+        diag = np.empty((2, self.F, self.T))
+        off = np.empty((self.F, self.T), dtype=np.complex128)
+        check(lib.fasst_sigma_comp(self._h, int(j), int(colmask), dptr(diag), dptr(off)),
+              "compute_sigma_comp_2d")
+        return diag, off
+
+    def inv_sigma_mix(self, diag, off, psd):
+        diag = np.ascontiguousarray(diag, dtype=np.float64)
+        off = np.ascontiguousarray(off, dtype=np.complex128)
+        n = diag.shape[0]
+        if diag.shape != (n, 2, self.F, self.T) or off.shape != (n, self.F, self.T):
+            raise ValueError("sigma_comps_diag %s / sigma_comps_off %s" % (diag.shape, off.shape))
+        psd = np.ascontiguousarray(np.broadcast_to(psd, (self.F,)), dtype=np.float64)
+        idiag = np.empty((2, self.F, self.T))
+        ioff = np.empty((self.F, self.T), dtype=np.complex128)
+        check(lib.fasst_inv_sigma_mix(self.device, n, self.F, self.T, dptr(diag), dptr(off),
+                                      dptr(psd), dptr(idiag), dptr(ioff)),
+              "compute_inv_sigma_mix_2d")
+        return idiag, ioff
 
     def wiener_images(self, psd, X=None):
         psd = np.ascontiguousarray(psd, dtype=np.float64)

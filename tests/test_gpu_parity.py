@@ -218,6 +218,10 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (97, 150, 2, 100, 2, 3),     # K = 100
     (65, 77, 4, 128, 1, 2),      # K = 128 on 4 sources
     (129, 90, 3, 72, [1, 2, 1], 3),  # K = 72, mixed ranks
+    # K > 64 with more than 4 sources (the VR E-step with its W operand from L2)
+    (65, 77, 8, 128, 1, 2),      # J = 8, K = 128
+    (33, 40, 5, 70, 2, 2),       # J = 5, K = 70, total rank 10
+    (49, 52, 6, 100, [1, 2, 1, 2, 1, 2], 2),  # J = 6, K = 100, mixed ranks
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
@@ -236,11 +240,8 @@ def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
 
 
 def test_k_above_64_outside_single_component_path_fails_loudly():
-    """K > 64 runs the single-component path only (at most 4 spatial
-    components, fixed FW): other structures raise instead of running."""
-    m, o, X = _c3_like(33, 40, 5, 70, 1, 1)
-    with pytest.raises(NotImplementedError):
-        m.estim_param_a_post_model()
+    """K > 64 runs the single-component path only (one spectral component per
+    spatial component, fixed FW): other structures raise instead of running."""
     m, o, X = _c3_like(33, 40, 2, 70, 1, 1)
     m.spec_comps[0]['factor'][0]['FW_frdm_prior'] = 'free'
     with pytest.raises(NotImplementedError):
