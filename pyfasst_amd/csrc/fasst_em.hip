@@ -352,6 +352,16 @@ void k_estep_mx(const EArgs a) {
   }
   __syncthreads();
 
+  // CJR (J >= 4): the lane's Sigma_x coefficients in registers for the
+  // whole kernel (J = 8: 474 -> 240 LDS reads and 243 -> 84 waits per tile,
+  // E-step 1.00 -> 0.98 ms; J = 4: 0.372 -> 0.364 ms, same-box A/B)
+  constexpr bool CJR = J >= 4;
+  double cjr[CJR ? J : 1][4];
+  if constexpr (CJR)
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) cjr[j][c] = s_cj[(j * 4 + c) * 16 + fl];
   double inv_rk[J];
 #pragma unroll
   for (int j = 0; j < J; ++j)
@@ -479,6 +489,9 @@ void k_estep_mx(const EArgs a) {
                      WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
     }
     const double *cj = s_cj + lofs + fl;
+    // the lane's Sigma_x coefficients: LDS (re-read per tile) or, with
+    // CJR, the registers loaded once per kernel
+    auto cjv = [&](int j, int c) { return CJR ? cjr[j][c] : cj[(j * 4 + c) * 16]; };
     // point i of the lane's four (frame t0 + tq + 4 i): Sigma_x, its guarded
     // inverse, loglik, P = Cx S, N = S Cx S - S, and rho stored; no LDS
     auto pt_valu = [&](int i, double (&P)[8], double (&N)[4]) {
@@ -491,10 +504,10 @@ void k_estep_mx(const EArgs a) {
       double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        d0 += cj[(j * 4 + 0) * 16] * V[j];
-        d1 += cj[(j * 4 + 1) * 16] * V[j];
-        ore += cj[(j * 4 + 2) * 16] * V[j];
-        oim += cj[(j * 4 + 3) * 16] * V[j];
+        d0 += cjv(j, 0) * V[j];
+        d1 += cjv(j, 1) * V[j];
+        ore += cjv(j, 2) * V[j];
+        oim += cjv(j, 3) * V[j];
       }
       // inv_herm_mat_2d (signalTools.py:177-194)
       double det = d0 * d1 - (ore * ore + oim * oim);
@@ -539,8 +552,8 @@ void k_estep_mx(const EArgs a) {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const double Vj = V[j];
-        const double qa = (cj[(j * 4 + 0) * 16] * N[0] + cj[(j * 4 + 1) * 16] * N[1]) +
-                          2.0 * (cj[(j * 4 + 2) * 16] * N[2] + cj[(j * 4 + 3) * 16] * N[3]);
+        const double qa = (cjv(j, 0) * N[0] + cjv(j, 1) * N[1]) +
+                          2.0 * (cjv(j, 2) * N[2] + cjv(j, 3) * N[3]);
         const double q = RKU == 1 ? qa : qa * inv_rk[j];
         const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
         if constexpr (SA)
@@ -572,11 +585,12 @@ void k_estep_mx(const EArgs a) {
             wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
       }
     };
-    // SWP (J > 4): the next point's VALU work sits between this point's slab
-    // reads and its MFMAs.  Neutral at J <= 4 (0.376-0.381 vs 0.380-0.382 ms
-    // at C3); at J > 4 the unpipelined form trips ROCm 7.2's AGPR-copy
-    // rewrite pass (J = 8, K = 64)
-    constexpr bool SWP = J > 4;
+    // SWP (J >= 4): the next point's VALU work sits between this point's slab
+    // reads and its MFMAs (J = 4 with the reader-formed pairs: 0.370 -> 0.367
+    // ms alone, 0.373 -> 0.3625 with CJR; with the writer-formed pairs it was
+    // neutral; at J > 4 the unpipelined form also tripped ROCm 7.2's
+    // AGPR-copy rewrite pass)
+    constexpr bool SWP = J >= 4;
     auto slab_fence = [&]() {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();

@@ -127,9 +127,6 @@ __device__ __forceinline__ d4 nmfma(double a, double b, d4 c) {
 // row to `part`; the consumer (k_nmf_w_part / k_nmf_h_part) sums the groups
 // in index order: deterministic.
 constexpr int kNmfPW = 2;
-#ifndef NMF_ABLATE
-#define NMF_ABLATE 0  // timing-only ablations (1: no per-tile loads, 2: no ratio VALU, 3: no fold, 4: no tiles)
-#endif
 
 typedef unsigned nmf_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nmf_ld2(__amdgpu_buffer_rsrc_t r, unsigned vo, double &a, double &b) {
@@ -157,27 +154,16 @@ __device__ __forceinline__ constexpr int nmf_con_k(int kc, int fl) {
   return kc < (NKC & ~1) ? 32 * (kc >> 1) + 2 * fl + (kc & 1) : 16 * kc + fl;
 }
 
-#ifndef NMF_SPREAD
-#define NMF_SPREAD 1
-#endif
-#ifndef NMF_FOLD4
-#define NMF_FOLD4 1
-#endif
-#ifndef NMF_PAIR
-#define NMF_PAIR 1
-#endif
 // interleave a tile's prefetch (NL 16-byte loads) with the first MFMAs of
 // the tile in flight, one load per two MFMAs: issued all at once, the four
 // waves' loads queue on the CU's address unit and hold back their MFMAs
 template <int NKC>
 __device__ __forceinline__ void nmf_spread_loads() {
-  if constexpr (NMF_SPREAD) {
-    constexpr int NL = 4 + 2 * NKC + 4 * (NKC / 2 + (NKC & 1));
+  constexpr int NL = 4 + 2 * NKC + 4 * (NKC / 2 + (NKC & 1));
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // one VMEM read
-      __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);   // two MFMAs
-    }
+  for (int j = 0; j < NL; ++j) {
+    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // one VMEM read
+    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);   // two MFMAs
   }
 }
 
@@ -188,19 +174,8 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[kNmfPW][NKC], d4 (&den)
                                                double *__restrict__ pn, double *__restrict__ pd,
                                                int r0, int R, int wv, int lane) {
   constexpr int NE = kNmfPW * NKC * 4, K = 16 * NKC;
-  if (NMF_ABLATE == 3) {  // timing only: no fold, one store per lane
-    double a = 0.0;
-#pragma unroll
-    for (int p = 0; p < kNmfPW; ++p)
-#pragma unroll
-      for (int kc = 0; kc < NKC; ++kc)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) a += num[p][kc][m] + den[p][kc][m];
-    pn[lane + 64 * wv] = a;
-    return;
-  }
   const int fl = lane & 15, tq = lane >> 4;
-  if (NMF_FOLD4) {
+  {
     // all four partials into LDS at once (NE x 2 KB per wave), one barrier,
     // then each wave sums a quarter of the elements in wave order (the
     // sequential fold's association: bit-identical) and stores them
@@ -228,37 +203,6 @@ __device__ __forceinline__ void nmf_fold_store(d4 (&num)[kNmfPW][NKC], d4 (&den)
         pd[o] = b;
       }
     }
-    return;
-  }
-  __shared__ double red[2][NE][64];
-  for (int w = 0; w < 4; ++w) {
-    if (wv == w) {
-#pragma unroll
-      for (int p = 0; p < kNmfPW; ++p)
-#pragma unroll
-        for (int kc = 0; kc < NKC; ++kc)
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const int e = (p * NKC + kc) * 4 + m;
-            double a = num[p][kc][m], b = den[p][kc][m];
-            if (w) {
-              a = red[0][e][lane] + a;
-              b = red[1][e][lane] + b;
-            }
-            if (w < 3) {
-              red[0][e][lane] = a;
-              red[1][e][lane] = b;
-            } else {
-              const int r = r0 + kNmfPW * (tq + 4 * m) + p, k = nmf_con_k<NKC>(kc, fl);
-              if (r < R) {
-                const size_t o = TR ? (size_t)r * K + k : (size_t)k * R + r;
-                pn[o] = a;
-                pd[o] = b;
-              }
-            }
-          }
-    }
-    __syncthreads();
   }
 }
 
@@ -328,13 +272,8 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double h = v[i];
-#if NMF_ABLATE == 2
-        x[i] = sxv[cs][i][p] * h;
-        y[i] = h;
-#else
         x[i] = sxv[cs][i][p] * nmf_rcp(fmax(h * h, kNmfEps));
         y[i] = nmf_rcp(fmax(h, kNmfEps));
-#endif
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -350,19 +289,7 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
   // The prefetch is unconditional (the last tile again past the end) and its
   // values are consumed on every path, so it can neither be sunk below the
   // MFMAs nor make the compiler's vmcnt waits cover it before they run
-  auto rotate = [&]() {
-#pragma unroll
-    for (int s2 = 0; s2 < NKS; ++s2) th[0][s2] = th[1][s2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) hb[0][i][kc] = hb[1][i][kc];
-#pragma unroll
-      for (int p = 0; p < PW; ++p) sxv[0][i][p] = sxv[1][i][p];
-    }
-  };
   if (tb < te) load(tb, 0);
-#if NMF_PAIR
   // two tiles per trip, slots alternating (no register moves); every load
   // is consumed on every path out of its trip, so none is sunk or waited
   // for early
@@ -378,16 +305,6 @@ __global__ __launch_bounds__(256, 1) void k_nmf_wnum(const double *__restrict__ 
     __builtin_amdgcn_sched_barrier(0);
   }
   if (tt < te) compute(0);
-  if (false)
-#endif
-  for (int tt = tb; tt < (NMF_ABLATE == 4 ? tb : te); ++tt) {
-    if (NMF_ABLATE != 1) load(min(tt + 1, te - 1), 1);
-    if (!NMF_SPREAD) __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs
-    compute(0);
-    nmf_spread_loads<NKC>();
-    __builtin_amdgcn_sched_barrier(0);  // the moves wait for the prefetch
-    rotate();
-  }
   const size_t slab = (size_t)K * F;
   double *pn = part + (size_t)blockIdx.y * 2 * slab;
   nmf_fold_store<NKC, false>(num, den, pn, pn + slab, g0, F, wv, lane);
@@ -465,13 +382,8 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double h = v[i];
-#if NMF_ABLATE == 2
-        x[i] = sxv[cs][i][p] * h;
-        y[i] = h;
-#else
         x[i] = sxv[cs][i][p] * nmf_rcp(fmax(h * h, kNmfEps));
         y[i] = nmf_rcp(fmax(h, kNmfEps));
-#endif
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -482,19 +394,7 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
         }
     }
   };
-  auto rotate = [&]() {  // as k_nmf_wnum
-#pragma unroll
-    for (int s2 = 0; s2 < NKS; ++s2) ao[0][s2] = ao[1][s2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) bw[0][i][kc] = bw[1][i][kc];
-#pragma unroll
-      for (int p = 0; p < PW; ++p) sxv[0][i][p] = sxv[1][i][p];
-    }
-  };
   if (fb < fe) load(fb, 0);
-#if NMF_PAIR
   // two tiles per trip, slots alternating (no register moves); every load
   // is consumed on every path out of its trip, so none is sunk or waited
   // for early
@@ -510,16 +410,6 @@ __global__ __launch_bounds__(256, 1) void k_nmf_hnum(const double *__restrict__ 
     __builtin_amdgcn_sched_barrier(0);
   }
   if (ft < fe) compute(0);
-  if (false)
-#endif
-  for (int ft = fb; ft < (NMF_ABLATE == 4 ? fb : fe); ++ft) {
-    if (NMF_ABLATE != 1) load(min(ft + 1, fe - 1), 1);
-    if (!NMF_SPREAD) __builtin_amdgcn_sched_barrier(0);
-    compute(0);
-    nmf_spread_loads<NKC>();
-    __builtin_amdgcn_sched_barrier(0);  // the moves wait for the prefetch
-    rotate();
-  }
   const size_t slab = (size_t)K * N;
   double *pn = part + (size_t)blockIdx.y * 2 * slab;
   nmf_fold_store<NKC, true>(num, den, pn, pn + slab, t0g, N, wv, lane);
