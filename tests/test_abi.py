@@ -39,3 +39,23 @@ def test_library_is_gfx950_code_object():
     from pyfasst_amd import _lib
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
+
+
+def test_step_abi_refuses_bad_shapes_before_touching_a_device():
+    """The GEM step entry points validate their arguments on the host first:
+    a free 'conv' rank next to other ranks (the reference's solve raises,
+    audioModel.py:856-857) and a total rank above 16 return FASST_ERR_SHAPE
+    with a message, no device call."""
+    import numpy as np
+    from pyfasst_amd import _lib
+    F, R = 5, 3
+    rss = np.zeros((F, R, R), complex)
+    rxs = np.zeros((F, 2, R), complex)
+    mix = np.zeros((R, 2, F), complex)
+    kind = np.array([2, 0, 1], dtype=np.int32)
+    st = _lib.lib.fasst_mix_solve(0, F, R, _lib.dptr(rss), _lib.dptr(rxs), _lib.dptr(mix),
+                                  _lib.iptr(kind))
+    assert st == _lib.FASST_ERR_SHAPE
+    assert "conv" in _lib.last_error()
+    st = _lib.lib.fasst_suff_stat(None, 17, *([None] * 8))
+    assert st == _lib.FASST_ERR_SHAPE
