@@ -122,29 +122,59 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
                                                int J, int Tp, int KP, const int *halt) {
   HALT_GUARD(halt);
   extern __shared__ __attribute__((aligned(16))) double s_f[];
-  constexpr bool fwg = FWG;       // FW read from L2 (its [KP][KP] copy would not fit)
-  double *s_fw = s_f;             // [KP][KP] (KP <= 64)
-  double *s_tw = s_f + (fwg ? 0 : KP * KP);   // [KP][64]
+  // FWG (KP = 128): FW's [KP][KP] copy and the TW tile do not fit LDS
+  // together, so FW goes through it in two halves of its rows q (the
+  // contraction index), each thread keeping its outputs in registers (FW
+  // read straight from L2 was a 1 KB-stride gather per lane: 1.36 ms at
+  // J = 8, K = 128)
+  constexpr bool fwg = FWG;
+  double *s_fw = s_f;                                  // [QH][KP] (q-major, transposed)
+  double *s_tw = s_f + (fwg ? 64 * KP : KP * KP);      // [KP][64]
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
   const int tn = min(64, Tp - t0);
-  if (!fwg)
-    for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
-      const int k = idx / KP, q = idx % KP;  // stored transposed: s_fw[q][k]
-      s_fw[q * KP + k] = FW[(size_t)j * KP * KP + idx];
-    }
-  const double *fwj = FW + (size_t)j * KP * KP;
   for (int idx = threadIdx.x; idx < KP * 64; idx += blockDim.x) {
     const int q = idx >> 6, tl = idx & 63;
     s_tw[idx] = tl < tn ? TW[((size_t)j * KP + q) * Tp + t0 + tl] : 0.0;
+  }
+  if constexpr (fwg) {
+    constexpr int KPG = 128, NO = 64 * KPG / 256;   // outputs per thread
+    double acc[NO];
+#pragma unroll
+    for (int m = 0; m < NO; ++m) acc[m] = 0.0;
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();   // (h = 1: the first half's reads are done)
+      for (int idx = threadIdx.x; idx < 64 * KPG; idx += blockDim.x) {
+        const int k = idx / 64, ql = idx % 64;  // coalesced over q in FW's rows
+        s_fw[ql * KPG + k] = FW[((size_t)j * KPG + k) * KPG + 64 * h + ql];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < NO; ++m) {
+        const int idx = threadIdx.x + 256 * m, tl = idx / KPG, k = idx % KPG;
+        double s = 0.0;
+        for (int ql = 0; ql < 64; ++ql) s += s_fw[ql * KPG + k] * s_tw[(64 * h + ql) * 64 + tl];
+        acc[m] += s;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NO; ++m) {
+      const int idx = threadIdx.x + 256 * m, tl = idx / KPG, k = idx % KPG;
+      if (tl < tn) {
+        FWHt[((size_t)j * Tp + t0 + tl) * KPG + k] = acc[m];
+        if (TWt) TWt[((size_t)j * Tp + t0 + tl) * KPG + k] = s_tw[k * 64 + tl];
+      }
+    }
+    return;
+  }
+  for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
+    const int k = idx / KP, q = idx % KP;  // stored transposed: s_fw[q][k]
+    s_fw[q * KP + k] = FW[(size_t)j * KP * KP + idx];
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < tn * KP; idx += blockDim.x) {
     const int tl = idx / KP, k = idx % KP;
     double s = 0.0;
-    if (fwg)
-      for (int q = 0; q < KP; ++q) s += fwj[k * KP + q] * s_tw[q * 64 + tl];
-    else
-      for (int q = 0; q < KP; ++q) s += s_fw[q * KP + k] * s_tw[q * 64 + tl];
+    for (int q = 0; q < KP; ++q) s += s_fw[q * KP + k] * s_tw[q * 64 + tl];
     FWHt[((size_t)j * Tp + t0 + tl) * KP + k] = s;
     if (TWt) TWt[((size_t)j * Tp + t0 + tl) * KP + k] = s_tw[k * 64 + tl];  // H^T (FW update)
   }
@@ -220,6 +250,9 @@ __device__ __forceinline__ double mfma44(double a, double b, double c) {
 // VR (J > 4): also the per-source pipelined V tile, one wave per SIMD (the
 // register file, not the LDS, bounds it: at two waves the kernel spills
 // 500+ bytes per lane to scratch) and the epilogue one bin group at a time.
+#ifndef ESTEP_VST
+#define ESTEP_VST 1
+#endif
 template <int J>
 struct MXShape {
   static constexpr bool VR = J > 4;
@@ -231,7 +264,12 @@ struct MXShape {
   static constexpr int SP = NVG, SN = NVG + 2, SV2 = NVG + 3;  // set offsets: P lo/hi, N, VV
   static constexpr int NSET = NVG + 3 + (RP ? 0 : NPG);  // V groups | P lo | P hi | N | VV groups
   static constexpr int GS = NSET * 64 + 1;      // doubles per bin group (+1: bank skew)
-  static constexpr int SLAB = 4 * GS;           // doubles per wave
+  // VST (J > 4): the V sets of all four point rounds are written once per
+  // tile, right after the V tile ([round][bin group][NVG sets], VGS each),
+  // then P / N per round ([bin group][3 sets], PGS each)
+  static constexpr bool VST = VR && ESTEP_VST;
+  static constexpr int VGS = NVG * 64 + 1, PGS = 3 * 64 + 1;
+  static constexpr int SLAB = VST ? 16 * VGS + 4 * PGS : 4 * GS;   // doubles per wave
 };
 // RP pair group h: (base, d)
 template <int Q>
@@ -261,7 +299,7 @@ __host__ __device__ constexpr bool rp_live(int h) {
 // K = 128); then the V tiles read their W operand from L2
 template <int J, int NKS>
 __host__ __device__ constexpr bool mx_w_in_lds() {
-  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB) * sizeof(double) <=
+  return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB + J * 4 * 16) * sizeof(double) <=
          160 * 1024;
 }
 template <int J, int NKS>
@@ -372,9 +410,21 @@ void k_estep_mx(const EArgs a) {
   double *wr = slab + (fl >> 2) * S::GS + 16 * tq + 4 * (fl & 3);
   // reader side: operands of lane (X, b, Y) sit at [group][set][lane]
   const double *rd = slab + lane;
+  auto slab_fence0 = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   // RP: W_e = V_{(m + e) mod Q} of the lane's point (m = Y) sits in set
   // ((m + e) mod Q) / 4 at Y' = (m + e) mod 4 of the same (X, b)
   const double *rdq = slab + (lane & ~3);
+  constexpr bool VST = S::VST;
+  // VST: this lane's V of round i at wrv + i 4 VGS (+ (j >> 2) 64 + (j & 3)),
+  // its P / N at wpn; the reader's V of round i, bin group g at
+  // rdq + (4 i + g) VGS, P / N at rpn + g PGS
+  double *wrv = slab + (fl >> 2) * S::VGS + 16 * tq + 4 * (fl & 3);
+  double *wpn = slab + 16 * S::VGS + (fl >> 2) * S::PGS + 16 * tq + 4 * (fl & 3);
+  const double *rpn = slab + 16 * S::VGS + lane;
   int vro[Q];
 #pragma unroll
   for (int e = 0; e < Q; ++e) {
@@ -488,6 +538,13 @@ void k_estep_mx(const EArgs a) {
         v[j] = mfma4(j < JA ? twv[j < JA ? j : 0][s] : tw[(size_t)(4 * s) * a.Tp],
                      WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
     }
+    if constexpr (VST) {
+      slab_fence0();   // the previous tile's last reads before these writes
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] = v[j][i];
+    }
     const double *cj = s_cj + lofs + fl;
     // the lane's Sigma_x coefficients: LDS (re-read per tile) or, with
     // CJR, the registers loaded once per kernel
@@ -499,7 +556,7 @@ void k_estep_mx(const EArgs a) {
       const double x00 = cxv[0][i], x11 = cxv[1][i], xr = cxv[2][i], xi = cxv[3][i];
       double V[J];
 #pragma unroll
-      for (int j = 0; j < J; ++j) V[j] = v[j][i];
+      for (int j = 0; j < J; ++j) V[j] = VST ? wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] : v[j][i];
       // Sigma_x = sum_r V_r a_r a_r^H + PSD I   (compute_suff_stat :613-652)
       double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
 #pragma unroll
@@ -565,6 +622,15 @@ void k_estep_mx(const EArgs a) {
     };
     // point i's MFMA operands -> the wave's slab (reader layout)
     auto pt_write = [&](int i, const double (&P)[8], const double (&N)[4]) {
+      if constexpr (VST) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          wpn[0 * 64 + c] = P[c];
+          wpn[1 * 64 + c] = P[4 + c];
+          wpn[2 * 64 + c] = N[c];
+        }
+        return;
+      }
       double V[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) V[j] = v[j][i];
@@ -591,6 +657,9 @@ void k_estep_mx(const EArgs a) {
     // neutral; at J > 4 the unpipelined form also tripped ROCm 7.2's
     // AGPR-copy rewrite pass)
     constexpr bool SWP = J >= 4;
+#ifndef ESTEP_ILV
+#define ESTEP_ILV 0
+#endif
     auto slab_fence = [&]() {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -600,7 +669,43 @@ void k_estep_mx(const EArgs a) {
     // MFMAs (read -> wait -> MFMA one at a time left the LDS latency exposed);
     // with SWP the next point's VALU work sits between the reads and the
     // MFMAs (its slab writes after them)
-    auto mfma_pass = [&](auto between) {
+    auto mfma_pass = [&](int i, auto between) {
+      if constexpr (VST) {
+        // the bin groups in two halves (half the operands live)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          double w[2][Q], pn[2][3];
+#pragma unroll
+          for (int g2 = 0; g2 < 2; ++g2) {
+            const int g = 2 * hh + g2;
+#pragma unroll
+            for (int e = 0; e < Q; ++e) w[g2][e] = rdq[(4 * i + g) * S::VGS + vro[e]];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) pn[g2][q] = rpn[g * S::PGS + q * 64];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (hh == 0) {
+            between();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int g2 = 0; g2 < 2; ++g2) {
+            const int g = 2 * hh + g2;
+#pragma unroll
+            for (int vg = 0; vg < NVG; ++vg) {
+              xacc[g][vg][0] = mfma44(w[g2][4 * vg], pn[g2][0], xacc[g][vg][0]);
+              xacc[g][vg][1] = mfma44(w[g2][4 * vg], pn[g2][1], xacc[g][vg][1]);
+            }
+#pragma unroll
+            for (int h = 0; h < NPG; ++h)
+              if (rp_live<J>(h))
+                pacc[g][h] = mfma44(w[g2][rp_base<Q>(h)] * w[g2][(rp_base<Q>(h) + rp_d<Q>(h)) & (Q - 1)],
+                                    pn[g2][2], pacc[g][h]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+      }
       if constexpr (RP) {
         // rotated sources W_e, then P lo / hi and N, of the 4 bin groups
         double w[4][Q], pn[4][3];
@@ -614,7 +719,16 @@ void k_estep_mx(const EArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (SWP) {
           between();
-          __builtin_amdgcn_sched_barrier(0);
+          // ILV: the next point's VALU chain and these MFMAs interleaved (one
+          // MFMA per ILV VALU instructions) instead of one after the other
+          if constexpr (ESTEP_ILV == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (SWP && ESTEP_ILV > 0) {
+#pragma unroll
+          for (int u = 0; u < 4 * (2 * NVG + NPG); ++u) {
+            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x2, ESTEP_ILV, 0);
+          }
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -661,7 +775,7 @@ void k_estep_mx(const EArgs a) {
       for (int i = 0; i < 4; ++i) {
         slab_fence();   // point i's slab writes land before the cross-lane reads
         double Pn[8], Nn[4];
-        mfma_pass([&]() {
+        mfma_pass(i, [&]() {
           if (i < 3) pt_valu(i + 1, Pn, Nn);
         });
         slab_fence();   // point i + 1's writes must not overtake point i's reads
@@ -674,7 +788,7 @@ void k_estep_mx(const EArgs a) {
         pt_valu(i, P, N);
         pt_write(i, P, N);
         slab_fence();   // the slab writes land before the cross-lane reads
-        mfma_pass([]() {});
+        mfma_pass(i, []() {});
         slab_fence();   // the next point's writes must not overtake these reads
       }
     }
@@ -2967,7 +3081,11 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
   prof_begin(c, KFWH);
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-  (c->KP > 64 ? k_fwh_t<true> : k_fwh_t<false>)<<<dim3((c->Tp + 63) / 64, J), 256, fw_lds(c, c->KP * 64),
+  if (c->KP > 64)   // FW halves + TW tile: 128 KB of LDS
+    FASST_HIP(hipFuncSetAttribute((const void *)k_fwh_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)((64 + 64) * c->KP * sizeof(double))));
+  (c->KP > 64 ? k_fwh_t<true> : k_fwh_t<false>)<<<dim3((c->Tp + 63) / 64, J), 256,
+            c->KP > 64 ? (64 + 64) * c->KP * sizeof(double) : fw_lds(c, c->KP * 64),
             side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
                     c->halt);
   prof_end(c, KFWH);

@@ -857,12 +857,17 @@ __global__ void k_alpha_update(const double *__restrict__ part, int nb, double *
   alpha[1] = 1 - aR;
 }
 
-// out[r] = sum_n T[r][n] HM[r][n] (diag of (WM^T X) HM^T, :910-918); block per r
-__global__ __launch_bounds__(256) void k_rowdot(const double *__restrict__ T,
-                                                const double *__restrict__ HM,
-                                                double *__restrict__ out, int N) {
+// out_q[r] = sum_n T_q[r][n] HM[r][n] (diag of (WM^T X) HM^T, :910-918) for
+// the four beta operands q = blockIdx.y; block per (r, q)
+struct RowdotArgs {
+  const double *T[4];
+};
+__global__ __launch_bounds__(256) void k_rowdot(const RowdotArgs ta, const double *__restrict__ HM,
+                                                double *__restrict__ outq, int N) {
   __shared__ double s_red[256];
   const int r = blockIdx.x;
+  const double *__restrict__ T = ta.T[blockIdx.y];
+  double *__restrict__ out = outq + (size_t)blockIdx.y * gridDim.x;
   double a = 0.0;
   for (int n = threadIdx.x; n < N; n += 256) a += T[(size_t)r * N + n] * HM[(size_t)r * N + n];
   s_red[threadIdx.x] = a;
@@ -1070,10 +1075,27 @@ static size_t skinny_workspace(int F, int N, int R, int stereo, long slots) {
                   (size_t)hmt_split(F, N, slots).nz * no * F * R);
 }
 
+// the no outputs' split-K slabs ([z][q][n]) summed in z order, one launch
+// (grid.y = q) instead of one per output
+struct SlabDst {
+  double *d[4];
+};
+__global__ void k_slab_reduce(const double *__restrict__ part, int nz, size_t zstride, SlabDst dst,
+                              size_t n) {
+  const double *pq = part + blockIdx.y * n;
+  double *out = dst.d[blockIdx.y];
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int z = 0; z < nz; ++z) s += pq[z * zstride + i];
+    out[i] = s;
+  }
+}
 void reduce_slabs(simm_ctx *c, int no, int nz, size_t n, double *const *dst) {
-  for (int q = 0; q < no; ++q)
-    k_gemm_reduce<<<(int)std::min<size_t>((n + 255) / 256, 4096), 256, 0, c->stream>>>(
-        c->gwork.p + (size_t)q * n, nz, (size_t)no * n, dst[q], n);
+  SlabDst d;
+  for (int q = 0; q < 4; ++q) d.d[q] = q < no ? dst[q] : nullptr;
+  k_slab_reduce<<<dim3((int)std::min<size_t>((n + 255) / 256, 4096), no), 256, 0, c->stream>>>(
+      c->gwork.p, nz, (size_t)no * n, d, n);
 }
 
 // K <= 4 filters (the documented configurations) or <= 8: the per-lane
@@ -1396,10 +1418,10 @@ int simm_iteration(simm_ctx *c, double omega, int update_hgamma, double *reco) {
     double *Cs[4] = {c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N};
     if ((st = wmt_xy(c, Cs))) return st;
   }
-  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p, c->HM.p, c->bd.p, N);
-  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p, c->HM.p, c->bd.p + R, N);
-  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN0.p + (size_t)R * N, c->HM.p, c->bd.p + 2 * R, N);
-  k_rowdot<<<R, 256, 0, c->stream>>>(c->RN1.p + (size_t)R * N, c->HM.p, c->bd.p + 3 * R, N);
+  {
+    const RowdotArgs ta = {{c->RN0.p, c->RN1.p, c->RN0.p + (size_t)R * N, c->RN1.p + (size_t)R * N}};
+    k_rowdot<<<dim3(R, 4), 256, 0, c->stream>>>(ta, c->HM.p, c->bd.p, N);
+  }
   k_beta_update<<<1, 64, 0, c->stream>>>(c->bd.p, c->bR.p, c->bL.p, R, omega);
   return refresh_sm(c);
 }
