@@ -473,6 +473,14 @@ void k_estep_mx(const EArgs a) {
       }
     }
   };
+  // CXE (J > 4): the next tile's Cx loads are issued right after this
+  // tile's last point consumed its Cx (in the pipelined point loop), so they
+  // land during the last point's MFMAs and the next tile's V tile (J = 6 /
+  // 8: 0.790 / 0.961 -> 0.749 / 0.944 ms; at J = 4, two waves per SIMD,
+  // 0.361 -> 0.368 ms: not used there)
+  constexpr bool CXE = J > 4;
+  double cxv[4][4];
+  if (CXE && tb + wvu < te) load_cx(tb + wvu, cxv);
   for (int tt = tb + wvu; tt < te; tt += 4) {
     const int t0 = tt * 16;
     int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
@@ -492,8 +500,7 @@ void k_estep_mx(const EArgs a) {
         twv[j][s] = SA ? es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u)
                        : tw[(size_t)(4 * s) * a.Tp];
     }
-    double cxv[4][4];  // this tile's Cx (in flight with the TW operands)
-    load_cx(tt, cxv);
+    if constexpr (!CXE) load_cx(tt, cxv);  // this tile's Cx (in flight with the TW operands)
     __builtin_amdgcn_sched_barrier(0);
     d4 v[J];
     if constexpr (VR) {
@@ -657,9 +664,7 @@ void k_estep_mx(const EArgs a) {
     // neutral; at J > 4 the unpipelined form also tripped ROCm 7.2's
     // AGPR-copy rewrite pass)
     constexpr bool SWP = J >= 4;
-#ifndef ESTEP_ILV
-#define ESTEP_ILV 0
-#endif
+
     auto slab_fence = [&]() {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -719,16 +724,7 @@ void k_estep_mx(const EArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (SWP) {
           between();
-          // ILV: the next point's VALU chain and these MFMAs interleaved (one
-          // MFMA per ILV VALU instructions) instead of one after the other
-          if constexpr (ESTEP_ILV == 0) __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (SWP && ESTEP_ILV > 0) {
-#pragma unroll
-          for (int u = 0; u < 4 * (2 * NVG + NPG); ++u) {
-            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x2, ESTEP_ILV, 0);
-          }
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -777,6 +773,7 @@ void k_estep_mx(const EArgs a) {
         double Pn[8], Nn[4];
         mfma_pass(i, [&]() {
           if (i < 3) pt_valu(i + 1, Pn, Nn);
+          if (CXE && i == 2 && tt + 4 < te) load_cx(tt + 4, cxv);
         });
         slab_fence();   // point i + 1's writes must not overtake point i's reads
         if (i < 3) pt_write(i + 1, Pn, Nn);
