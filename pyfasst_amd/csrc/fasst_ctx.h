@@ -26,6 +26,9 @@ struct fasst_ctx {
   // consumer, so they overlap the E-step instead of serialising before it
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // the renormalisation's scales and FB / FW / mixing rescale run on the side
+  // stream beside the TW contraction (gem_iteration's fused tail)
+  hipEvent_t ev_tail = nullptr, ev_scales = nullptr, ev_rows = nullptr;
   // observation
   int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
   fasst::DBuf<double> cx;        // 4*Tp*Fp
@@ -72,6 +75,15 @@ struct fasst_ctx {
   fasst::DBuf<double> epart, llpart, bnum, tnum, tden, psd, ll, hsum, rscal, rpmax, rpe, rtpart;
   fasst::DBuf<double> gden, TWt, pnum, pden;  // FW update (free FW)
   int nchunk_r = 1;
+  // fused tail: FB column maxima / mixing energy per k_fb_update block, TW
+  // restart sums per k_tw_update block
+  fasst::DBuf<double> rpmax2, rpe2, rtpart2;
+  int ntb = 1;
+  // W = FB.FW of the renormalised parameters, formed on the side stream by
+  // the fused tail and swapped into Wkf at the iteration's end; w_ready: the
+  // next iteration of the same fasst_run batch skips launch_w_old
+  fasst::DBuf<double> Wkf_next;
+  int w_ready = 0;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart

@@ -250,9 +250,6 @@ __device__ __forceinline__ double mfma44(double a, double b, double c) {
 // VR (J > 4): also the per-source pipelined V tile, one wave per SIMD (the
 // register file, not the LDS, bounds it: at two waves the kernel spills
 // 500+ bytes per lane to scratch) and the epilogue one bin group at a time.
-#ifndef ESTEP_VST
-#define ESTEP_VST 1
-#endif
 template <int J>
 struct MXShape {
   static constexpr bool VR = J > 4;
@@ -267,7 +264,7 @@ struct MXShape {
   // VST (J > 4): the V sets of all four point rounds are written once per
   // tile, right after the V tile ([round][bin group][NVG sets], VGS each),
   // then P / N per round ([bin group][3 sets], PGS each)
-  static constexpr bool VST = VR && ESTEP_VST;
+  static constexpr bool VST = VR;
   static constexpr int VGS = NVG * 64 + 1, PGS = 3 * 64 + 1;
   static constexpr int SLAB = VST ? 16 * VGS + 4 * PGS : 4 * GS;   // doubles per wave
 };
@@ -394,6 +391,7 @@ void k_estep_mx(const EArgs a) {
   // whole kernel (J = 8: 474 -> 240 LDS reads and 243 -> 84 waits per tile,
   // E-step 1.00 -> 0.98 ms; J = 4: 0.372 -> 0.364 ms, same-box A/B)
   constexpr bool CJR = J >= 4;
+  constexpr bool NF = J >= 4;
   double cjr[CJR ? J : 1][4];
   if constexpr (CJR)
 #pragma unroll
@@ -613,12 +611,28 @@ void k_estep_mx(const EArgs a) {
       // (:1521-1575, N1), formed where V is at hand
       // Since V >= 0, rho = |V^2 q + V| / max(V, eps) = |V q + 1| min(V / eps, 1)
       // (q = a^H N a / rk): no reciprocal (the two forms differ by rounding)
+      // NF: the factors 2 (the off-diagonal pair) and 1 / rk (a uniform rank)
+      // folded into N once per point instead of once per source
+      double Nf[4];
+      {
+        const double ir = RKU ? 1.0 / (double)RKU : 1.0;
+        Nf[0] = N[0] * ir;
+        Nf[1] = N[1] * ir;
+        Nf[2] = N[2] * (2.0 * ir);
+        Nf[3] = N[3] * (2.0 * ir);
+      }
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const double Vj = V[j];
-        const double qa = (cjv(j, 0) * N[0] + cjv(j, 1) * N[1]) +
-                          2.0 * (cjv(j, 2) * N[2] + cjv(j, 3) * N[3]);
-        const double q = RKU == 1 ? qa : qa * inv_rk[j];
+        double q;
+        if constexpr (NF) {
+          q = cjv(j, 0) * Nf[0] + cjv(j, 1) * Nf[1] + cjv(j, 2) * Nf[2] + cjv(j, 3) * Nf[3];
+          if constexpr (RKU == 0) q *= inv_rk[j];
+        } else {
+          const double qa = (cjv(j, 0) * N[0] + cjv(j, 1) * N[1]) +
+                            2.0 * (cjv(j, 2) * N[2] + cjv(j, 3) * N[3]);
+          q = RKU == 1 ? qa : qa * inv_rk[j];
+        }
         const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
         if constexpr (SA)
           es_st<2>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
@@ -1350,8 +1364,16 @@ struct UArgs {
   int F, Fp, KP, J, nchunk;
   double omega;
   int kb0[kMaxJ], kb1[kMaxJ], fb_free[kMaxJ];  // columns [kb0, kb1) are updated
+  // fused tail (pmax non-null): the renormalisation's stage-1 statistics of
+  // this block's 16 bins, FB column maxima [J][nft][KP] and ('conv') the
+  // mixing filters' energy [J][nft]
+  double *pmax, *pe;
+  const double2 *A;
+  int roff[kMaxJ + 1];
+  unsigned convm;
   const int *halt;
 };
+__device__ double block_sum(double x, double *s);
 // FB *= (num / max(den, eps))^omega with den = FW . rowsum(TW) (see
 // k_fb_contract) or, for one of several spectral components, the contracted
 // denominator; then W_new = FB . FW in both layouts.
@@ -1409,6 +1431,26 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
     const int k = idx / 16, fl = idx % 16;
     a.Wkf_new[((size_t)j * KP + k) * a.Fp + f0 + fl] = s_wn[fl * (KP + 1) + k];
+  }
+  if (!a.pmax) return;
+  // renormalize_parameters' statistics of the updated FB rows (k_renorm_stats
+  // per 16-bin block; max_f is exact in any order)
+  const int nb = min(16, a.F - f0);
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
+    double m = -INFINITY;
+    for (int fl = 0; fl < nb; ++fl) m = fmax(m, s_fb[fl * KP + k]);
+    a.pmax[((size_t)j * gridDim.x + blockIdx.x) * KP + k] = m;
+  }
+  if (a.convm >> j & 1u) {
+    __shared__ double s_e[256];
+    const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+    double e = 0.0;
+    for (int idx = threadIdx.x; idx < nr * 2 * nb; idx += blockDim.x) {
+      const double2 x = a.A[(size_t)(2 * r0 + idx / nb) * a.Fp + f0 + idx % nb];
+      e += x.x * x.x + x.y * x.y;
+    }
+    e = block_sum(e, s_e);
+    if (threadIdx.x == 0) a.pe[(size_t)j * gridDim.x + blockIdx.x] = e;
   }
 }
 
@@ -1732,6 +1774,12 @@ struct TUArgs {
   int T, Tp, KP, J, nsplit;
   double omega;
   int kb0[kMaxJ], kb1[kMaxJ], tw_free[kMaxJ];  // rows [kb0, kb1) are updated
+  // fused tail (scal non-null): the renormalisation's TW column scale w2
+  // (k_renorm_scales) applied after the update to the K[j] live rows, and the
+  // restart test's partial sums per block into tpart [slot][ntb]
+  const double *scal;
+  double *tpart;
+  int ntb, K[kMaxJ], soff[kMaxJ];
   const int *halt;
 };
 // TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
@@ -1739,6 +1787,47 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
   HALT_GUARD(a.halt);
   __shared__ double s_r[64][65];
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
+  if (a.scal) {
+    // y = fl(fl(TW r) w2): the two roundings of k_tw_update then k_renorm_apply
+    const bool fr = a.tw_free[j];
+    const double *w2 = a.scal + (size_t)j * (2 + 2 * a.KP) + 2 + a.KP;
+    double tsum = 0.0;
+    for (int kb = 0; kb < a.K[j]; kb += 64) {
+      const int kn = min(64, a.K[j] - kb);
+      if (fr)
+        for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
+          const int tl = idx / kn, kl = idx % kn, t = t0 + tl;
+          double r = 1.0;
+          if (t < a.T) {
+            double num = 0.0, den = 0.0;
+            for (int c = 0; c < a.nsplit; ++c) {
+              const size_t o = (((size_t)c * a.J + j) * a.Tp + t) * a.KP + kb + kl;
+              num += a.tnum[o];
+              den += a.tden[o];
+            }
+            const double ratio = num / fmax(den, kEps);
+            r = a.omega == 1.0 ? ratio : pow(ratio, a.omega);
+          }
+          s_r[kl][tl] = r;
+        }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
+        const int kl = idx / 64, tl = idx % 64, t = t0 + tl, k = kb + kl;
+        if (t < a.T) {
+          double *p = a.TW + ((size_t)j * a.KP + k) * a.Tp + t;
+          double x = *p;
+          if (fr && k >= a.kb0[j] && k < a.kb1[j]) x *= s_r[kl][tl];
+          const double y = x * w2[k];
+          *p = y;
+          tsum += y;
+        }
+      }
+      __syncthreads();
+    }
+    tsum = block_sum(tsum, &s_r[0][0]);
+    if (threadIdx.x == 0) a.tpart[(size_t)a.soff[j] * a.ntb + blockIdx.x] = tsum;
+    return;
+  }
   if (!a.tw_free[j]) return;
   // ratios for 64 frames x KP components (coalesced over k), then a
   // transposed, coalesced-over-t read-modify-write of TW
@@ -1891,6 +1980,13 @@ struct RArgs {
   double *pe;     // [J][nchunk] partial mixing-filter energy (conv)
   double *tpart;  // [nslot][nchunk] partial sums of the rescaled TW, per block
   int *flags;
+  // fused tail (k_renorm_scales / _rows / _tail): k_fb_update's statistics
+  // [J][nstat][KP] and [J][nstat], k_tw_update's restart sums [nslot][ntb],
+  // the E-step's loglik partials
+  const double *pmax2, *pe2, *tpart2, *llpart;
+  double *ll_out;
+  double inv_FT;
+  int nstat, ntb, nll;
   int F, T, Fp, Tp, KP, nchunk, tpc, fpc, nslot;
   unsigned convm;    // bit j: spatial component j is 'conv' (per-bin filters in A)
   int K[kMaxJ], roff[kMaxJ + 1];
@@ -2112,6 +2208,129 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
   if (dead) {
     a.flags[kFlagHalt] = 1;
     a.flags[kFlagIter] = iter;
+  }
+}
+
+// Fused tail of gem_iteration (one spectral component per source, no time
+// blobs, fixed FW): the same renormalize_parameters (audioModel.py:1991-2037)
+// with the stage-1 statistics taken by k_fb_update, the scales formed once
+// per source (k_renorm_scales) and the FB / mixing / FW rescale
+// (k_renorm_rows) on the side stream while the TW contraction runs; TW's
+// rescale and restart sums ride in k_tw_update, and k_renorm_tail closes the
+// iteration with the restart test and the loglik sum.
+__global__ __launch_bounds__(256) void k_renorm_scales(const RArgs a) {
+  HALT_GUARD(a.halt);
+  __shared__ double s_red[256];
+  __shared__ double s_w[kMaxKP];
+  __shared__ double s_e;
+  const int j = blockIdx.x, K = a.K[j], KP = a.KP, ns = a.nstat;
+  const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+  const bool cj = a.convm >> j & 1u;
+  if (cj) {
+    double e = 0.0;
+    for (int q = threadIdx.x; q < ns; q += blockDim.x) e += a.pe2[(size_t)j * ns + q];
+    e = block_sum(e, s_red);
+    if (threadIdx.x == 0) s_e = e / (double)(nr * 2 * a.F);
+  } else if (threadIdx.x == 0) {
+    double e = 0.0;
+    for (int q = 0; q < nr * 2; ++q) {
+      const double2 x = a.Pinst[2 * r0 + q];
+      e += x.x * x.x + x.y * x.y;
+    }
+    s_e = e / (double)(nr * 2);
+  }
+  // column maxima over the blocks: thread (g, k) takes blocks q = g mod G
+  const int G = (int)blockDim.x / KP;
+  double m = -INFINITY;
+  if (threadIdx.x < G * KP)
+    for (int q = threadIdx.x / KP; q < ns; q += G)
+      m = fmax(m, a.pmax2[((size_t)j * ns + q) * KP + threadIdx.x % KP]);
+  __syncthreads();
+  if (threadIdx.x < G * KP) s_red[threadIdx.x] = m;
+  __syncthreads();
+  const double e = s_e;
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {   // (KP <= kMaxKP < 256)
+    double x = -INFINITY;
+    for (int g = 0; g < G; ++g) x = fmax(x, s_red[g * KP + k]);
+    const double w = x * e;
+    s_w[k] = w == 0.0 ? 1.0 : w;
+  }
+  __syncthreads();
+  double *sc = a.scal + (size_t)j * (2 + 2 * KP);
+  const double *fw = a.FW + (size_t)j * KP * KP;
+  for (int cc = threadIdx.x; cc < KP; cc += blockDim.x) {
+    double s = 1.0;
+    if (cc < K) {   // FW.mean(axis=0) of the column's spectral component
+      s = 0.0;
+      for (int r = 0; r < K; ++r) s += fw[r * KP + cc] * s_w[r];
+      s /= (double)K;
+      if (s == 0.0) s = 1.0;
+    }
+    sc[2 + cc] = s_w[cc];
+    sc[2 + KP + cc] = s;
+  }
+  if (threadIdx.x == 0) sc[0] = e;
+}
+
+// FB rows of 16 bins (FB e / w), the 'conv' filters / sqrt(e); block x = 0
+// also rescales FW (FW w / w2) and the 'inst' parameters of its source
+__global__ __launch_bounds__(256) void k_renorm_rows(const RArgs a) {
+  HALT_GUARD(a.halt);
+  const int j = blockIdx.y, f0 = blockIdx.x * 16, K = a.K[j], KP = a.KP;
+  const int nb = min(16, a.F - f0);
+  const double *sc = a.scal + (size_t)j * (2 + 2 * KP);
+  const double e = sc[0], se = sqrt(e);
+  for (int idx = threadIdx.x; idx < nb * KP; idx += blockDim.x) {
+    const int k = idx % KP;
+    double *p = a.FB + ((size_t)j * a.Fp + f0 + idx / KP) * KP + k;
+    if (k < K) *p = (*p * e) / sc[2 + k];
+  }
+  const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
+  if (a.convm >> j & 1u) {
+    for (int idx = threadIdx.x; idx < nr * 2 * nb; idx += blockDim.x) {
+      double2 *p = a.A + (size_t)(2 * r0 + idx / nb) * a.Fp + f0 + idx % nb;
+      *p = make_double2(p->x / se, p->y / se);
+    }
+  } else if (blockIdx.x == 0 && threadIdx.x < nr * 2) {
+    double2 *p = a.Pinst + 2 * r0 + threadIdx.x;
+    *p = make_double2(p->x / se, p->y / se);
+  }
+  if (blockIdx.x == 0) {
+    double *FW = a.FW + (size_t)j * KP * KP;
+    for (int idx = threadIdx.x; idx < K * K; idx += blockDim.x) {
+      const int r = idx / K, cc = idx % K;
+      FW[r * KP + cc] = (FW[r * KP + cc] * sc[2 + r]) / sc[2 + KP + cc];
+    }
+  }
+}
+
+// one block: the iteration's loglik (k_loglik's sum) and the TW restart test
+// from k_tw_update's partial sums (audioModel.py:2023)
+__global__ __launch_bounds__(256) void k_renorm_tail(const RArgs a, int iter) {
+  HALT_GUARD(a.halt);
+  __shared__ double s[256];
+  double x = 0.0;
+  for (int i = threadIdx.x; i < a.nll; i += 256) x += a.llpart[i];
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.ll_out[0] = -(s[0] * a.inv_FT);
+  __syncthreads();
+  for (int sl = 0; sl < a.nslot; ++sl) {
+    double t = 0.0;
+    for (int c = threadIdx.x; c < a.ntb; c += 256) t += a.tpart2[(size_t)sl * a.ntb + c];
+    t = block_sum(t, s);
+    if (threadIdx.x == 0) {
+      const int dead = t < kEps ? 1 : 0;
+      a.flags[1 + sl] = dead;
+      if (dead) {
+        a.flags[kFlagHalt] = 1;
+        a.flags[kFlagIter] = iter;
+      }
+    }
   }
 }
 
@@ -2521,6 +2740,12 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(rpmax, (size_t)J * c->nchunk_r * KP);
   ALLOC(rpe, (size_t)J * c->nchunk_r);
   ALLOC(rtpart, (size_t)kMaxSlot * c->nchunk_r);
+  c->ntb = (Tp + 63) / 64;
+  ALLOC(rpmax2, (size_t)J * c->nft * KP);
+  ALLOC(rpe2, (size_t)J * c->nft);
+  ALLOC(rtpart2, (size_t)kMaxSlot * c->ntb);
+  ALLOC(Wkf_next, (size_t)J * KP * Fp);
+  c->w_ready = 0;
 #undef ALLOC
   c->configured = 1;
   return FASST_OK;
@@ -2559,7 +2784,7 @@ static void update_multi(fasst_ctx *c) {
 // Time-blob arguments of step b (only_j as multi_step); which = 0: every
 // block with time blobs, 1: those whose TW is free, 2: those whose TB is free
 static TBArgs tb_args(const fasst_ctx *c, int b, int only_j, int which, double omega) {
-  TBArgs a;
+  TBArgs a{};
   for (int j = 0; j < kMaxJ; ++j) {
     bool on = j < c->J && b < c->nblk[j] && c->tbl[j][b] > 0 && (only_j < 0 || j == only_j);
     if (on && which == 1) on = c->btw[j][b] != 0;
@@ -2605,8 +2830,8 @@ static int launch_tb_h(fasst_ctx *c, const TBArgs &a) {
   return FASST_OK;
 }
 
-static int launch_renorm(fasst_ctx *c, int iter) {
-  RArgs r;
+static RArgs renorm_args(fasst_ctx *c) {
+  RArgs r{};
   r.A = c->A.p;
   r.Pinst = c->Pinst.p;
   r.FB = c->FB.p;
@@ -2641,6 +2866,20 @@ static int launch_renorm(fasst_ctx *c, int iter) {
     r.roff[j] = j <= c->J ? c->roff[j] : c->R;
     r.soff[j] = j <= c->J ? c->soff[j] : c->nslot;
   }
+  r.pmax2 = c->rpmax2.p;
+  r.pe2 = c->rpe2.p;
+  r.tpart2 = c->rtpart2.p;
+  r.llpart = c->llpart.p;
+  r.ll_out = nullptr;
+  r.inv_FT = 1.0 / ((double)c->F * (double)c->T);
+  r.nstat = c->nft;
+  r.ntb = c->ntb;
+  r.nll = c->nchunk_e * c->nft;
+  return r;
+}
+
+static int launch_renorm(fasst_ctx *c, int iter) {
+  RArgs r = renorm_args(c);
   prof_begin(c, KREN);
   k_renorm_stats<<<dim3(c->nchunk_r, c->J), 256, 0, c->stream>>>(r);
   if (c->nchunk_r * c->KP > 64 * 64 || c->KP > 64)
@@ -2650,7 +2889,7 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   k_renorm_final<<<1, 256, 0, c->stream>>>(r, c->J, iter);
   FASST_LAUNCH_CHECK();
   if (c->anytb) {
-    TBRArgs tr;
+    TBRArgs tr{};
     tr.scal = c->rscal.p;
     tr.flags = c->flags.p;
     tr.halt = c->halt;
@@ -2677,6 +2916,48 @@ static int launch_renorm(fasst_ctx *c, int iter) {
     }
   }
   prof_end(c, KREN);
+  return FASST_OK;
+}
+
+// gem_iteration's fused tail (see k_renorm_scales): the single-component
+// path without time blobs or free FW.  Off unless FASST_FAST_TAIL=1 until it
+// has passed the GPU parity suite (built and reviewed, not yet run on a GPU)
+static bool fast_tail(const fasst_ctx *c) {
+  static const int on = [] {
+    const char *v = getenv("FASST_FAST_TAIL");
+    return v ? atoi(v) : 0;
+  }();
+  if (!on || c->multi || c->anytb) return false;
+  for (int j = 0; j < c->J; ++j)
+    if (c->fw_free[j]) return false;
+  return true;
+}
+
+// the scales and the FB / mixing / FW rescale, after k_fb_update: on the side
+// stream (fork) beside the TW contraction; ev_scales gates k_tw_update,
+// ev_rows the iteration's end
+static int launch_tail_side(fasst_ctx *c, bool fork) {
+  const RArgs r = renorm_args(c);
+  hipStream_t side = fork ? c->aux : c->stream;
+  if (fork) {
+    FASST_HIP(hipEventRecord(c->ev_tail, c->stream));
+    FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_tail, 0));
+  }
+  prof_begin(c, KREN);
+  k_renorm_scales<<<c->J, 256, 0, side>>>(r);
+  FASST_LAUNCH_CHECK();
+  if (fork) FASST_HIP(hipEventRecord(c->ev_scales, c->aux));
+  k_renorm_rows<<<dim3(c->nft, c->J), 256, 0, side>>>(r);
+  FASST_LAUNCH_CHECK();
+  prof_end(c, KREN);
+  // the next iteration's W (the TW contraction still reads Wkf)
+  prof_begin(c, KW);
+  (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, c->J), 256,
+                fw_lds(c, 16 * (c->KP + 1)), side>>>(c->FB.p, c->FW.p, c->Wkf_next.p, nullptr,
+                                                     c->J, c->Fp, c->KP, c->halt);
+  prof_end(c, KW);
+  FASST_LAUNCH_CHECK();
+  if (fork) FASST_HIP(hipEventRecord(c->ev_rows, c->aux));
   return FASST_OK;
 }
 
@@ -2806,12 +3087,24 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
 // one step: block b of every source that has one (only_j < 0), or of source
 // only_j alone (lambdaCorr > 0: the penalty couples the sources, so the
 // components go one at a time in the reference's key order)
+// The fused-tail pointers of k_fb_update / k_tw_update are null or the
+// context's own buffers; anything else is refused here, on the host, before a
+// kernel could dereference it (an uninitialised argument struct on the
+// multi-block path once sent garbage pointers to the device)
+static int check_tail_args(const fasst_ctx *c, const UArgs &u, const TUArgs &tu) {
+  const bool ok_u = !u.pmax || (u.pmax == c->rpmax2.p && u.pe == c->rpe2.p && u.A == c->A.p);
+  const bool ok_t = !tu.scal || (tu.scal == c->rscal.p && tu.tpart == c->rtpart2.p);
+  if (ok_u && ok_t) return FASST_OK;
+  set_error("internal: fused renormalisation arguments do not point at the context's buffers");
+  return FASST_ERR_SHAPE;
+}
+
 static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
   const int J = c->J, nkc = c->KP / 16;
   const size_t plane = (size_t)J * c->Tp * c->Fp;
   const bool lam = c->lambda > 0.0;
   {
-    MPArgs mp;
+    MPArgs mp{};
     mp.TW = c->TW.p;
     mp.Wkf = c->Wkf.p;
     mp.hatW = c->hatW.p;
@@ -2832,7 +3125,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     mp.tpc = c->tpc_b;
     mp.first = b == 0;
     mp.halt = c->halt;
-    BArgs bb;
+    BArgs bb{};
     bb.TW = c->TW.p;
     bb.Wkf = c->Wkf.p;
     bb.FWHt = c->FWHt.p;
@@ -2851,7 +3144,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     bb.nft = c->nft;
     bb.tpc = c->tpc_b;
     bb.zbase = bb.tbase = 0;
-    UArgs u;
+    UArgs u{};   // (pmax null: no fused-tail statistics on this path)
     u.FB = c->FB.p;
     u.FW = c->FW.p;
     u.bnum = c->bnum.p;
@@ -2866,7 +3159,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     u.J = J;
     u.nchunk = c->nchunk_b;
     u.omega = omega;
-    TArgs t;
+    TArgs t{};
     t.TW = c->TW.p;
     t.Wkf_old = c->Wkf.p;
     t.Wkf_new = c->Wkf_new.p;
@@ -2884,7 +3177,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     t.nft = c->nft;
     t.ntt = c->ntt;
     t.fpc = c->fpc_t;
-    TUArgs tu;
+    TUArgs tu{};   // (scal null: the plain TW update)
     tu.TW = c->TW.p;
     tu.tnum = c->tnum.p;
     tu.tden = c->tden.p;
@@ -2934,6 +3227,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
         break;
     }
     FASST_LAUNCH_CHECK();
+    if (int st = check_tail_args(c, u, tu)) return st;
     (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
                   fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
                   c->stream>>>(u);
@@ -2943,7 +3237,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     if (any_fw) {
       // FW update of the step's components (:1578-1631): V_mid = (FB_new FW) H
       // of the component, then W_new rebuilt with FW_new
-      FWArgs w;
+      FWArgs w{};
       w.TW = c->TW.p;
       w.TWt = c->TWt.p;
       w.Wkf_old = c->Wkf.p;
@@ -3095,14 +3389,16 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
 
 // update_spectral_components (audioModel.py:1469-1978) from the rho planes in
 // c->hatW (rho_j = hat_W_j / max(V_j, eps), V from the parameters before the
-// update), after launch_spectral_prep and launch_w_old
-static int spectral_update(fasst_ctx *c, double omega) {
+// update), after launch_spectral_prep and launch_w_old.  tail (fast_tail
+// models inside gem_iteration): 1 = the fused renormalisation tail on the
+// main stream, 2 = its side-stream part forked beside the TW contraction
+static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   const int J = c->J;
   const int nkc = c->KP / 16;
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
   if (c->multi) return multi_spectral(c, omega);
-  BArgs b;
+  BArgs b{};
   b.TW = c->TW.p;
   b.Wkf = c->Wkf.p;
   b.FWHt = c->FWHt.p;
@@ -3123,7 +3419,7 @@ static int spectral_update(fasst_ctx *c, double omega) {
   b.zbase = b.tbase = 0;
   for (int j = 0; j < kMaxJ; ++j) b.fb_free[j] = j < J ? c->fb_free[j] : 0;
   // spectral update: FB then TW (one NMF factor per source)
-  TArgs t;
+  TArgs t{};
   t.TW = c->TW.p;
   t.Wkf_old = c->Wkf.p;
   t.Wkf_new = c->Wkf_new.p;
@@ -3143,7 +3439,7 @@ static int spectral_update(fasst_ctx *c, double omega) {
   t.fpc = c->fpc_t;
   t.cp = t.pw = t.oth = nullptr;
   t.omega = omega;
-  TUArgs tu;
+  TUArgs tu{};
   tu.TW = c->TW.p;
   tu.tnum = c->tnum.p;
   tu.halt = c->halt;
@@ -3154,7 +3450,7 @@ static int spectral_update(fasst_ctx *c, double omega) {
   tu.J = J;
   tu.nsplit = c->nsplit_t;
   tu.omega = omega;
-  UArgs u;
+  UArgs u{};
   u.FB = c->FB.p;
   u.FW = c->FW.p;
   u.bnum = c->bnum.p;
@@ -3169,6 +3465,18 @@ static int spectral_update(fasst_ctx *c, double omega) {
   u.nchunk = c->nchunk_b;
   u.omega = omega;
   u.bden = nullptr;
+  u.pmax = tail ? c->rpmax2.p : nullptr;
+  u.pe = c->rpe2.p;
+  u.A = c->A.p;
+  u.convm = c->convm;
+  for (int j = 0; j <= kMaxJ; ++j) u.roff[j] = j <= J ? c->roff[j] : c->R;
+  tu.scal = tail ? c->rscal.p : nullptr;
+  tu.tpart = c->rtpart2.p;
+  tu.ntb = c->ntb;
+  for (int j = 0; j < kMaxJ; ++j) {
+    tu.K[j] = j < J ? c->K[j] : 0;
+    tu.soff[j] = j < J ? c->soff[j] : 0;
+  }
   for (int j = 0; j < kMaxJ; ++j) {
     const bool in = j < J;
     tu.kb0[j] = u.kb0[j] = t.kb0[j] = 0;
@@ -3183,16 +3491,19 @@ static int spectral_update(fasst_ctx *c, double omega) {
     default: launch_contract<8>(c, b, t, true); break;
   }
   FASST_LAUNCH_CHECK();
+  if (int st = check_tail_args(c, u, tu)) return st;
   prof_begin(c, KFBU);
   (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
                 fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
                 c->stream>>>(u);
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
+  if (tail)
+    if (int st = launch_tail_side(c, tail == 2)) return st;
   if (any_fw) {
     // FW update (:1578-1631) between the FB and TW updates; W_new = FB_new FW_old
     // from k_fb_update is the V_mid operand, then W_new is rebuilt with FW_new
-    FWArgs w;
+    FWArgs w{};
     w.TW = c->TW.p;
     w.TWt = c->TWt.p;
     w.Wkf_old = c->Wkf.p;
@@ -3245,8 +3556,9 @@ static int spectral_update(fasst_ctx *c, double omega) {
     default: launch_contract<8>(c, b, t, false); break;
   }
   FASST_LAUNCH_CHECK();
+  if (tail == 2) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_scales, 0));
   prof_begin(c, KTWU);
-  k_tw_update<<<dim3((c->Tp + 63) / 64, J), 256, 0, c->stream>>>(tu);
+  k_tw_update<<<dim3(c->ntb, J), 256, 0, c->stream>>>(tu);
   prof_end(c, KTWU);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
@@ -3298,11 +3610,12 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   const bool fork = !c->prof;
   int st = launch_spectral_prep(c, fork);
   if (st) return st;
-  st = launch_w_old(c);
-  if (st) return st;
+  const bool w_ready = c->w_ready;   // (the previous iteration's fused tail formed W)
+  c->w_ready = 0;
+  if (!w_ready && (st = launch_w_old(c))) return st;
   st = build_inst_A(c);
   if (st) return st;
-  EArgs e;
+  EArgs e{};
   e.cx00 = c->cx.p;
   e.cx11 = c->cx.p + (size_t)c->Tp * c->Fp;
   e.cxr = c->cx.p + 2 * (size_t)c->Tp * c->Fp;
@@ -3329,11 +3642,14 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   launch_estep(c, e, c->nchunk_e);
   FASST_LAUNCH_CHECK();
   if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
-  prof_begin(c, KLL);
-  k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
-                                     1.0 / ((double)c->F * (double)c->T), c->halt);
-  prof_end(c, KLL);
-  FASST_LAUNCH_CHECK();
+  const bool ft = fast_tail(c);
+  if (!ft) {   // (fused tail: summed by k_renorm_tail)
+    prof_begin(c, KLL);
+    k_loglik<<<1, 256, 0, c->stream>>>(c->llpart.p, c->nchunk_e * c->nft, ll_dev,
+                                       1.0 / ((double)c->F * (double)c->T), c->halt);
+    prof_end(c, KLL);
+    FASST_LAUNCH_CHECK();
+  }
   // mixing update
   bool any_free = false, all_free = true;
   for (int j = 0; j < J; ++j) {
@@ -3341,7 +3657,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     all_free &= c->spat_free[j] != 0;
   }
   if (any_free) {
-    MArgs m;
+    MArgs m{};
     m.part = c->epart.p;
     m.Wkf = c->Wkf.p;
     m.hsum = c->hsum.p;
@@ -3366,7 +3682,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     prof_end(c, KMIX);
     FASST_LAUNCH_CHECK();
     if (!c->conv) {
-      IArgs ia;
+      IArgs ia{};
       ia.rss = c->rss.p;
       ia.rxs = c->rxs.p;
       ia.A = c->A.p;
@@ -3391,8 +3707,18 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     }
   }
   (void)all_free;
-  if ((st = spectral_update(c, omega))) return st;
-  return launch_renorm(c, iter);
+  if ((st = spectral_update(c, omega, ft ? (fork ? 2 : 1) : 0))) return st;
+  if (!ft) return launch_renorm(c, iter);
+  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
+  RArgs r = renorm_args(c);
+  r.ll_out = ll_dev;
+  prof_begin(c, KLL);
+  k_renorm_tail<<<1, 256, 0, c->stream>>>(r, iter);
+  prof_end(c, KLL);
+  FASST_LAUNCH_CHECK();
+  std::swap(c->Wkf.p, c->Wkf_next.p);
+  c->w_ready = 1;
+  return FASST_OK;
 }
 
 }  // namespace fasst
@@ -3433,7 +3759,10 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_scales, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_rows, hipEventDisableTiming) != hipSuccess) {
     set_error("hipStreamCreate / hipEventCreate failed");
     st = FASST_ERR_DEVICE;
   }
@@ -3500,6 +3829,10 @@ int fasst_destroy(fasst_ctx *c) {
     c->rpmax.release();
     c->rpe.release();
     c->rtpart.release();
+    c->rpmax2.release();
+    c->rpe2.release();
+    c->rtpart2.release();
+    c->Wkf_next.release();
     c->mplanes.release();
     c->bden.release();
     for (int i = 0; i < fasst_ctx::kNK; ++i) {
@@ -3508,6 +3841,9 @@ int fasst_destroy(fasst_ctx *c) {
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
+    if (c->ev_scales) (void)hipEventDestroy(c->ev_scales);
+    if (c->ev_rows) (void)hipEventDestroy(c->ev_rows);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
@@ -3863,6 +4199,7 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   // host reads the flags once at the end.  Profiling keeps one sync per
   // iteration so the per-kernel events can be folded.
   c->halt = c->flags.p + kFlagHalt;
+  c->w_ready = 0;
   const int sync_every = c->prof ? 1 : n_iter;
   int done = 0;
   for (int it = 0; it < n_iter; ++it) {
