@@ -4217,6 +4217,13 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
     if (c->h_flags[kFlagHalt] || c->h_flags[0]) break;
   }
   c->halt = nullptr;
+  // a halted batch skipped its later iterations' kernels while the host still
+  // swapped the fused tail's W buffers: rebuild W = FB.FW from the parameters
+  if (c->w_ready && (c->h_flags[kFlagHalt] || c->h_flags[0])) {
+    if ((st = launch_w_old(c))) return st;
+    FASST_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->w_ready = 0;
   if (c->h_flags[0]) {
     set_error("Singular Matrix");
     return FASST_ERR_SINGULAR;
