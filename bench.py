@@ -84,7 +84,27 @@ def iteration_work(F, T, J, R, K):
 ITERATION_KERNELS = ("k_w_from_fb", "k_fwh_t", "k_tw_rowsum", "k_inst_A", "k_estep_part1",
                      "k_estep_part2", "k_estep", "k_loglik", "k_mix", "k_mix_inst",
                      "k_fb_contract", "k_fb_update", "k_tw_contract", "k_tw_update",
-                     "k_renorm_stats", "k_renorm_apply", "k_renorm_final")
+                     "k_renorm_stats", "k_renorm_apply", "k_renorm_final", "k_renorm_scales",
+                     "k_renorm_rows", "k_renorm_tail")
+
+
+PROF_STEPS = 64   # iterations of the per-kernel timing pass (two event rings)
+
+
+def pmc_file(J, K, T, rounds=range(9, 0, -1)):
+    """The newest committed rocprofv3 FETCH / WRITE summary of THIS
+    configuration (tools/gpu_prof.sh + tools/summarize_prof.py):
+    profiles/rN_bench.json for the headline, rN_bench_J<J>K<K>.json for a
+    structure variant; None if there is none."""
+    if T != T_FRAMES:
+        return None
+    default_cfg = (J, K) == (J_SRC, K_NMF)
+    for r in rounds:
+        name = "r%d_bench.json" % r if default_cfg else "r%d_bench_J%dK%d.json" % (r, J, K)
+        p = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(p):
+            return p
+    return None
 
 
 def build_model(seed, device, T=T_FRAMES, J=J_SRC, K=K_NMF):
@@ -385,9 +405,11 @@ def main(argv=None):
     if world > 1:
         check_clips(clips)
 
-    # per-kernel HIP-event timing on the engine's stream (separate, untimed pass)
+    # per-kernel HIP-event timing in the timed loop's own schedule (separate,
+    # untimed pass): the side stream stays forked, each kernel's events sit
+    # on the stream it runs on, and the host syncs once per 32 iterations
     eng.set_profiling(True)
-    eng.run(psd_schedule(m, 5), m.nmfUpdateCoeff)
+    run_rows(psd_schedule(m, PROF_STEPS))
     times = eng.kernel_times()
     eng.set_profiling(False)
 
@@ -401,12 +423,7 @@ def main(argv=None):
         pmc = None
         # PMC traffic of THIS configuration's own rocprofv3 passes
         # (tools/gpu_prof.sh; BENCH_ARGS="--J 8" -> profiles/r4_bench_J8K32.json)
-        default_cfg = (args.J, args.K, args.T) == (J_SRC, K_NMF, T_FRAMES)
-        pmc_name = "r4_bench.json" if default_cfg else "r4_bench_J%dK%d.json" % (args.J, args.K)
-        if args.T != T_FRAMES:
-            pmc_name = None
-        pmc_path = os.environ.get("FASST_PMC_JSON",
-                                  os.path.join(ROOT, "profiles", pmc_name) if pmc_name else "")
+        pmc_path = os.environ.get("FASST_PMC_JSON") or pmc_file(args.J, args.K, args.T) or ""
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))["kernels"]
@@ -486,6 +503,8 @@ def main(argv=None):
                        "loglik": c[3], "timed_s": round(c[4], 6)} for c in clips],
             "roofline": rl,
             "kernels_ms": {k: round(v[0], 4) for k, v in sorted(times.items())},
+            "kernels_schedule": "in situ: %d iterations, side stream forked, HIP events on each "
+                                "kernel's own stream, one host sync per 32 iterations" % PROF_STEPS,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_T)

@@ -84,6 +84,11 @@ struct fasst_ctx {
   // next iteration of the same fasst_run batch skips launch_w_old
   fasst::DBuf<double> Wkf_next;
   int w_ready = 0;
+  // the fused tail is taken for the structures it covers (fast_tail in
+  // fasst_em.hip) unless FASST_FAST_TAIL=0 was set when this context was created
+  int ftail = 1;
+  // every launch of an iteration on the main stream (FASST_SERIAL_PREP=1: A/B)
+  int serial = 0;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart
@@ -92,10 +97,12 @@ struct fasst_ctx {
   double *h_ll = nullptr;        // pinned host mirror (one value)
   int psd_cap = 0, ll_cap = 0;
   // per-kernel HIP-event timing (fasst_set_profiling / fasst_kernel_times)
-  static constexpr int kNK = 13;
-  int prof = 0;
-  hipEvent_t ev0[kNK] = {}, ev1[kNK] = {};
-  int used[kNK] = {0};
+  // (events on the stream each kernel runs on, the side-stream fork kept, a
+  // ring of kProfRing iterations between host syncs: the timed schedule)
+  static constexpr int kNK = 15, kProfRing = 32;
+  int prof = 0, pslot = 0;
+  hipEvent_t ev0[kNK][kProfRing] = {}, ev1[kNK][kProfRing] = {};
+  int used[kNK][kProfRing] = {{0}};
   double prof_ms[kNK] = {0};
   long prof_cnt[kNK] = {0};
 };

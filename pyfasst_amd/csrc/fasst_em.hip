@@ -2540,34 +2540,37 @@ __global__ __launch_bounds__(256) void k_tb_renorm(const TBRArgs a) {
 
 // ---------------------------------------------------------------- host side
 enum KernelId {
-  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KFWU
+  KW = 0, KFWH, KINSTA, KESTEP, KLL, KMIX, KMIXI, KFBC, KFBU, KTWC, KREN, KTWU, KFWU, KROWS, KRTAIL
 };
 static const char *kKernelNames[fasst_ctx::kNK] = {
     "k_w_from_fb", "k_fwh_t", "k_inst_A", "k_estep", "k_loglik", "k_mix",
     "k_mix_inst", "k_fb_contract", "k_fb_update", "k_tw_contract", "k_renorm", "k_tw_update",
-    "k_fw_update"};
+    "k_fw_update", "k_tw_rowsum", "k_renorm_tail"};
 
-static inline void prof_begin(fasst_ctx *c, int id) {
+// per-kernel timing: an event pair around the launch on the stream it runs on
+// (s = nullptr: the main stream), slot = the iteration's place in the ring
+static inline void prof_begin(fasst_ctx *c, int id, hipStream_t s = nullptr) {
   if (c->prof) {
-    (void)hipEventRecord(c->ev0[id], c->stream);
-    c->used[id] = 1;
+    (void)hipEventRecord(c->ev0[id][c->pslot], s ? s : c->stream);
+    c->used[id][c->pslot] = 1;
   }
 }
-static inline void prof_end(fasst_ctx *c, int id) {
-  if (c->prof) (void)hipEventRecord(c->ev1[id], c->stream);
+static inline void prof_end(fasst_ctx *c, int id, hipStream_t s = nullptr) {
+  if (c->prof) (void)hipEventRecord(c->ev1[id][c->pslot], s ? s : c->stream);
 }
-// after a stream sync: fold the recorded event pairs into the averages
+// after a device sync: fold the recorded event pairs into the averages
 static void prof_collect(fasst_ctx *c) {
   if (!c->prof) return;
-  for (int i = 0; i < fasst_ctx::kNK; ++i) {
-    if (!c->used[i]) continue;
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, c->ev0[i], c->ev1[i]) == hipSuccess) {
-      c->prof_ms[i] += ms;
-      c->prof_cnt[i] += 1;
+  for (int i = 0; i < fasst_ctx::kNK; ++i)
+    for (int q = 0; q < fasst_ctx::kProfRing; ++q) {
+      if (!c->used[i][q]) continue;
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, c->ev0[i][q], c->ev1[i][q]) == hipSuccess) {
+        c->prof_ms[i] += ms;
+        c->prof_cnt[i] += 1;
+      }
+      c->used[i][q] = 0;
     }
-    c->used[i] = 0;
-  }
 }
 
 static int launch_grid(size_t n, int block = 256) {
@@ -2923,11 +2926,7 @@ static int launch_renorm(fasst_ctx *c, int iter) {
 // path without time blobs or free FW.  Off unless FASST_FAST_TAIL=1 until it
 // has passed the GPU parity suite (built and reviewed, not yet run on a GPU)
 static bool fast_tail(const fasst_ctx *c) {
-  static const int on = [] {
-    const char *v = getenv("FASST_FAST_TAIL");
-    return v ? atoi(v) : 0;
-  }();
-  if (!on || c->multi || c->anytb) return false;
+  if (!c->ftail || c->multi || c->anytb) return false;
   for (int j = 0; j < c->J; ++j)
     if (c->fw_free[j]) return false;
   return true;
@@ -2943,19 +2942,19 @@ static int launch_tail_side(fasst_ctx *c, bool fork) {
     FASST_HIP(hipEventRecord(c->ev_tail, c->stream));
     FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_tail, 0));
   }
-  prof_begin(c, KREN);
+  prof_begin(c, KREN, side);
   k_renorm_scales<<<c->J, 256, 0, side>>>(r);
   FASST_LAUNCH_CHECK();
   if (fork) FASST_HIP(hipEventRecord(c->ev_scales, c->aux));
   k_renorm_rows<<<dim3(c->nft, c->J), 256, 0, side>>>(r);
   FASST_LAUNCH_CHECK();
-  prof_end(c, KREN);
+  prof_end(c, KREN, side);
   // the next iteration's W (the TW contraction still reads Wkf)
-  prof_begin(c, KW);
+  prof_begin(c, KW, side);
   (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, c->J), 256,
                 fw_lds(c, 16 * (c->KP + 1)), side>>>(c->FB.p, c->FW.p, c->Wkf_next.p, nullptr,
                                                      c->J, c->Fp, c->KP, c->halt);
-  prof_end(c, KW);
+  prof_end(c, KW, side);
   FASST_LAUNCH_CHECK();
   if (fork) FASST_HIP(hipEventRecord(c->ev_rows, c->aux));
   return FASST_OK;
@@ -3369,7 +3368,7 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
     FASST_HIP(hipEventRecord(c->ev_fork, c->stream));
     FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   }
-  prof_begin(c, KFWH);
+  prof_begin(c, KFWH, side);
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
   if (c->KP > 64)   // FW halves + TW tile: 128 KB of LDS
@@ -3379,9 +3378,11 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
             c->KP > 64 ? (64 + 64) * c->KP * sizeof(double) : fw_lds(c, c->KP * 64),
             side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
                     c->halt);
-  prof_end(c, KFWH);
+  prof_end(c, KFWH, side);
   FASST_LAUNCH_CHECK();
+  prof_begin(c, KROWS, side);
   k_tw_rowsum<<<J * c->KP, 256, 0, side>>>(c->TW.p, c->hsum.p, c->T, c->Tp, c->halt);
+  prof_end(c, KROWS, side);
   FASST_LAUNCH_CHECK();
   if (fork) FASST_HIP(hipEventRecord(c->ev_join, c->aux));
   return FASST_OK;
@@ -3605,9 +3606,9 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
       }
   }
   // (FW.TW)^T and the TW row sums depend only on the previous iteration's
-  // parameters: fork them onto the side stream (kept on the main stream
-  // while per-kernel event timing is on)
-  const bool fork = !c->prof;
+  // parameters: fork them onto the side stream (FASST_SERIAL_PREP=1 keeps
+  // every launch on the main stream: A/B)
+  const bool fork = !c->serial;
   int st = launch_spectral_prep(c, fork);
   if (st) return st;
   const bool w_ready = c->w_ready;   // (the previous iteration's fused tail formed W)
@@ -3712,9 +3713,9 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
   RArgs r = renorm_args(c);
   r.ll_out = ll_dev;
-  prof_begin(c, KLL);
+  prof_begin(c, KRTAIL);
   k_renorm_tail<<<1, 256, 0, c->stream>>>(r, iter);
-  prof_end(c, KLL);
+  prof_end(c, KRTAIL);
   FASST_LAUNCH_CHECK();
   std::swap(c->Wkf.p, c->Wkf_next.p);
   c->w_ready = 1;
@@ -3755,6 +3756,8 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->Tp = round_up(T, kTile);
   c->nft = c->Fp / kTile;
   c->ntt = c->Tp / kTile;
+  if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v) != 0;
+  if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
@@ -3836,8 +3839,10 @@ int fasst_destroy(fasst_ctx *c) {
     c->mplanes.release();
     c->bden.release();
     for (int i = 0; i < fasst_ctx::kNK; ++i) {
-      if (c->ev0[i]) (void)hipEventDestroy(c->ev0[i]);
-      if (c->ev1[i]) (void)hipEventDestroy(c->ev1[i]);
+      for (int q = 0; q < fasst_ctx::kProfRing; ++q) {
+        if (c->ev0[i][q]) (void)hipEventDestroy(c->ev0[i][q]);
+        if (c->ev1[i][q]) (void)hipEventDestroy(c->ev1[i][q]);
+      }
     }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -4200,9 +4205,10 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   // iteration so the per-kernel events can be folded.
   c->halt = c->flags.p + kFlagHalt;
   c->w_ready = 0;
-  const int sync_every = c->prof ? 1 : n_iter;
+  const int sync_every = c->prof ? fasst_ctx::kProfRing : n_iter;
   int done = 0;
   for (int it = 0; it < n_iter; ++it) {
+    c->pslot = it % fasst_ctx::kProfRing;
     st = gem_iteration(c, c->psd.p + (size_t)it * c->Fp, c->ll.p + it, omega, it);
     if (st) {
       c->halt = nullptr;
@@ -4248,16 +4254,18 @@ extern "C" {
 int fasst_set_profiling(fasst_ctx *c, int on) {
   if (!c) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
-  if (on && !c->ev0[0])
-    for (int i = 0; i < fasst_ctx::kNK; ++i) {
-      FASST_HIP(hipEventCreate(&c->ev0[i]));
-      FASST_HIP(hipEventCreate(&c->ev1[i]));
-    }
+  if (on && !c->ev0[0][0])
+    for (int i = 0; i < fasst_ctx::kNK; ++i)
+      for (int q = 0; q < fasst_ctx::kProfRing; ++q) {
+        FASST_HIP(hipEventCreate(&c->ev0[i][q]));
+        FASST_HIP(hipEventCreate(&c->ev1[i][q]));
+      }
   c->prof = on ? 1 : 0;
+  c->pslot = 0;
   for (int i = 0; i < fasst_ctx::kNK; ++i) {
     c->prof_ms[i] = 0.0;
     c->prof_cnt[i] = 0;
-    c->used[i] = 0;
+    for (int q = 0; q < fasst_ctx::kProfRing; ++q) c->used[i][q] = 0;
   }
   return FASST_OK;
 }
