@@ -150,7 +150,8 @@ int fasst_wiener_images(fasst_ctx *ctx, const double *psd, const double *X, doub
 /* Separation sources for fasst_wiener_images / fasst_separate_waveforms
  * (separate_comps' spec_comp_ind, audioModel.py:1130-1164): source n sums the
  * terms [term_off[n], term_off[n + 1]); term i is the spectral components in
- * columns term_mask[i] (bit k = column k, fasst_set_blocks layout) of spatial
+ * columns term_mask[2 i .. 2 i + 1] (a 128-bit column set: bit k of word
+ * k / 64 = column k, fasst_set_blocks layout; K <= 128) of spatial
  * component term_j[i] (compute_sigma_comp_2d, :1327-1372).  Sigma_x is the
  * sum over the sources plus the PSD (compute_inv_sigma_mix_2d, :1374-1394).
  * nsrc = 0 (the default): one source per spatial component, all columns.
@@ -205,7 +206,8 @@ int fasst_inv_herm_mat_2d(int device, int n, const double *diag, const double *o
  *
  * retrieve_subsrc_params (:514-578), the powers half: V out [nj][F][T], the
  * power of spatial components j0 .. j0+nj-1 from the context's parameters
- * (colmask[jj]: the NMF columns to include, bit k; NULL: all).            */
+ * (colmask[2 jj .. 2 jj + 1]: the NMF columns to include, a 128-bit set,
+ * bit k of word k / 64 = column k; NULL: all).                             */
 int fasst_source_powers(fasst_ctx *ctx, int j0, int nj, const unsigned long long *colmask,
                         double *V);
 /* compute_suff_stat (:580-764) on the context's Cx: V [R][F][T] per-rank
@@ -225,8 +227,9 @@ int fasst_mix_solve(int device, int F, int R, const double *rss, const double *r
  * fasst_get_spectral); no renormalisation (fasst_renormalize).            */
 int fasst_spectral_update(fasst_ctx *ctx, const double *hat_W, double omega);
 /* compute_sigma_comp_2d (:1327-1372): spatial component j, NMF columns
- * colmask -> diag [2][F][T], off complex128 [F][T].                        */
-int fasst_sigma_comp(fasst_ctx *ctx, int j, unsigned long long colmask, double *diag,
+ * colmask[0 .. 1] (128-bit set, bit k of word k / 64 = column k) ->
+ * diag [2][F][T], off complex128 [F][T].                                   */
+int fasst_sigma_comp(fasst_ctx *ctx, int j, const unsigned long long *colmask, double *diag,
                      double *off);
 /* compute_inv_sigma_mix_2d (:1374-1394): n components' diag [n][2][F][T],
  * off complex128 [n][F][T], psd [F] -> inverse of their sum + PSD I:

@@ -509,6 +509,18 @@ def make_convolutive(model):
         sc['params'] = p
 
 
+# audioModel.py:2224-2294, initMethod 'rand' (the DEMIX branch is out of scope)
+def init_conv_rand(model, rng=np.random):
+    nc, F, J = model.channels, model.nbFreqsSigRepr, len(model.spat_comps)
+    for j, sc in model.spat_comps.items():
+        sc['mix_type'] = 'conv'
+    A = rng.randn(J, F, nc) + 1j * rng.randn(J, F, nc)
+    for n, (j, sc) in enumerate(model.spat_comps.items()):
+        sc['params'] = np.zeros([model.rank[n], nc, F], dtype=complex)
+        for r in range(model.rank[n]):
+            sc['params'][r] = A[j].T
+
+
 # ----------------------------------------------------------------------------
 # tools/nmf.py:24-61 (IS-NMF multiplicative updates)
 def nmf_decomposition(SX, nbComps=10, niter=10, rng=np.random):

@@ -85,7 +85,8 @@ SIGNATURES = {
     "fasst_mix_solve": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp,
                                        _ip]),
     "fasst_spectral_update": (ctypes.c_int, [_vp, _dp, ctypes.c_double]),
-    "fasst_sigma_comp": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_ulonglong, _dp, _dp]),
+    "fasst_sigma_comp": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong),
+                                        _dp, _dp]),
     "fasst_inv_sigma_mix": (ctypes.c_int, [ctypes.c_int] * 4 + [_dp, _dp, _dp, _dp, _dp]),
     "fasst_wiener_gain": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, _dp, _dp, _dp, _dp, _dp]),
     # include/fasst_simm.h

@@ -658,6 +658,58 @@ class FASST(object):
             V += Vc
         return V
 
+    def comp_spat_cmps_powers(self, spat_comp_ind, spec_comp_ind=[], factor_ind=[]):
+        """Sum of the spectral powers of the spatial components listed in
+        spat_comp_ind (audioModel.py:500-512; spec_comp_ind / factor_ind are
+        accepted and unused, as there).  Each component's power comes from
+        the device (fasst_source_powers on the uploaded parameters) and the
+        sum runs on the host in the list's order."""
+        self._upload()
+        V = 0
+        for i in spat_comp_ind:
+            V += self._engine.source_powers(int(i), 1)[0]
+        return V
+
+    def setComponentParameter(self, newValue, spec_ind, fact_ind=0, partLabel='FB',
+                              prior='free', keepDimensions=True):
+        """The reference's unfinished helper (audioModel.py:2042-2089): it
+        prints its notice, then its first statement reads the misspelt name
+        `keepDimenstions` and raises NameError before touching anything.
+        Kept as that behaviour so the class surface is the same; set the
+        components directly (spec_comps[k]['factor'][f][...]), as its notice
+        says."""
+        print("NOT IMPLEMENTED YET, PLEASE SET THE COMPONENTS DIRECTLY")
+        raise NameError("name 'keepDimenstions' is not defined")
+
+    def initializeConvParams(self, initMethod='demix'):
+        """Convolutive spatial parameters (audioModel.py:2224-2294): every
+        spatial component becomes 'conv'; 'rand' draws the steering vectors
+        A = randn(J, F, nc) + 1j randn(J, F, nc) from the global np.random
+        stream (the reference's draw order) and gives every rank of
+        component j the parameters A[j].T.  'demix' needs the DEMIX
+        estimator (pyfasst.demixTF), which is outside this engine's scope
+        (DESIGN.md §7): NotImplementedError."""
+        nc = self.audioObject.channels
+        for spat_ind, spat_comp in self.spat_comps.items():
+            if spat_comp['mix_type'] != 'inst':
+                warnings.warn("Spatial component %d " % spat_ind +
+                              "already not instantaneous, overwriting...")
+            spat_comp['mix_type'] = 'conv'
+        if initMethod == 'demix':
+            raise NotImplementedError("initializeConvParams('demix'): the DEMIX estimator "
+                                      "(demixTF) is outside the HIP engine's scope; use 'rand'")
+        elif 'rand' in initMethod:
+            J = len(self.spat_comps)
+            A = (np.random.randn(J, self.nbFreqsSigRepr, nc) +
+                 1j * np.random.randn(J, self.nbFreqsSigRepr, nc))
+        else:
+            raise ValueError("Init method not implemented.")
+        for nspat, (spat_ind, spat_comp) in enumerate(self.spat_comps.items()):
+            spat_comp['params'] = np.zeros([self.rank[nspat], nc, self.nbFreqsSigRepr],
+                                           dtype=complex)
+            for r in range(self.rank[nspat]):
+                spat_comp['params'][r] = A[spat_ind].T
+
 
 class MultiChanNMFInst_FASST(FASST):
     """Multichannel NMF, instantaneous mixing (audioModel.py:2296-2420)."""

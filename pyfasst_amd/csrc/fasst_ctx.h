@@ -67,7 +67,7 @@ struct fasst_ctx {
   // component): source n sums the terms [toff[n], toff[n + 1]), term i = the
   // columns tmask[i] (bit k = column k) of spatial component tj[i]
   int nsrc = 0, toff[fasst::kMaxSlot + 1] = {0}, tj[fasst::kMaxSlot] = {0};
-  unsigned long long tmask[fasst::kMaxSlot] = {0};
+  unsigned long long tmask[fasst::kMaxSlot][2] = {{0}};   // 128-bit column sets
   fasst::DBuf<double2> A, Pinst;
   // work space
   int nchunk_e = 1, tpc_e = 1, nchunk_b = 1, tpc_b = 1, nacc = 0;
@@ -89,6 +89,9 @@ struct fasst_ctx {
   int ftail = 1;
   // every launch of an iteration on the main stream (FASST_SERIAL_PREP=1: A/B)
   int serial = 0;
+  // TW contraction form: 0 = k_tw_contract (W operands from L2 per lane),
+  // 1 = k_tw_contract_lds (FASST_TWL, read at creation)
+  int twl = 1;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart

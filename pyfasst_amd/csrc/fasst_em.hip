@@ -1768,6 +1768,230 @@ __global__ __launch_bounds__(64) void k_tw_contract(const TArgs a) {
   }
 }
 
+// k_tw_contract's plain form (one spectral component per source, no
+// lambdaCorr / time blobs, KP <= 64) with its per-bin-step operands staged in
+// LDS by LDS-DMA (raw-buffer loads ... lds: no VGPR cost, NS stages in
+// flight): a block of NW waves shares one source and bin chunk, wave w owns
+// TPW frame tiles.  Stage c (bin tile fb + c) holds
+//   Wo [KP][16]  W_old rows      (Wkf_old: KP / 8 pieces of 8 rows x 128 B;
+//                not with SO)
+//   Wn [KP][16]  W_new rows      (Wkf_new)
+//   Wf [16][KP]  W_new, [f][k]   (Wfk_new, 16 KP contiguous doubles; a row r
+//                with bit 2 set has its 128-B halves swapped, so the rows 4
+//                apart that one ds_read_b64 lane group reads hit disjoint
+//                bank halves; the DMA source applies the same involution)
+//   rho [NW][TPW][8 granules][16 frames] x 16 B: the wave's own rho tiles,
+//                granule-major so a lane's four consecutive bins are two
+//                conflict-free ds_read_b128
+// One s_barrier per bin step: wait (counted vmcnt) for the wave's own stage c
+// pieces -> barrier -> issue stage c + NS - 1 into the buffer stage c - 1
+// left -> compute stage c.  The arithmetic is k_tw_contract's, term for term.
+template <int NKC, int NW, int TPW, int NS>
+struct TwlCfg {
+  static constexpr int NKC_ = NKC, NW_ = NW, TPW_ = TPW, NS_ = NS, NT = 64 * NW;
+  static constexpr int KP = 16 * NKC;
+  static constexpr int NWO = KP / 8;                // W pieces: Wo, Wn, Wf
+  static constexpr int WPI = 3 * NWO;               // 1 KB W pieces per stage
+  static constexpr int WD = 128 * WPI;              // W doubles per stage
+  static constexpr int WN0 = 16 * KP, WF0 = 32 * KP;   // Wn / Wf offsets
+  static constexpr int RD = 256;                    // rho doubles per frame tile
+  static constexpr int SS = WD + NW * TPW * RD;     // doubles per stage
+  static constexpr size_t smem = (size_t)NS * SS * sizeof(double);
+  static constexpr int WPW = (WPI + NW - 1) / NW;   // W pieces per wave (upper bound)
+  static constexpr int LPC = WPI / NW + 2 * TPW;    // loads per wave per stage (lower bound)
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// (the body is a device function: the host pass of a kernel template
+// analyses its body, and the AMDGPU buffer-resource builtins do not exist there)
+template <class CF>
+__device__ __forceinline__ void tw_contract_lds_body(const TArgs &a);
+template <class CF>
+__global__ __launch_bounds__(CF::NT) FASST_NO_LDS_PAIRING
+void k_tw_contract_lds(const TArgs a) {
+  tw_contract_lds_body<CF>(a);
+}
+template <class CF>
+__device__ __forceinline__ void tw_contract_lds_body(const TArgs &a) {
+  HALT_GUARD(a.halt);
+  constexpr int NKC = CF::NKC_, NW = CF::NW_, TPW = CF::TPW_, NS = CF::NS_;
+  constexpr int KP = CF::KP, NKS = 4 * NKC, SS = CF::SS, WPI = CF::WPI, NWO = CF::NWO;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  // (wv through readfirstlane: the compiler then knows it is wave-uniform, so
+  // the piece / tile branches below are scalar, not exec-masked waterfalls)
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fl = lane & 15, tq = lane >> 4;
+  const dim3 bi = xcd_block();   // x: frame-tile group, y: source, z: bin chunk
+  const int j = bi.y;
+  if (!a.tw_free[j]) return;
+  const int tt0 = (bi.x * NW + wv) * TPW;   // this wave's first frame tile
+  const int fb = bi.z * a.fpc, fe = min(fb + a.fpc, a.nft), nst = fe - fb;
+  // TW operands of the V tiles (resident for the whole bin loop)
+  double bt[TPW][NKS];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    const bool tin = tt0 + p < a.ntt;
+    const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + (tt0 + p) * 16 + fl;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) bt[p][s] = tin ? tw[(size_t)(4 * s) * a.Tp] : 0.0;
+  }
+  // (retire them before the first DMA: a use of an ordinary load while LDS-DMA
+  // is in flight would drain the DMA ring)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // buffer resources: W rows of source j, its rho plane
+  const unsigned wbytes = (unsigned)((size_t)KP * a.Fp * sizeof(double));
+  const unsigned pbytes = (unsigned)((size_t)a.Tp * a.Fp * sizeof(double));
+  const __amdgpu_buffer_rsrc_t rWo = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.Wkf_old + (size_t)j * KP * a.Fp), 0, wbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rWn = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.Wkf_new + (size_t)j * KP * a.Fp), 0, wbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rWf = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.Wfk_new + (size_t)j * a.Fp * KP), 0, wbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(a.hatW + (size_t)j * a.Tp * a.Fp), 0, pbytes, 0x00020000);
+  // per-lane byte offsets of this wave's pieces (loop-invariant; the bin
+  // step's offset rides in the SGPR soffset)
+  constexpr int WPW = CF::WPW;
+  static_assert(WPW <= 8, "W pieces per wave");
+  unsigned wvo[8];
+#pragma unroll
+  for (int r = 0; r < WPW; ++r) {
+    const int p = wv + NW * r;
+    unsigned o = 0;
+    if (p < NWO + KP / 8) {          // Wo / Wn: row 8 p' + lane / 8, granule lane % 8
+      const int pp = p < NWO ? p : p - NWO, k = 8 * pp + (lane >> 3);
+      o = (unsigned)(((size_t)k * a.Fp + 2 * (lane & 7)) * sizeof(double));
+    } else if (p < WPI) {            // Wf: LDS position P -> element P ^ swz
+      const int P = (p - NWO - KP / 8) * 128 + 2 * lane;
+      const int e = P ^ ((((P / KP) >> 2) & 1) << 4);
+      o = (unsigned)(e * sizeof(double));
+    }
+    wvo[r] = o;
+  }
+  unsigned rvo[TPW][2];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    // frame tiles past the last one re-read the last (never used)
+    const int tt = min(tt0 + p, a.ntt - 1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int g = 4 * q + (lane >> 4);
+      rvo[p][q] = (unsigned)(((size_t)(tt * 16 + fl) * a.Fp + 2 * g) * sizeof(double));
+    }
+  }
+  auto issue = [&](int c) {   // stage c (bin tile fb + c) into buffer c % NS
+    double *st = smem + (c % NS) * SS;
+    const int f0 = (fb + c) * 16;
+#pragma unroll
+    for (int r = 0; r < WPW; ++r) {
+      const int p = wv + NW * r;
+      // (wave-uniform branches: one resource per call, never a runtime
+      // select of a 128-bit resource)
+      lds_void_t *d = (lds_void_t *)(st + 128 * p);
+      if (p < NWO)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rWo, d, 16, wvo[r], f0 * 8, 0, 0);
+      else if (p < NWO + KP / 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rWn, d, 16, wvo[r], f0 * 8, 0, 0);
+      else if (p < WPI)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rWf, d, 16, wvo[r], f0 * KP * 8, 0, 0);
+    }
+    double *sr = st + CF::WD + wv * TPW * CF::RD;
+#pragma unroll
+    for (int p = 0; p < TPW; ++p)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (lds_void_t *)(sr + p * CF::RD + 128 * q), 16,
+                                                 rvo[p][q], f0 * 8, 0, 0);
+  };
+  d4 num[TPW][NKC], den[TPW][NKC];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p)
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) num[p][kc] = den[p][kc] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < NS - 1; ++c)
+    if (c < nst) issue(c);
+  // lane's LDS read offsets (doubles) inside a stage
+  const int fpl = 4 * (fl & 3) + (fl >> 2);   // V-tile bin row permutation (k_tw_contract)
+  const int ow = tq * 16 + fpl;   // Wo / Wn: row tq + 4 s at + 64 s
+  // Wf element (4 tq + i, 16 kc + fl) sits at (4 tq + i) KP + 16 kc + fl
+  // with bit 4 flipped for odd tq: + 16 where the flipped bit was 0 (even kc,
+  // or even i at KP = 16, where bit 4 is the row's low bit), - 16 otherwise
+  const int s1 = (tq & 1) << 4;
+  const int ofp = CF::WF0 + 4 * tq * KP + fl + s1, ofm = ofp - 2 * s1;
+  const int orr = CF::WD + wv * TPW * CF::RD + (2 * tq * 16 + fl) * 2;   // granules 2 tq, 2 tq + 1
+  const int bq = 4 * tq;
+  for (int c = 0; c < nst; ++c) {
+    // this wave's stage c pieces have landed (younger stages may still fly)
+    const int ahead = min(NS - 2, nst - 1 - c);
+    if (NS >= 3 && ahead >= 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CF::LPC < 63 ? CF::LPC : 63) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave's stage c is in; stage c - 1 is read
+    if (c + NS - 1 < nst) issue(c + NS - 1);
+    const double *st = smem + (c % NS) * SS;
+    const int f0 = (fb + c) * 16;
+#pragma unroll
+    for (int p = 0; p < TPW; ++p) {
+      if (tt0 + p >= a.ntt) break;  // wave-uniform: no frame tile left
+      const int t = (tt0 + p) * 16 + fl;
+      typedef double dv2 __attribute__((ext_vector_type(2)));
+      const dv2 h01 = *(const dv2 *)(st + orr + p * CF::RD);
+      const dv2 h23 = *(const dv2 *)(st + orr + p * CF::RD + 32);
+      const double h[4] = {h01.x, h01.y, h23.x, h23.y};
+      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
+#pragma unroll
+      for (int s = 0; s < NKS; s += 2) {
+        const double ao0 = st[ow + 64 * s], ao1 = st[ow + 64 * (s + 1)];
+        vo = mfma4(ao0, bt[p][s], vo);
+        vo2 = mfma4(ao1, bt[p][s + 1], vo2);
+        const double an0 = st[CF::WN0 + ow + 64 * s], an1 = st[CF::WN0 + ow + 64 * (s + 1)];
+        vn = mfma4(an0, bt[p][s], vn);
+        vn2 = mfma4(an1, bt[p][s + 1], vn2);
+      }
+      vo += vo2;
+      vn += vn2;
+      const bool tok = t < a.T;
+      double r3[4], r4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double vm = fmax(vn[i], kEps);
+        const double rv = rcp_nr(vm);
+        const bool ok = tok && f0 + bq + i < a.F;
+        const double other = fmax(vo[i], kEps);
+        const double q = (h[i] * other) * (rv * rv);   // hat_W from the E-step's rho
+        r3[i] = ok ? other * q : 0.0;
+        r4[i] = ok ? other * rv : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kc = 0; kc < NKC; ++kc) {
+          const bool ev = ((KP == 16 ? i : kc) & 1) == 0;
+          const double bw = st[(ev ? ofp : ofm) + i * KP + kc * 16];
+          num[p][kc] = mfma4(r3[i], bw, num[p][kc]);
+          den[p][kc] = mfma4(r4[i], bw, den[p][kc]);
+        }
+    }
+  }
+  const size_t base = ((size_t)bi.z * a.J + j) * a.Tp;
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) {
+    if (tt0 + p >= a.ntt) break;
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const size_t o = (base + (tt0 + p) * 16 + tq + 4 * m) * a.KP + kc * 16 + fl;
+        a.tnum[o] = num[p][kc][m];
+        a.tden[o] = den[p][kc][m];
+      }
+  }
+}
+
 struct TUArgs {
   double *TW;
   const double *tnum, *tden;
@@ -2581,6 +2805,7 @@ static int launch_grid(size_t n, int block = 256) {
 
 static int estep_occupancy(const fasst_ctx *c);
 static int contract_occupancy(const fasst_ctx *c, bool fb);
+static int twl_occupancy(const fasst_ctx *c, int *units);
 static int tpw_of(const fasst_ctx *c);
 // dynamic LDS of the kernels that stage FW ([KP][KP] when KP <= 64) next to
 // `rest` doubles
@@ -2691,13 +2916,21 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   if (const char *v = getenv("FASST_NCHUNK_B")) c->nchunk_b = std::max(1, std::min(atoi(v), c->ntt));
   c->tpc_b = (c->ntt + c->nchunk_b - 1) / c->nchunk_b;
   c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
-  const long cap_t = (long)contract_occupancy(c, false) * ncu;
+  long cap_t = (long)contract_occupancy(c, false) * ncu;
   // (the bin split also multiplies k_tw_update's reduction: a fixed, small
   // split measured best at C3)
   c->nsplit_t = std::max(1, std::min(4, c->nft / 32));
-  const int tpw = tpw_of(c);
-  if ((long)((c->ntt + tpw - 1) / tpw) * J * c->nsplit_t < cap_t)
-    c->nsplit_t = best_split((long)((c->ntt + tpw - 1) / tpw) * J, cap_t, c->nft / 16);
+  int tw_units = (c->ntt + tpw_of(c) - 1) / tpw_of(c);
+  {
+    int u = 0;
+    const int occ = twl_occupancy(c, &u);
+    if (occ) {
+      cap_t = (long)occ * ncu;
+      tw_units = u;
+    }
+  }
+  if ((long)tw_units * J * c->nsplit_t < cap_t)
+    c->nsplit_t = best_split((long)tw_units * J, cap_t, c->nft / 16);
   if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
   c->fpc_t = (c->nft + c->nsplit_t - 1) / c->nsplit_t;
   c->nsplit_t = (c->nft + c->fpc_t - 1) / c->fpc_t;
@@ -3039,6 +3272,40 @@ template <int NKC>
 constexpr int tpw_for() { return NKC > 4 ? 1 : kTPW; }
 static int tpw_of(const fasst_ctx *c) { return c->KP > 64 ? 1 : kTPW; }
 
+// k_tw_contract_lds shapes (NW waves per block, TPW frame tiles per wave, NS
+// stages); c->twl picks one (0: the register-operand k_tw_contract)
+template <class CF>
+static void launch_twl_cfg(fasst_ctx *c, const TArgs &t) {
+  const int g = (c->ntt + CF::NW_ * CF::TPW_ - 1) / (CF::NW_ * CF::TPW_);
+  k_tw_contract_lds<CF><<<dim3(g, c->J, c->nsplit_t), CF::NT, CF::smem, c->stream>>>(t);
+}
+template <class CF>
+static int twl_occ_cfg(const fasst_ctx *c, int *units) {
+  (void)hipFuncSetAttribute((const void *)k_tw_contract_lds<CF>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)CF::smem);
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract_lds<CF>, CF::NT, CF::smem) !=
+      hipSuccess)
+    n = 1;
+  *units = (c->ntt + CF::NW_ * CF::TPW_ - 1) / (CF::NW_ * CF::TPW_);
+  return std::max(1, n);
+}
+// launch (units == nullptr) or occupancy query of shape c->twl at NKC
+template <int NKC>
+static int twl_switch(fasst_ctx *c, const TArgs *t, int *units) {
+  switch (c->twl) {
+#define TWL_CASE(id, NW, TPW, NS)                                  \
+  case id:                                                         \
+    if (!units) launch_twl_cfg<TwlCfg<NKC, NW, TPW, NS>>(c, *t);   \
+    return units ? twl_occ_cfg<TwlCfg<NKC, NW, TPW, NS>>(c, units) : 1;
+    // (C3 same-box A/B, k_tw_contract 0.395 ms: NW x TPW x NS = 8 x 1 x 2
+    // 0.378, 4 x 2 x 2 0.379, 4 x 1 x 3 0.396, 4 x 2 x 3 0.437 ms)
+    TWL_CASE(1, 8, 1, 2)
+#undef TWL_CASE
+    default: return 0;
+  }
+}
+
 template <int NKC>
 static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb, int nz = 0) {
   if (fb) {
@@ -3046,12 +3313,27 @@ static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool f
     k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, nz ? nz : c->nchunk_b), 64,
                                0, c->stream>>>(b);
     prof_end(c, KFBC);
+  } else if (NKC <= 4 && c->twl) {
+    prof_begin(c, KTWC);
+    twl_switch<NKC <= 4 ? NKC : 4>(c, &t, nullptr);
+    prof_end(c, KTWC);
   } else {
     prof_begin(c, KTWC);
     constexpr int TPW = tpw_for<NKC>();
     k_tw_contract<NKC, TPW><<<dim3((c->ntt + TPW - 1) / TPW, c->J, c->nsplit_t), 64, 0,
                               c->stream>>>(t);
     prof_end(c, KTWC);
+  }
+}
+
+// resident k_tw_contract_lds blocks per CU (0: c->twl off or KP > 64)
+static int twl_occupancy(const fasst_ctx *c, int *units) {
+  if (!c->twl || c->KP > 64) return 0;
+  fasst_ctx *cc = const_cast<fasst_ctx *>(c);
+  switch (c->KP) {
+    case 16: return twl_switch<1>(cc, nullptr, units);
+    case 32: return twl_switch<2>(cc, nullptr, units);
+    default: return twl_switch<4>(cc, nullptr, units);
   }
 }
 
@@ -3758,6 +4040,7 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->ntt = c->Tp / kTile;
   if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v) != 0;
   if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
+  if (const char *v = getenv("FASST_TWL")) c->twl = atoi(v);
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||

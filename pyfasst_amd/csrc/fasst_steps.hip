@@ -29,15 +29,19 @@ __device__ __forceinline__ double2 c_mul(double2 a, double2 b) {
 __device__ __forceinline__ double2 c_conj(double2 a) { return make_double2(a.x, -a.y); }
 
 // V[j][f][t] = sum_k W[j][k][f] H[j][k][t] (W = FB.FW in Wkf, H in TW's rows;
-// colmask: the columns of spectral components to include, bit k)
+// (m0, m1): the columns of spectral components to include, bit k of word
+// k / 64 -- KP reaches 128)
+__device__ __forceinline__ bool col_in(unsigned long long m0, unsigned long long m1, int k) {
+  return ((k < 64 ? m0 >> k : m1 >> (k - 64)) & 1ull) != 0;
+}
 __global__ void k_source_powers(const double *__restrict__ Wkf, const double *__restrict__ TW,
                                 double *__restrict__ V, int F, int T, int Fp, int Tp, int KP,
-                                int j0, unsigned long long colmask) {
+                                int j0, unsigned long long m0, unsigned long long m1) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x, f = blockIdx.y, jj = blockIdx.z, j = j0 + jj;
   if (t >= T) return;
   double s = 0.0;
   for (int k = 0; k < KP; ++k)
-    if (colmask >> k & 1ull) s += Wkf[((size_t)j * KP + k) * Fp + f] * TW[((size_t)j * KP + k) * Tp + t];
+    if (col_in(m0, m1, k)) s += Wkf[((size_t)j * KP + k) * Fp + f] * TW[((size_t)j * KP + k) * Tp + t];
   V[((size_t)jj * F + f) * T + t] = s;
 }
 
@@ -425,12 +429,12 @@ __global__ void k_mix_solve_conv(const double2 *__restrict__ rss, const double2 
 __global__ void k_sigma_comp(const double *__restrict__ Wkf, const double *__restrict__ TW,
                              const double2 *__restrict__ A, double *__restrict__ diag,
                              double2 *__restrict__ off, int F, int T, int Fp, int Tp, int KP, int j,
-                             int r0, int r1, unsigned long long colmask) {
+                             int r0, int r1, unsigned long long m0, unsigned long long m1) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x, f = blockIdx.y;
   if (t >= T) return;
   double v = 0.0;
   for (int k = 0; k < KP; ++k)
-    if (colmask >> k & 1ull) v += Wkf[((size_t)j * KP + k) * Fp + f] * TW[((size_t)j * KP + k) * Tp + t];
+    if (col_in(m0, m1, k)) v += Wkf[((size_t)j * KP + k) * Fp + f] * TW[((size_t)j * KP + k) * Tp + t];
   double c0 = 0.0, c1 = 0.0;
   double2 co = make_double2(0.0, 0.0);
   for (int r = r0; r < r1; ++r) {
@@ -505,9 +509,10 @@ int fasst_source_powers(fasst_ctx *c, int j0, int nj, const unsigned long long *
   DBuf<double> dV;
   if ((st = dV.alloc_uninit((size_t)c->F * c->T))) return st;
   for (int jj = 0; jj < nj; ++jj) {
-    const unsigned long long m = colmask ? colmask[jj] : ~0ull;
+    const unsigned long long m0 = colmask ? colmask[2 * jj] : ~0ull;
+    const unsigned long long m1 = colmask ? colmask[2 * jj + 1] : ~0ull;
     k_source_powers<<<dim3((c->T + 255) / 256, c->F, 1), 256, 0, c->stream>>>(
-        c->Wkf.p, c->TW.p, dV.p, c->F, c->T, c->Fp, c->Tp, c->KP, j0 + jj, m);
+        c->Wkf.p, c->TW.p, dV.p, c->F, c->T, c->Fp, c->Tp, c->KP, j0 + jj, m0, m1);
     FASST_LAUNCH_CHECK();
     FASST_HIP(hipMemcpyAsync(V + (size_t)jj * c->F * c->T, dV.p, (size_t)c->F * c->T * sizeof(double),
                              hipMemcpyDeviceToHost, c->stream));
@@ -610,8 +615,9 @@ int fasst_mix_solve(int device, int F, int R, const double *rss, const double *r
   return FASST_OK;
 }
 
-int fasst_sigma_comp(fasst_ctx *c, int j, unsigned long long colmask, double *diag, double *off) {
-  if (!c || !c->configured || j < 0 || j >= c->J || !diag || !off) return FASST_ERR_SHAPE;
+int fasst_sigma_comp(fasst_ctx *c, int j, const unsigned long long *colmask, double *diag,
+                     double *off) {
+  if (!c || !c->configured || j < 0 || j >= c->J || !colmask || !diag || !off) return FASST_ERR_SHAPE;
   DeviceGuard g(c->device);
   int st;
   if ((st = launch_w_old(c)) || (st = build_inst_A(c))) return st;
@@ -621,7 +627,7 @@ int fasst_sigma_comp(fasst_ctx *c, int j, unsigned long long colmask, double *di
   if ((st = dd.alloc_uninit(2 * FT)) || (st = doff.alloc_uninit(FT))) return st;
   k_sigma_comp<<<dim3((c->T + 255) / 256, c->F), 256, 0, c->stream>>>(
       c->Wkf.p, c->TW.p, c->A.p, dd.p, doff.p, c->F, c->T, c->Fp, c->Tp, c->KP, j, c->roff[j],
-      c->roff[j + 1], colmask);
+      c->roff[j + 1], colmask[0], colmask[1]);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipMemcpyAsync(diag, dd.p, 2 * FT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   FASST_HIP(hipMemcpyAsync(off, doff.p, FT * sizeof(double2), hipMemcpyDeviceToHost, c->stream));

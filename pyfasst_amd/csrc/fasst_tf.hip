@@ -365,18 +365,18 @@ struct WSArgs {
   double2 *S;   // [nsrc][2][Tp][Fp]
   int F, T, Fp, Tp, KP, nsrc;
   int toff[kMaxSlot + 1], tj[kMaxSlot];
-  unsigned long long tmask[kMaxSlot];
+  unsigned long long tmask[kMaxSlot][2];   // 128-bit column sets (KP <= 128)
 };
 
 __device__ __forceinline__ d4 ws_term_v(const WSArgs &a, int i, int t0, int f, int tq, int fl) {
   const int j = a.tj[i];
-  const unsigned long long m = a.tmask[i];
+  const unsigned long long m0 = a.tmask[i][0], m1 = a.tmask[i][1];
   const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
   const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
   d4 v = d4{0.0, 0.0, 0.0, 0.0};
   for (int s = 0; s < (a.KP >> 2); ++s) {
     const int k = tq + 4 * s;
-    const double w = (m >> k) & 1ull ? wk[(size_t)(4 * s) * a.Fp] : 0.0;
+    const double w = ((k < 64 ? m0 >> k : m1 >> (k - 64)) & 1ull) ? wk[(size_t)(4 * s) * a.Fp] : 0.0;
     v = mfma4b(tw[(size_t)(4 * s) * a.Tp], w, v);
   }
   return v;
@@ -483,7 +483,8 @@ static int launch_wiener(fasst_ctx *c, const double *coef, const double *dpsd, d
     for (int i = 0; i <= kMaxSlot; ++i) w.toff[i] = i <= c->nsrc ? c->toff[i] : c->toff[c->nsrc];
     for (int i = 0; i < kMaxSlot; ++i) {
       w.tj[i] = c->tj[i];
-      w.tmask[i] = c->tmask[i];
+      w.tmask[i][0] = c->tmask[i][0];
+      w.tmask[i][1] = c->tmask[i][1];
     }
     k_wiener_src<<<grid, 64, 0, c->stream>>>(w);
     FASST_LAUNCH_CHECK();
@@ -806,8 +807,12 @@ int fasst_set_sources(fasst_ctx *c, int nsrc, const int *term_off, const int *te
     }
   for (int i = 0; i < term_off[nsrc]; ++i) {
     const int j = term_j[i];
-    if (j < 0 || j >= c->J || !term_mask[i] ||
-        (c->K[j] < 64 && (term_mask[i] >> c->K[j]) != 0ull)) {
+    const unsigned long long m0 = term_mask[2 * i], m1 = term_mask[2 * i + 1];
+    const int K = j >= 0 && j < c->J ? c->K[j] : 0;
+    // a non-empty set of the component's own columns 0 .. K - 1
+    const bool past = K < 64 ? ((m0 >> K) != 0ull || m1 != 0ull)
+                             : (K < 128 && (m1 >> (K - 64)) != 0ull);
+    if (j < 0 || j >= c->J || !(m0 | m1) || past) {
       set_error("fasst_set_sources: bad term %d (spatial component %d)", i, j);
       return FASST_ERR_SHAPE;
     }
@@ -816,7 +821,8 @@ int fasst_set_sources(fasst_ctx *c, int nsrc, const int *term_off, const int *te
   for (int n = 0; n <= nsrc; ++n) c->toff[n] = term_off[n];
   for (int i = 0; i < term_off[nsrc]; ++i) {
     c->tj[i] = term_j[i];
-    c->tmask[i] = term_mask[i];
+    c->tmask[i][0] = term_mask[2 * i];
+    c->tmask[i][1] = term_mask[2 * i + 1];
   }
   return FASST_OK;
 }

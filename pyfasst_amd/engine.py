@@ -27,6 +27,19 @@ def wiener_gain(device, sdiag, soff, idiag, ioff):
     return WG
 
 
+def colmask_words(masks):
+    """Column sets (Python ints, bit k = NMF column k, K <= 128) as the C
+    ABI's 128-bit form: uint64 [n][2] = (columns 0..63, columns 64..127)."""
+    out = np.zeros((len(masks), 2), dtype=np.uint64)
+    for i, m in enumerate(masks):
+        m = int(m)
+        if m < 0 or m >> 128:
+            raise ValueError("column set beyond the HIP path's 128 NMF columns")
+        out[i, 0] = m & 0xFFFFFFFFFFFFFFFF
+        out[i, 1] = m >> 64
+    return out
+
+
 class Engine(object):
     """Device state of one FASST model: observation (Cx, STFT) + parameters."""
 
@@ -199,7 +212,7 @@ class Engine(object):
             return
         off = np.cumsum([0] + [len(t) for t in sources]).astype(np.int32)
         tj = np.array([j for t in sources for j, _ in t] or [0], dtype=np.int32)
-        tm = np.array([m for t in sources for _, m in t] or [0], dtype=np.uint64)
+        tm = colmask_words([m for t in sources for _, m in t] or [0])
         check(lib.fasst_set_sources(self._h, len(sources), iptr(off), iptr(tj),
                                     tm.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))),
               "fasst_set_sources")
@@ -227,7 +240,7 @@ class Engine(object):
         out = np.empty((nj, self.F, self.T))
         mp = None
         if colmasks is not None:
-            m = np.ascontiguousarray(colmasks, dtype=np.uint64)
+            m = colmask_words(colmasks)
             mp = m.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))
         check(lib.fasst_source_powers(self._h, int(j0), int(nj), mp, dptr(out)),
               "fasst_source_powers")
@@ -275,7 +288,9 @@ class Engine(object):
     def sigma_comp(self, j, colmask):
         diag = np.empty((2, self.F, self.T))
         off = np.empty((self.F, self.T), dtype=np.complex128)
-        check(lib.fasst_sigma_comp(self._h, int(j), int(colmask), dptr(diag), dptr(off)),
+        m = colmask_words([colmask])
+        check(lib.fasst_sigma_comp(self._h, int(j), m.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)),
+                                   dptr(diag), dptr(off)),
               "compute_sigma_comp_2d")
         return diag, off
 

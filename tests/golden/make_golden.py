@@ -508,6 +508,39 @@ def run_nmfinit(same):
     print(name, out['logliks'])
 
 
+def run_convinit():
+    """initializeConvParams(initMethod='rand') (audioModel.py:2224-2294) on a
+    seeded model: the random steering vectors' RNG order, the 'conv'
+    parameters they fill, then 3 GEM iterations from that state."""
+    import warnings
+    warnings.simplefilter('ignore')
+    sys.path.insert(0, SCRATCH)
+    import numpy as np
+    import scipy.io.wavfile as wf
+    import pyfasst.audioModel as am
+    name = "convinit_rand"
+    data = synth_wav(4000, 8000, 79)
+    wav = "/tmp/golden_%s.wav" % name
+    wf.write(wav, 8000, data)
+    np.random.seed(0)
+    m = am.MultiChanNMFConv(wav, nbComps=3, nbNMFComps=4, spatial_rank=[1, 2, 1], verbose=0,
+                            iter_num=3, wlen=256, hopsize=64)
+    out = {'wav': data, 'fs': np.array(8000)}
+    np.random.seed(9)
+    m.initializeConvParams(initMethod='rand')
+    for j, sc in m.spat_comps.items():
+        out['init_params_%d' % j] = np.array(sc['params'])
+        out['mix_type_%d' % j] = np.array(sc['mix_type'])
+    out['logliks'] = np.real(m.estim_param_a_post_model())
+    for j, sc in m.spat_comps.items():
+        out['final_params_%d' % j] = np.array(sc['params'])
+    for k, comp in m.spec_comps.items():
+        out['final_FB_%d' % k] = np.array(comp['factor'][0]['FB'])
+        out['final_TW_%d' % k] = np.array(comp['factor'][0]['TW'])
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, out['logliks'])
+
+
 def run_pipeline():
     """The full lead/accompaniment pipeline SeparateLeadProcess(...)
     .autoMelSepAndWrite(maxFrames) (SeparateLeadStereoTF.py:263-540,
@@ -758,7 +791,8 @@ if __name__ == "__main__":
         name = sys.argv[2]
         {"stft": run_stft, "nmf": run_nmf, "inv_herm": run_inv_herm, "simm": run_simm,
          "lead": run_lead, "cqt": run_cqt, "viterbi": run_viterbi, "wf0": run_wf0, "nmfinit_same": lambda: run_nmfinit(True),
-         "nmfinit_indiv": lambda: run_nmfinit(False), "pipeline": run_pipeline,
+         "nmfinit_indiv": lambda: run_nmfinit(False), "convinit_rand": run_convinit,
+         "pipeline": run_pipeline,
          "wf0_cqt": run_wf0_cqt, "pipeline_mqt": run_pipeline_mqt,
          "pipeline_nnls": run_pipeline_nnls, "pipeline_suimm": run_pipeline_suimm}.get(
             name, lambda: run_case(name))()
@@ -767,7 +801,7 @@ if __name__ == "__main__":
     if not os.path.isdir(os.path.join(SCRATCH, "pyfasst")):
         make_scratch_ref.build(SCRATCH)
     names = sys.argv[1:] or (["inv_herm", "stft", "nmf", "simm", "lead", "cqt", "viterbi", "wf0", "nmfinit_same",
-                              "nmfinit_indiv", "pipeline", "wf0_cqt", "pipeline_mqt",
+                              "nmfinit_indiv", "convinit_rand", "pipeline", "wf0_cqt", "pipeline_mqt",
                               "pipeline_nnls", "pipeline_suimm"] + list(CASES))
     for name in names:
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", name])

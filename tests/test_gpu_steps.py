@@ -176,3 +176,24 @@ def test_step_methods_leave_fused_state_usable():
     assert rel(np.array(lls), np.array(llo)) < 1e-10
     for j in range(2):
         assert rel(m.spec_comps[j]['factor'][0]['TW'], o.spec_comps[j]['factor'][0]['TW']) < 1e-8
+
+
+def test_column_sets_past_64_vs_oracle():
+    """K > 64 (padded to 128 columns): the column sets of compute_sigma_comp_2d,
+    the source powers and the separation sources are 128-bit, so a spectral
+    component whose columns pass 64 (here 40..79 of source 0) is selected
+    exactly (a 64-bit mask kept only its low columns)."""
+    m, o, X = _c3_like(49, 60, 2, 80, 1, 1)
+    for mod in (m, o):
+        _split_spec(mod, {0: [40, 40], 1: [80]})
+        mod.noise['PSD'] = mod.noise['ann_PSD_lim'][0]
+    for j, keys in ((0, [2]), (0, [0]), (0, []), (1, [])):
+        sd, so = m.compute_sigma_comp_2d(j, keys)
+        sdo, soo = o.compute_sigma_comp_2d(j, keys)
+        assert rel(sd, sdo) < 1e-12 and rel(so, soo) < 1e-12, (j, keys)
+    # one separation source per spectral component (columns 40..79 of source 0)
+    groups = {n: [k] for n, k in enumerate(sorted(m.spec_comps))}
+    S = m.separated_images(groups)
+    So = o.separated_images(X, groups)
+    assert S.shape == So.shape
+    assert rel(np.abs(S), np.abs(So)) < 1e-11

@@ -1,0 +1,73 @@
+"""The FASST class-surface helpers outside the GEM loop proper, against the
+reference's golden run and the oracle: initializeConvParams
+(audioModel.py:2224-2294), comp_spat_cmps_powers (:500-512) and the
+reference's setComponentParameter stub (:2042-2089)."""
+import os
+
+import numpy as np
+import pytest
+import scipy.io.wavfile as wf
+
+import fasst_ref as R
+from helpers import load, rel
+from test_gpu_parity import _c3_like, _split_spec
+
+pytestmark = pytest.mark.gpu
+
+
+def _convinit_model(tmp_path, g):
+    import pyfasst_amd.audioModel as am
+    wav = os.path.join(str(tmp_path), "convinit.wav")
+    wf.write(wav, int(g['fs']), g['wav'])
+    np.random.seed(0)
+    return am.MultiChanNMFConv(wav, nbComps=3, nbNMFComps=4, spatial_rank=[1, 2, 1],
+                               iter_num=3, wlen=256, hopsize=64)
+
+
+def test_initialize_conv_params_rand_vs_reference(tmp_path):
+    """'rand': the steering vectors drawn in the reference's RNG order give
+    its parameters bit for bit; the EM from that state matches its run."""
+    g = load("convinit_rand")
+    m = _convinit_model(tmp_path, g)
+    np.random.seed(9)
+    m.initializeConvParams(initMethod='rand')
+    for j in range(3):
+        assert m.spat_comps[j]['mix_type'] == 'conv' == str(g['mix_type_%d' % j])
+        np.testing.assert_array_equal(m.spat_comps[j]['params'], g['init_params_%d' % j])
+    ll = m.estim_param_a_post_model()
+    assert rel(ll, g['logliks']) < 1e-10
+    for j in range(3):
+        assert rel(m.spat_comps[j]['params'], g['final_params_%d' % j]) < 1e-9
+    for k in range(3):
+        assert rel(m.spec_comps[k]['factor'][0]['FB'], g['final_FB_%d' % k]) < 1e-9
+        assert rel(m.spec_comps[k]['factor'][0]['TW'], g['final_TW_%d' % k]) < 1e-9
+
+
+def test_initialize_conv_params_other_methods(tmp_path):
+    g = load("convinit_rand")
+    m = _convinit_model(tmp_path, g)
+    with pytest.raises(NotImplementedError):   # DEMIX is out of scope
+        m.initializeConvParams()
+    with pytest.raises(ValueError):
+        m.initializeConvParams(initMethod='svd')
+
+
+def test_comp_spat_cmps_powers_vs_oracle():
+    """Sum of the listed spatial components' powers (several spectral
+    components on one of them), from the device's parameters."""
+    m, o, X = _c3_like(65, 77, 3, 12, 2, 1)
+    for mod in (m, o):
+        _split_spec(mod, {0: [5, 7], 1: [12], 2: [4, 4, 4]})
+    for inds in ([0], [2, 0], [0, 1, 2]):
+        V = m.comp_spat_cmps_powers(inds)
+        Vo = o.comp_spat_cmps_powers(inds)
+        assert V.shape == (65, 77)
+        assert rel(V, Vo) < 1e-13, inds
+
+
+def test_set_component_parameter_is_the_reference_stub():
+    m, o, X = _c3_like(33, 40, 2, 4, 1, 1)
+    FB = np.array(m.spec_comps[0]['factor'][0]['FB'])
+    with pytest.raises(NameError):
+        m.setComponentParameter(np.ones_like(FB), 0)
+    np.testing.assert_array_equal(m.spec_comps[0]['factor'][0]['FB'], FB)

@@ -239,6 +239,26 @@ def test_nmf_init_golden(same):
         np.testing.assert_array_equal(m.spec_comps[k]['factor'][0]['FB'], g['final_FB_%d' % k])
 
 
+def test_conv_rand_init_golden():
+    """initializeConvParams(initMethod='rand') (audioModel.py:2224-2294): the
+    steering vectors' RNG order and the 'conv' parameters, then EM."""
+    g = load("convinit_rand")
+    x, _ = R.read_scaled(g['wav'])
+    X = [R.stft(x[:, c], np.hanning(256), 64, 256) for c in range(2)]
+    m = R.RefFASST(iter_num=3)
+    m.set_transform(X)
+    np.random.seed(0)
+    R.init_nmf_inst(m, 3, 4, [1, 2, 1])
+    np.random.seed(9)
+    R.init_conv_rand(m)
+    for j in range(3):
+        assert m.spat_comps[j]['mix_type'] == str(g['mix_type_%d' % j])
+        np.testing.assert_array_equal(m.spat_comps[j]['params'], g['init_params_%d' % j])
+    np.testing.assert_array_equal(m.estim_param_a_post_model(), g['logliks'])
+    for j in range(3):
+        np.testing.assert_array_equal(m.spat_comps[j]['params'], g['final_params_%d' % j])
+
+
 def test_nnls_oracle_matches_reference_run():
     """initHF00='nnls' (SeparateLeadStereoTF.py:982-993): the oracle's per-frame
     scipy.optimize.nnls reproduces the HF00 the reference handed to SIMM."""
