@@ -84,9 +84,15 @@ struct fasst_ctx {
   // next iteration of the same fasst_run batch skips launch_w_old
   fasst::DBuf<double> Wkf_next;
   int w_ready = 0;
+  // FWHt and hsum of the final TW formed by the fused k_tw_update / tail
+  // (hpart: its per-block row sums): the next iteration of the batch skips
+  // launch_spectral_prep (no side-stream work beside its E-step)
+  fasst::DBuf<double> hpart;
+  int prep_ready = 0;
   // the fused tail is taken for the structures it covers (fast_tail in
-  // fasst_em.hip) unless FASST_FAST_TAIL=0 was set when this context was created
-  int ftail = 1;
+  // fasst_em.hip) unless FASST_FAST_TAIL=0 was set when this context was
+  // created; 2 (default): it also forms the next iteration's FWHt / hsum
+  int ftail = 2;
   // every launch of an iteration on the main stream (FASST_SERIAL_PREP=1: A/B)
   int serial = 0;
   // TW contraction form: 0 = k_tw_contract (W operands from L2 per lane),

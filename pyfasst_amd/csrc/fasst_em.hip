@@ -2004,17 +2004,28 @@ struct TUArgs {
   const double *scal;
   double *tpart;
   int ntb, K[kMaxJ], soff[kMaxJ];
+  // and (FWHt non-null, KP <= 64) the next iteration's spectral-update
+  // operands from the final TW of its 64 frames: FWHt = (FW TW)^T with the
+  // renormalised FW (k_fwh_t's sum), and per-block TW row sums hpart
+  // [J][KP][ntb] (k_tw_rowsum's; reduced in k_renorm_tail)
+  const double *FW;
+  double *FWHt, *hpart;
   const int *halt;
 };
 // TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
 __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
   HALT_GUARD(a.halt);
   __shared__ double s_r[64][65];
+  // (prep: the block's final TW rows [KP][64], padding rows / frames 0)
+  extern __shared__ __attribute__((aligned(16))) double s_y[];
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
   if (a.scal) {
     // y = fl(fl(TW r) w2): the two roundings of k_tw_update then k_renorm_apply
     const bool fr = a.tw_free[j];
     const double *w2 = a.scal + (size_t)j * (2 + 2 * a.KP) + 2 + a.KP;
+    const bool prep = a.FWHt != nullptr;
+    if (prep)
+      for (int idx = threadIdx.x; idx < a.KP * 64; idx += blockDim.x) s_y[idx] = 0.0;
     double tsum = 0.0;
     for (int kb = 0; kb < a.K[j]; kb += 64) {
       const int kn = min(64, a.K[j] - kb);
@@ -2044,12 +2055,45 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
           const double y = x * w2[k];
           *p = y;
           tsum += y;
+          if (prep) s_y[k * 64 + tl] = y;
         }
       }
       __syncthreads();
     }
     tsum = block_sum(tsum, &s_r[0][0]);
     if (threadIdx.x == 0) a.tpart[(size_t)a.soff[j] * a.ntb + blockIdx.x] = tsum;
+    if (!prep) return;
+    // FW (renormalised by k_renorm_rows, which this launch waits for),
+    // transposed into s_r: s_fw[q][k] = FW[k][q]
+    const int KP = a.KP;
+    double *s_fw = &s_r[0][0];   // (KP * KP <= 64 * 65)
+    for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
+      const int k = idx / KP, q = idx % KP;
+      s_fw[q * KP + k] = a.FW[(size_t)j * KP * KP + idx];
+    }
+    __syncthreads();
+    // FWHt^T tiles on the matrix cores: wave w forms frames 16 w .. 16 w + 15,
+    // D[k][t] = sum_q FW[k][q] y[q][t] (16x16x4 per 16 k x 4 q); lane (fl,
+    // tq) then holds FWHt[16 w + fl][16 kc + tq + 4 i]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
+    const int tn = min(64, a.Tp - t0);
+    for (int kc = 0; kc < KP / 16; ++kc) {
+      d4 d = d4{0.0, 0.0, 0.0, 0.0};
+      for (int q0 = 0; q0 < KP; q0 += 4)
+        d = mfma4(s_fw[(q0 + tq) * KP + 16 * kc + fl], s_y[(q0 + tq) * 64 + 16 * wv + fl], d);
+      if (16 * wv + fl < tn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          a.FWHt[((size_t)j * a.Tp + t0 + 16 * wv + fl) * KP + 16 * kc + tq + 4 * i] = d[i];
+    }
+    // row sums over the block's frames (t < T: the padding frames hold 0):
+    // one wave per row, lane = frame, the wave's tree
+    for (int q = wv; q < KP; q += 4) {
+      double h = s_y[q * 64 + lane];
+#pragma unroll
+      for (int mm = 32; mm > 0; mm >>= 1) h += __shfl_xor(h, mm, 64);
+      if (lane == 0) a.hpart[((size_t)j * KP + q) * a.ntb + blockIdx.x] = h;
+    }
     return;
   }
   if (!a.tw_free[j]) return;
@@ -2209,6 +2253,11 @@ struct RArgs {
   // the E-step's loglik partials
   const double *pmax2, *pe2, *tpart2, *llpart;
   double *ll_out;
+  // k_tw_update's TW row-sum partials [J][KP][ntb] -> hsum [J][KP] (null: the
+  // next iteration's k_tw_rowsum forms hsum)
+  const double *hpart;
+  double *hsum;
+  int J;
   double inv_FT;
   int nstat, ntb, nll;
   int F, T, Fp, Tp, KP, nchunk, tpc, fpc, nslot;
@@ -2532,6 +2581,19 @@ __global__ __launch_bounds__(256) void k_renorm_rows(const RArgs a) {
 // from k_tw_update's partial sums (audioModel.py:2023)
 __global__ __launch_bounds__(256) void k_renorm_tail(const RArgs a, int iter) {
   HALT_GUARD(a.halt);
+  if (blockIdx.x > 0) {
+    // blocks 1..: hsum[r] = sum_t TW row r from k_tw_update's per-block
+    // partials, one wave per row (lane-strided, then the wave's tree: a
+    // fixed order)
+    const int r = (blockIdx.x - 1) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= a.J * a.KP) return;
+    double h = 0.0;
+    for (int b = lane; b < a.ntb; b += 64) h += a.hpart[(size_t)r * a.ntb + b];
+#pragma unroll
+    for (int mm = 32; mm > 0; mm >>= 1) h += __shfl_xor(h, mm, 64);
+    if (lane == 0) a.hsum[r] = h;
+    return;
+  }
   __shared__ double s[256];
   double x = 0.0;
   for (int i = threadIdx.x; i < a.nll; i += 256) x += a.llpart[i];
@@ -2981,7 +3043,8 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(rpe2, (size_t)J * c->nft);
   ALLOC(rtpart2, (size_t)kMaxSlot * c->ntb);
   ALLOC(Wkf_next, (size_t)J * KP * Fp);
-  c->w_ready = 0;
+  ALLOC(hpart, (size_t)J * KP * c->ntb);
+  c->w_ready = c->prep_ready = 0;
 #undef ALLOC
   c->configured = 1;
   return FASST_OK;
@@ -3374,7 +3437,9 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
 // multi-block path once sent garbage pointers to the device)
 static int check_tail_args(const fasst_ctx *c, const UArgs &u, const TUArgs &tu) {
   const bool ok_u = !u.pmax || (u.pmax == c->rpmax2.p && u.pe == c->rpe2.p && u.A == c->A.p);
-  const bool ok_t = !tu.scal || (tu.scal == c->rscal.p && tu.tpart == c->rtpart2.p);
+  const bool ok_t = !tu.scal || (tu.scal == c->rscal.p && tu.tpart == c->rtpart2.p &&
+                                 (!tu.FWHt || (tu.FWHt == c->FWHt.p && tu.hpart == c->hpart.p &&
+                                               tu.FW == c->FW.p && c->KP <= 64)));
   if (ok_u && ok_t) return FASST_OK;
   set_error("internal: fused renormalisation arguments do not point at the context's buffers");
   return FASST_ERR_SHAPE;
@@ -3756,6 +3821,11 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   tu.scal = tail ? c->rscal.p : nullptr;
   tu.tpart = c->rtpart2.p;
   tu.ntb = c->ntb;
+  // the next iteration's FWHt / TW row sums formed here too (KP <= 64)
+  const bool prep = tail && c->KP <= 64 && c->ftail >= 2;
+  tu.FW = c->FW.p;
+  tu.FWHt = prep ? c->FWHt.p : nullptr;
+  tu.hpart = c->hpart.p;
   for (int j = 0; j < kMaxJ; ++j) {
     tu.K[j] = j < J ? c->K[j] : 0;
     tu.soff[j] = j < J ? c->soff[j] : 0;
@@ -3839,9 +3909,10 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
     default: launch_contract<8>(c, b, t, false); break;
   }
   FASST_LAUNCH_CHECK();
-  if (tail == 2) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_scales, 0));
+  // (prep reads the renormalised FW: wait for k_renorm_rows, else the scales)
+  if (tail == 2) FASST_HIP(hipStreamWaitEvent(c->stream, prep ? c->ev_rows : c->ev_scales, 0));
   prof_begin(c, KTWU);
-  k_tw_update<<<dim3(c->ntb, J), 256, 0, c->stream>>>(tu);
+  k_tw_update<<<dim3(c->ntb, J), 256, prep ? (size_t)c->KP * 64 * sizeof(double) : 0, c->stream>>>(tu);
   prof_end(c, KTWU);
   FASST_LAUNCH_CHECK();
   return FASST_OK;
@@ -3891,7 +3962,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   // parameters: fork them onto the side stream (FASST_SERIAL_PREP=1 keeps
   // every launch on the main stream: A/B)
   const bool fork = !c->serial;
-  int st = launch_spectral_prep(c, fork);
+  // (FWHt and the row sums were formed by the previous iteration's fused
+  // tail in the same batch: nothing to fork)
+  const bool prep_ready = c->prep_ready;
+  c->prep_ready = 0;
+  int st = prep_ready ? FASST_OK : launch_spectral_prep(c, fork);
   if (st) return st;
   const bool w_ready = c->w_ready;   // (the previous iteration's fused tail formed W)
   c->w_ready = 0;
@@ -3924,7 +3999,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.ybase = e.tbase = 0;
   launch_estep(c, e, c->nchunk_e);
   FASST_LAUNCH_CHECK();
-  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
+  if (fork && !prep_ready) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
   const bool ft = fast_tail(c);
   if (!ft) {   // (fused tail: summed by k_renorm_tail)
     prof_begin(c, KLL);
@@ -3995,12 +4070,17 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
   RArgs r = renorm_args(c);
   r.ll_out = ll_dev;
+  const bool prep = c->KP <= 64 && c->ftail >= 2;   // (spectral_update's k_tw_update formed FWHt)
+  r.hpart = prep ? c->hpart.p : nullptr;
+  r.hsum = c->hsum.p;
+  r.J = J;
   prof_begin(c, KRTAIL);
-  k_renorm_tail<<<1, 256, 0, c->stream>>>(r, iter);
+  k_renorm_tail<<<1 + (prep ? (J * c->KP + 3) / 4 : 0), 256, 0, c->stream>>>(r, iter);
   prof_end(c, KRTAIL);
   FASST_LAUNCH_CHECK();
   std::swap(c->Wkf.p, c->Wkf_next.p);
   c->w_ready = 1;
+  c->prep_ready = prep;
   return FASST_OK;
 }
 
@@ -4038,7 +4118,7 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->Tp = round_up(T, kTile);
   c->nft = c->Fp / kTile;
   c->ntt = c->Tp / kTile;
-  if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v) != 0;
+  if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v);
   if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
   if (const char *v = getenv("FASST_TWL")) c->twl = atoi(v);
   int st = FASST_OK;
@@ -4118,6 +4198,7 @@ int fasst_destroy(fasst_ctx *c) {
     c->rpmax2.release();
     c->rpe2.release();
     c->rtpart2.release();
+    c->hpart.release();
     c->Wkf_next.release();
     c->mplanes.release();
     c->bden.release();
@@ -4487,7 +4568,7 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
   // host reads the flags once at the end.  Profiling keeps one sync per
   // iteration so the per-kernel events can be folded.
   c->halt = c->flags.p + kFlagHalt;
-  c->w_ready = 0;
+  c->w_ready = c->prep_ready = 0;
   const int sync_every = c->prof ? fasst_ctx::kProfRing : n_iter;
   int done = 0;
   for (int it = 0; it < n_iter; ++it) {
@@ -4512,7 +4593,7 @@ int fasst_run(fasst_ctx *c, int n_iter, const double *psd, double omega, double 
     if ((st = launch_w_old(c))) return st;
     FASST_HIP(hipStreamSynchronize(c->stream));
   }
-  c->w_ready = 0;
+  c->w_ready = c->prep_ready = 0;
   if (c->h_flags[0]) {
     set_error("Singular Matrix");
     return FASST_ERR_SINGULAR;
