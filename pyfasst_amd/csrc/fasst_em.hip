@@ -331,9 +331,11 @@ __device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsign
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(es_u2, v), r, (int)vo, (int)so, AUX);
 }
 
+// (J = 4 at K = 128: the 64 KB W tile leaves one block per CU, so one wave
+// per SIMD and the full register file for the pipelined V tile)
 template <int J, int NKS, int RKU>
-__global__ __launch_bounds__(256, J > 4 ? 1 : 2)
-__attribute__((amdgpu_waves_per_eu(1, J > 4 ? 1 : 2))) FASST_NO_LDS_PAIRING
+__global__ __launch_bounds__(256, (J > 4 || (J == 4 && NKS == 32)) ? 1 : 2)
+__attribute__((amdgpu_waves_per_eu(1, (J > 4 || (J == 4 && NKS == 32)) ? 1 : 2))) FASST_NO_LDS_PAIRING
 void k_estep_mx(const EArgs a) {
   HALT_GUARD(a.halt);
   using S = MXShape<J>;
@@ -488,10 +490,17 @@ void k_estep_mx(const EArgs a) {
     // than 32 operands (J > 4 or K > 32 at J = 4) the sources beyond the first
     // 32 operands load next to their own MFMAs
     // (VR: none up front -- the V loop below pipelines them source by source)
-    constexpr int JA = VR ? 1 : (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
+    // CP: more operands than that (J <= 4 at K >= 64): the V tiles as one
+    // pipeline of 8-MFMA chunks over (source, k), each chunk's TW operands
+    // issued two chunks ahead -- the per-source inline loads left each
+    // source's load latency exposed (J = 4, K = 128: 2.70 ms).  (The same
+    // pipeline for the VR loop with W from L2, J > 4 at K = 128, crashes
+    // ROCm 7.2's compiler at distance 2 and spills 0.4-1.8 KB per lane at 1.)
+    constexpr bool CP = !VR && J * NKS > 32;
+    constexpr int JA = (VR || CP) ? 1 : (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
     double twv[JA][NKS];
 #pragma unroll
-    for (int j = 0; j < JA; ++j) {
+    for (int j = 0; j < (CP ? 0 : JA); ++j) {
       const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
       for (int s = 0; s < NKS; ++s)
@@ -501,7 +510,35 @@ void k_estep_mx(const EArgs a) {
     if constexpr (!CXE) load_cx(tt, cxv);  // this tile's Cx (in flight with the TW operands)
     __builtin_amdgcn_sched_barrier(0);
     d4 v[J];
-    if constexpr (VR) {
+    if constexpr (CP) {
+      constexpr int CH = 8, CPS = NKS / CH, NCH = J * CPS, PD = 2;   // chunks, prefetch distance
+      static_assert(NKS % CH == 0, "k chunks of 8");
+      double ta[PD + 1][CH], wa[PD + 1][WL ? 1 : CH];
+      auto ld = [&](int u, int sl) {
+        const int j = u / CPS, s0 = (u % CPS) * CH;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const int s = s0 + c;
+          ta[sl][c] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u);
+          if constexpr (!WL)
+            wa[sl][c] = a.Wkf[lofs + ((size_t)j * KP + tq + 4 * s) * a.Fp + f];
+        }
+      };
+#pragma unroll
+      for (int u = 0; u < PD; ++u) ld(u, u);
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        if (u + PD < NCH) ld(u + PD, (u + PD) % (PD + 1));
+        __builtin_amdgcn_sched_barrier(0);
+        const int j = u / CPS, s0 = (u % CPS) * CH, sl = u % (PD + 1);
+        if (s0 == 0) v[j] = d4{0.0, 0.0, 0.0, 0.0};
+        const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          v[j] = mfma4(ta[sl][c], WL ? sw[4 * (s0 + c) * 16] : wa[sl][WL ? 0 : c], v[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (VR) {
       // source j + 1's TW operands in flight while source j's MFMAs run; the
       // barriers keep the scheduler from hoisting every source's loads (at
       // K = 64 / 128 they alone would fill the register file)
@@ -533,7 +570,7 @@ void k_estep_mx(const EArgs a) {
       }
     }
 #pragma unroll
-    for (int j = 0; j < (VR ? 0 : J); ++j) {
+    for (int j = 0; j < ((VR || CP) ? 0 : J); ++j) {
       v[j] = d4{0.0, 0.0, 0.0, 0.0};
       const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
       const double *gw = a.Wkf + lofs + ((size_t)j * KP + tq) * a.Fp + f;
@@ -2004,7 +2041,7 @@ struct TUArgs {
   const double *scal;
   double *tpart;
   int ntb, K[kMaxJ], soff[kMaxJ];
-  // and (FWHt non-null, KP <= 64) the next iteration's spectral-update
+  // and (FWHt non-null) the next iteration's spectral-update
   // operands from the final TW of its 64 frames: FWHt = (FW TW)^T with the
   // renormalised FW (k_fwh_t's sum), and per-block TW row sums hpart
   // [J][KP][ntb] (k_tw_rowsum's; reduced in k_renorm_tail)
@@ -2063,29 +2100,42 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
     tsum = block_sum(tsum, &s_r[0][0]);
     if (threadIdx.x == 0) a.tpart[(size_t)a.soff[j] * a.ntb + blockIdx.x] = tsum;
     if (!prep) return;
-    // FW (renormalised by k_renorm_rows, which this launch waits for),
-    // transposed into s_r: s_fw[q][k] = FW[k][q]
+    // FW (renormalised by k_renorm_rows, which this launch waits for)
+    // transposed into s_r, s_fw[q][k] = FW[k][q], QB rows q at a time (all of
+    // them at KP <= 64, the only sizes spectral_update asks this for)
     const int KP = a.KP;
-    double *s_fw = &s_r[0][0];   // (KP * KP <= 64 * 65)
-    for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
-      const int k = idx / KP, q = idx % KP;
-      s_fw[q * KP + k] = a.FW[(size_t)j * KP * KP + idx];
-    }
-    __syncthreads();
+    double *s_fw = &s_r[0][0];
+    const double *gfw = a.FW + (size_t)j * KP * KP;
+    const int QB = KP <= 64 ? KP : 32;
     // FWHt^T tiles on the matrix cores: wave w forms frames 16 w .. 16 w + 15,
     // D[k][t] = sum_q FW[k][q] y[q][t] (16x16x4 per 16 k x 4 q); lane (fl,
     // tq) then holds FWHt[16 w + fl][16 kc + tq + 4 i]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
     const int tn = min(64, a.Tp - t0);
-    for (int kc = 0; kc < KP / 16; ++kc) {
-      d4 d = d4{0.0, 0.0, 0.0, 0.0};
-      for (int q0 = 0; q0 < KP; q0 += 4)
-        d = mfma4(s_fw[(q0 + tq) * KP + 16 * kc + fl], s_y[(q0 + tq) * 64 + 16 * wv + fl], d);
-      if (16 * wv + fl < tn)
+    d4 d[kMaxKP / 16];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          a.FWHt[((size_t)j * a.Tp + t0 + 16 * wv + fl) * KP + 16 * kc + tq + 4 * i] = d[i];
+    for (int kc = 0; kc < kMaxKP / 16; ++kc) d[kc] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int qb = 0; qb < KP; qb += QB) {
+      for (int idx = threadIdx.x; idx < QB * KP; idx += blockDim.x) {
+        const int k = idx / QB, q = idx % QB;   // (coalesced over q in FW's rows)
+        s_fw[q * KP + k] = gfw[(size_t)k * KP + qb + q];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kc = 0; kc < kMaxKP / 16; ++kc)
+        if (16 * kc < KP)
+          for (int q0 = 0; q0 < QB; q0 += 4)
+            d[kc] = mfma4(s_fw[(q0 + tq) * KP + 16 * kc + fl], s_y[(qb + q0 + tq) * 64 + 16 * wv + fl],
+                          d[kc]);
+      __syncthreads();
     }
+    if (16 * wv + fl < tn)
+#pragma unroll
+      for (int kc = 0; kc < kMaxKP / 16; ++kc)
+        if (16 * kc < KP)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            a.FWHt[((size_t)j * a.Tp + t0 + 16 * wv + fl) * KP + 16 * kc + tq + 4 * i] = d[kc][i];
     // row sums over the block's frames (t < T: the padding frames hold 0):
     // one wave per row, lane = frame, the wave's tree
     for (int q = wv; q < KP; q += 4) {
@@ -3376,9 +3426,9 @@ static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool f
     k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, nz ? nz : c->nchunk_b), 64,
                                0, c->stream>>>(b);
     prof_end(c, KFBC);
-  } else if (NKC <= 4 && c->twl) {
+  } else if (c->twl) {
     prof_begin(c, KTWC);
-    twl_switch<NKC <= 4 ? NKC : 4>(c, &t, nullptr);
+    twl_switch<NKC>(c, &t, nullptr);
     prof_end(c, KTWC);
   } else {
     prof_begin(c, KTWC);
@@ -3389,14 +3439,15 @@ static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool f
   }
 }
 
-// resident k_tw_contract_lds blocks per CU (0: c->twl off or KP > 64)
+// resident k_tw_contract_lds blocks per CU (0: c->twl off)
 static int twl_occupancy(const fasst_ctx *c, int *units) {
-  if (!c->twl || c->KP > 64) return 0;
+  if (!c->twl) return 0;
   fasst_ctx *cc = const_cast<fasst_ctx *>(c);
   switch (c->KP) {
     case 16: return twl_switch<1>(cc, nullptr, units);
     case 32: return twl_switch<2>(cc, nullptr, units);
-    default: return twl_switch<4>(cc, nullptr, units);
+    case 64: return twl_switch<4>(cc, nullptr, units);
+    default: return twl_switch<8>(cc, nullptr, units);
   }
 }
 
@@ -3439,7 +3490,7 @@ static int check_tail_args(const fasst_ctx *c, const UArgs &u, const TUArgs &tu)
   const bool ok_u = !u.pmax || (u.pmax == c->rpmax2.p && u.pe == c->rpe2.p && u.A == c->A.p);
   const bool ok_t = !tu.scal || (tu.scal == c->rscal.p && tu.tpart == c->rtpart2.p &&
                                  (!tu.FWHt || (tu.FWHt == c->FWHt.p && tu.hpart == c->hpart.p &&
-                                               tu.FW == c->FW.p && c->KP <= 64)));
+                                               tu.FW == c->FW.p)));
   if (ok_u && ok_t) return FASST_OK;
   set_error("internal: fused renormalisation arguments do not point at the context's buffers");
   return FASST_ERR_SHAPE;
@@ -3822,7 +3873,9 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   tu.tpart = c->rtpart2.p;
   tu.ntb = c->ntb;
   // the next iteration's FWHt / TW row sums formed here too (KP <= 64)
-  const bool prep = tail && c->KP <= 64 && c->ftail >= 2;
+  // (not at KP = 128: its 64 KB TW tile leaves k_tw_update one block per CU,
+  // 0.12 -> 0.38 ms at J = 4, more than the 0.23 ms it takes off the E-step)
+  const bool prep = tail && c->ftail >= 2 && c->KP <= 64;
   tu.FW = c->FW.p;
   tu.FWHt = prep ? c->FWHt.p : nullptr;
   tu.hpart = c->hpart.p;
@@ -4070,7 +4123,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
   RArgs r = renorm_args(c);
   r.ll_out = ll_dev;
-  const bool prep = c->KP <= 64 && c->ftail >= 2;   // (spectral_update's k_tw_update formed FWHt)
+  const bool prep = c->ftail >= 2 && c->KP <= 64;   // (spectral_update's k_tw_update formed FWHt)
   r.hpart = prep ? c->hpart.p : nullptr;
   r.hsum = c->hsum.p;
   r.J = J;
