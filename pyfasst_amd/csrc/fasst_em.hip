@@ -538,6 +538,42 @@ void k_estep_mx(const EArgs a) {
           v[j] = mfma4(ta[sl][c], WL ? sw[4 * (s0 + c) * 16] : wa[sl][WL ? 0 : c], v[j]);
         __builtin_amdgcn_sched_barrier(0);
       }
+    } else if constexpr (VR && !(WL || NKS <= 16)) {
+      // J > 4 at K = 128 (W from L2): a runtime loop over the sources, each
+      // source's V tile a 4-chunk pipeline of 8 MFMAs with the next chunk's TW
+      // and W operands in flight (the last chunk prefetches source j + 1's
+      // first), written to the VST slab as soon as it is formed -- the fully
+      // unrolled form crashes or spills (CP above); the inline loads left one
+      // L2 round trip per source exposed (J = 8, K = 128: 6.85 ms)
+      slab_fence0();   // the previous tile's last reads before these writes
+      constexpr int CH = 8, CPS = NKS / CH;
+      double ta[2][CH], wa[2][CH];
+      auto ld = [&](int j, int s0, int sl) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          ta[sl][c] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * (s0 + c)) * a.Tp) * 8u);
+          wa[sl][c] = a.Wkf[lofs + ((size_t)j * KP + tq + 4 * (s0 + c)) * a.Fp + f];
+        }
+      };
+      ld(0, 0, 0);
+#pragma unroll 1
+      for (int j = 0; j < J; ++j) {
+        d4 vj = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < CPS; ++c) {
+          const int sl = c & 1;
+          if (c + 1 < CPS)
+            ld(j, (c + 1) * CH, sl ^ 1);
+          else if (j + 1 < J)
+            ld(j + 1, 0, sl ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cc = 0; cc < CH; ++cc) vj = mfma4(ta[sl][cc], wa[sl][cc], vj);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] = vj[i];
+      }
     } else if constexpr (VR) {
       // source j + 1's TW operands in flight while source j's MFMAs run; the
       // barriers keep the scheduler from hoisting every source's loads (at
@@ -580,7 +616,7 @@ void k_estep_mx(const EArgs a) {
         v[j] = mfma4(j < JA ? twv[j < JA ? j : 0][s] : tw[(size_t)(4 * s) * a.Tp],
                      WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
     }
-    if constexpr (VST) {
+    if constexpr (VST && (WL || NKS <= 16)) {   // (else written by the loop above)
       slab_fence0();   // the previous tile's last reads before these writes
 #pragma unroll
       for (int i = 0; i < 4; ++i)

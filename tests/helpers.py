@@ -127,6 +127,13 @@ FULL_CASES = {
                     data_rank=2, data_seed=0, init_seed=1),
     "c3_t1000": dict(F=2049, T=1000, J=4, K=32, rank=2, conv=True, iters=3, K_true=8,
                      data_rank=2, data_seed=3, init_seed=1),
+    # K = 128 at the full F (the production launch shapes of the K > 64
+    # paths: the pipelined E-step V tiles, the LDS-staged TW contraction at
+    # KP = 128, the FW-from-L2 staging kernels)
+    "j8k128_t1000": dict(F=2049, T=1000, J=8, K=128, rank=1, conv=True, iters=2, K_true=8,
+                         data_rank=1, data_seed=5, init_seed=1),
+    "j4k128_t1000": dict(F=2049, T=1000, J=4, K=128, rank=2, conv=True, iters=2, K_true=8,
+                         data_rank=2, data_seed=6, init_seed=1),
     "c1_50": dict(F=1025, T=1122, J=2, K=32, rank=1, conv=False, iters=50, K_true=8,
                   data_rank=1, data_seed=0, init_seed=0),
     "c5_full": dict(F=2049, N=20000, NF0=1092, P=30, K=4, R=40, iters=1, data_seed=0,

@@ -63,7 +63,7 @@ def _drift(m, g, name):
     return d
 
 
-@pytest.mark.parametrize("name", ["c3_full", "c3_t1000"])
+@pytest.mark.parametrize("name", ["c3_full", "c3_t1000", "j8k128_t1000", "j4k128_t1000"])
 def test_config3_full_size_vs_oracle(name):
     """BASELINE configs[2] (F=2049, T=10000, J=4, r=2, K=32) at its real size:
     the production launch shapes (several E-step / FB chunks, TW bin splits,
