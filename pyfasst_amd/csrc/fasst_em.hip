@@ -1994,7 +1994,6 @@ __device__ __forceinline__ void tw_contract_lds_body(const TArgs &a) {
   const int s1 = (tq & 1) << 4;
   const int ofp = CF::WF0 + 4 * tq * KP + fl + s1, ofm = ofp - 2 * s1;
   const int orr = CF::WD + wv * TPW * CF::RD + (2 * tq * 16 + fl) * 2;   // granules 2 tq, 2 tq + 1
-  const int bq = 4 * tq;
   for (int c = 0; c < nst; ++c) {
     // this wave's stage c pieces have landed (younger stages may still fly)
     const int ahead = min(NS - 2, nst - 1 - c);
@@ -2006,38 +2005,33 @@ __device__ __forceinline__ void tw_contract_lds_body(const TArgs &a) {
     __builtin_amdgcn_s_barrier();   // every wave's stage c is in; stage c - 1 is read
     if (c + NS - 1 < nst) issue(c + NS - 1);
     const double *st = smem + (c % NS) * SS;
-    const int f0 = (fb + c) * 16;
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
       if (tt0 + p >= a.ntt) break;  // wave-uniform: no frame tile left
-      const int t = (tt0 + p) * 16 + fl;
       typedef double dv2 __attribute__((ext_vector_type(2)));
       const dv2 h01 = *(const dv2 *)(st + orr + p * CF::RD);
       const dv2 h23 = *(const dv2 *)(st + orr + p * CF::RD + 32);
       const double h[4] = {h01.x, h01.y, h23.x, h23.y};
-      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo, vo2 = vo, vn2 = vo;
+      // (this kernel is bound by MFMA + VALU issue, which do not overlap on
+      // gfx950: one accumulation chain per V tile, one Newton step on
+      // v_rcp_f64, no padding masks -- a bin past F meets W_new's zero rows
+      // in the contraction, a frame past T lands in num / den columns
+      // k_tw_update never reads, and every padded operand is finite)
+      d4 vo = d4{0.0, 0.0, 0.0, 0.0}, vn = vo;
 #pragma unroll
-      for (int s = 0; s < NKS; s += 2) {
-        const double ao0 = st[ow + 64 * s], ao1 = st[ow + 64 * (s + 1)];
-        vo = mfma4(ao0, bt[p][s], vo);
-        vo2 = mfma4(ao1, bt[p][s + 1], vo2);
-        const double an0 = st[CF::WN0 + ow + 64 * s], an1 = st[CF::WN0 + ow + 64 * (s + 1)];
-        vn = mfma4(an0, bt[p][s], vn);
-        vn2 = mfma4(an1, bt[p][s + 1], vn2);
+      for (int s = 0; s < NKS; ++s) {
+        vo = mfma4(st[ow + 64 * s], bt[p][s], vo);
+        vn = mfma4(st[CF::WN0 + ow + 64 * s], bt[p][s], vn);
       }
-      vo += vo2;
-      vn += vn2;
-      const bool tok = t < a.T;
       double r3[4], r4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double vm = fmax(vn[i], kEps);
-        const double rv = rcp_nr(vm);
-        const bool ok = tok && f0 + bq + i < a.F;
+        double rv = __builtin_amdgcn_rcp(vm);
+        rv = fma(fma(-vm, rv, 1.0), rv, rv);
         const double other = fmax(vo[i], kEps);
-        const double q = (h[i] * other) * (rv * rv);   // hat_W from the E-step's rho
-        r3[i] = ok ? other * q : 0.0;
-        r4[i] = ok ? other * rv : 0.0;
+        r4[i] = other * rv;                // other / V_new
+        r3[i] = (h[i] * r4[i]) * r4[i];    // other hat_W / V_new^2, hat_W = rho other
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
