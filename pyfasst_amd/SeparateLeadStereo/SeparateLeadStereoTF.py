@@ -442,6 +442,59 @@ class SeparateLeadProcess(object):
         warnings.warn("This function does not work well with framed estimation.")
         raise TypeError("exceptions must derive from BaseException")
 
+    # the reference's scale patterns (:1105-1110) in the order its Python 2
+    # dict iterates them (string hashes of CPython 2.7 without randomisation:
+    # slots 0, 3, 5, 7 of the 8-slot table) -- the row order of
+    # scoresPerTuning and the key determineTuning returns
+    _tuningPatterns = (
+        ('andalusPattern', (0, 1, 4, 5, 7, 8, 11)),
+        ('minorHarmoPattern', (0, 2, 3, 5, 7, 8, 10)),
+        ('minorMelodPattern', (0, 2, 3, 5, 7, 9, 11)),
+        ('majorPattern', (0, 2, 4, 5, 7, 9, 11)),
+    )
+
+    def computeChroma(self, maxFrames=3000):
+        """Chroma of the pipeline's HF0 (:1074-1094): bin n of the
+        12·stepNotes-bin octave = mean over frames' HF0 rows n, n + 12·stepNotes,
+        ..., then each frame normalised to sum 1.  Runs estimHF0 first when HF0
+        is missing, as the reference does."""
+        import warnings
+        if not hasattr(self, 'SIMMParams'):
+            raise AttributeError("The parameters for the SIMM are not well initialized")
+        if 'HF0' not in self.SIMMParams:
+            self.estimHF0(maxFrames=maxFrames)
+        if not hasattr(self, 'N'):
+            warnings.warn("Issues with the attributes, running again the estimation.")
+            self.estimHF0(maxFrames=maxFrames)
+        octave = 12 * self.SIMMParams['stepNotes']
+        HF0 = np.asarray(self.SIMMParams['HF0'])
+        chroma = np.zeros([octave, self.computeNFrames()])
+        for n in range(octave):
+            chroma[n] = HF0[n::octave].mean(axis=0)
+        chroma /= chroma.sum(axis=0)
+        self.chroma = chroma
+
+    def determineTuning(self):
+        """Key / tuning / scale by pattern scores on the summed chroma
+        (:1096-1128): (scoresPerTuning [4, stepNotes·12], bestTuning, bestKey,
+        pattern name), the indices by integer division as the reference's
+        Python 2 code computes them."""
+        if not hasattr(self, 'chroma'):
+            self.computeChroma()
+        summary = self.chroma.sum(axis=1)
+        nbTunings = self.SIMMParams['stepNotes']
+        nbKey = 12
+        scores = np.zeros([len(self._tuningPatterns), nbTunings * nbKey])
+        for ntun in range(nbTunings):
+            for nk in range(nbKey):
+                for npatt, (_, pattern) in enumerate(self._tuningPatterns):
+                    idx = np.mod((np.array(pattern) + nk) * nbTunings + ntun, summary.size)
+                    scores[npatt, ntun + nk * nbTunings] = summary[idx].sum()
+        best = int(np.argmax(scores))
+        bestPattern, rest = divmod(best, nbTunings * nbKey)
+        bestKey, bestTuning = divmod(rest, nbTunings)
+        return scores, bestTuning, bestKey, self._tuningPatterns[bestPattern][0]
+
     def initiateHF0WithIndexBestPath(self):
         """HF00: the melody's neighbourhood set to max HF0 (:1321-1368)."""
         NF0 = self.SIMMParams['NF0']
