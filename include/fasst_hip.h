@@ -170,10 +170,13 @@ int fasst_separate_waveforms(fasst_ctx *ctx, const double *psd, const double *wi
                              const double *analysis_window, int wlen, int nfft, int hop,
                              double *y);
 
-/* Per-kernel timing with HIP events recorded on the context's stream
- * (used by bench.py for the roofline of the dominant kernel).
- * fasst_kernel_times returns the number of kernel slots and fills the mean
- * duration in ms of each slot over the profiled iterations.                */
+/* Per-kernel timing with HIP events (used by bench.py for the roofline of
+ * the dominant kernel), in the timed loop's own schedule: each pair is
+ * recorded on the stream its kernel runs on (the side stream stays forked),
+ * in a ring of 32 iterations between host syncs.  fasst_kernel_times
+ * returns the number of kernel slots and fills the mean duration in ms of
+ * each slot over the profiled iterations (a side-stream slot measures its
+ * kernel while the main stream's kernels run beside it).                   */
 int fasst_set_profiling(fasst_ctx *ctx, int on);
 int fasst_kernel_times(fasst_ctx *ctx, double *avg_ms, long *counts, int nk);
 const char *fasst_kernel_name(int i);

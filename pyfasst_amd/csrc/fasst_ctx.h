@@ -32,6 +32,7 @@ struct fasst_ctx {
   // observation
   int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
   fasst::DBuf<double> cx;        // 4*Tp*Fp
+  bool cx_ready = false;          // an observation was written (set_cx / set_stft / set_audio)
   fasst::DBuf<double2> X;        // 2*Tp*Fp (resident STFT, optional)
   bool have_X = false;
   // model
@@ -98,6 +99,7 @@ struct fasst_ctx {
   // TW contraction form: 0 = k_tw_contract (W operands from L2 per lane),
   // 1 = k_tw_contract_lds (FASST_TWL, read at creation)
   int twl = 1;
+  int twub = 0;   // FASST_TWU_BATCH: k_tw_update's batched element loops (A/B)
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart

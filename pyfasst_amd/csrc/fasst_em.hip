@@ -27,6 +27,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <mutex>
 
 namespace fasst {
@@ -68,6 +69,16 @@ __device__ __forceinline__ dim3 xcd_block() {
 
 __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// max(x, y) as ONE v_max_f64: fmax() lowers to llvm.maxnum, whose operands
+// the backend first canonicalises (a second v_max_f64 each) unless it can
+// prove them canonical, which it cannot for MFMA results.  For the finite
+// operands it is used on the two forms agree.
+__device__ __forceinline__ double vmax_f64(double x, double y) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
 }
 
 // 1/x for finite normal x (the E-step's guarded det and max(V, eps)):
@@ -2026,10 +2037,10 @@ __device__ __forceinline__ void tw_contract_lds_body(const TArgs &a) {
       double r3[4], r4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const double vm = fmax(vn[i], kEps);
+        const double vm = vmax_f64(vn[i], kEps);
         double rv = __builtin_amdgcn_rcp(vm);
         rv = fma(fma(-vm, rv, 1.0), rv, rv);
-        const double other = fmax(vo[i], kEps);
+        const double other = vmax_f64(vo[i], kEps);
         r4[i] = other * rv;                // other / V_new
         r3[i] = (h[i] * r4[i]) * r4[i];    // other hat_W / V_new^2, hat_W = rho other
       }
@@ -2077,6 +2088,7 @@ struct TUArgs {
   // [J][KP][ntb] (k_tw_rowsum's; reduced in k_renorm_tail)
   const double *FW;
   double *FWHt, *hpart;
+  int batch;   // (FASST_TWU_BATCH) the element loops with all loads issued first
   const int *halt;
 };
 // TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
@@ -2096,6 +2108,62 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
     double tsum = 0.0;
     for (int kb = 0; kb < a.K[j]; kb += 64) {
       const int kn = min(64, a.K[j] - kb);
+      // batch (64 kn = 2048 or 4096 elements, E per thread): every split
+      // load of the thread's E elements in flight before the first use, and
+      // the TW read-modify-write likewise (the plain loops below make one
+      // memory round trip per element); same sums in the same order
+      auto batched = [&](auto e_tag) {
+        constexpr int E = decltype(e_tag)::value;
+        const int n = 64 * kn;
+        if (fr) {
+          double nu[E], de[E];
+#pragma unroll
+          for (int u = 0; u < E; ++u) nu[u] = de[u] = 0.0;
+          for (int c = 0; c < a.nsplit; ++c)
+#pragma unroll
+            for (int u = 0; u < E; ++u) {
+              const int idx = threadIdx.x + 256 * u, tl = idx / kn, kl = idx % kn;
+              const size_t o = (((size_t)c * a.J + j) * a.Tp + min(t0 + tl, a.T - 1)) * a.KP + kb + kl;
+              nu[u] += a.tnum[o];
+              de[u] += a.tden[o];
+            }
+#pragma unroll
+          for (int u = 0; u < E; ++u) {
+            const int idx = threadIdx.x + 256 * u, tl = idx / kn, kl = idx % kn;
+            const double ratio = nu[u] / fmax(de[u], kEps);
+            s_r[kl][tl] = t0 + tl < a.T ? (a.omega == 1.0 ? ratio : pow(ratio, a.omega)) : 1.0;
+          }
+        }
+        __syncthreads();
+        double x[E];
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+          const int idx = threadIdx.x + 256 * u, kl = idx / 64, tl = idx % 64;
+          x[u] = a.TW[((size_t)j * a.KP + kb + kl) * a.Tp + min(t0 + tl, a.T - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+          const int idx = threadIdx.x + 256 * u, kl = idx / 64, tl = idx % 64, t = t0 + tl, k = kb + kl;
+          if (t < a.T) {
+            double y = x[u];
+            if (fr && k >= a.kb0[j] && k < a.kb1[j]) y *= s_r[kl][tl];
+            y *= w2[k];
+            a.TW[((size_t)j * a.KP + k) * a.Tp + t] = y;
+            tsum += y;
+            if (prep) s_y[k * 64 + tl] = y;
+          }
+        }
+        __syncthreads();
+        (void)n;
+      };
+      if (a.batch && kn == 32) {
+        batched(std::integral_constant<int, 8>{});
+        continue;
+      }
+      if (a.batch && kn == 64) {
+        batched(std::integral_constant<int, 16>{});
+        continue;
+      }
       if (fr)
         for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
           const int tl = idx / kn, kl = idx % kn, t = t0 + tl;
@@ -3900,6 +3968,7 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   u.convm = c->convm;
   for (int j = 0; j <= kMaxJ; ++j) u.roff[j] = j <= J ? c->roff[j] : c->R;
   tu.scal = tail ? c->rscal.p : nullptr;
+  tu.batch = c->twub;
   tu.tpart = c->rtpart2.p;
   tu.ntb = c->ntb;
   // the next iteration's FWHt / TW row sums formed here too (KP <= 64)
@@ -4204,6 +4273,7 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v);
   if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
   if (const char *v = getenv("FASST_TWL")) c->twl = atoi(v);
+  if (const char *v = getenv("FASST_TWU_BATCH")) c->twub = atoi(v);
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||

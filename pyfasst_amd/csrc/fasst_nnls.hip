@@ -227,8 +227,24 @@ __global__ __launch_bounds__(64) void k_nnls(const NnlsArgs a) {
           s_j = r1;
         }
         __syncthreads();
-        const int np2 = s_p;
-        for (int r = s_j; r < np2; ++r) append_row(r, lst[r]);
+        int np2 = s_p;
+        for (int r = s_j; r < np2;) {
+          if (append_row(r, lst[r])) {
+            ++r;
+            continue;
+          }
+          // dependent on the compacted set: it leaves P too (skipped until P
+          // next grows), and the rows after it move up one
+          if (lane == 0) {
+            const int k = lst[r];
+            x[k] = 0.0;
+            st[k] = 2;
+            for (int i = r; i + 1 < np2; ++i) lst[i] = lst[i + 1];
+            s_p = np2 - 1;
+          }
+          __syncthreads();
+          np2 = s_p;
+        }
         solve_z(np2);
       }
       if (it >= a.maxiter) break;

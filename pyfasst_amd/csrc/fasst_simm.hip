@@ -381,11 +381,13 @@ __global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(const SPl p, const doubl
 //   2 j + h contracts them (k = tq).  The staged chunk columns are stored
 //   interleaved, column c at (c & 1) 16 + (c >> 1), so the B reads of one
 //   MFMA stay consecutive in tq (the pitch-34 rows keep them conflict-free).
-template <bool ST, int KM, bool V16 = false>
+// KC: frames per staged chunk (32; 16 halves the plane registers of a lane,
+// 40 -> 20 doubles in the stereo form, which spilled at 32)
+template <bool ST, int KM, bool V16 = false, int KC = 32>
 __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const double *__restrict__ HM,
                                                         double *__restrict__ out, size_t slab,
                                                         int R, int kchunk) {
-  constexpr int NC = ST ? 2 : 1, NO = 2 * NC, KC = 32, PH = KC + 2;
+  constexpr int NC = ST ? 2 : 1, NO = 2 * NC, PH = KC + 2, NJ = KC / 4;
   constexpr int NR = 48 + KM + 1;   // HM rows, HPHI rows, the pending scale
   __shared__ double sH[NR * PH];
   const int F = p.F, N = p.N, K = p.K;
@@ -406,15 +408,15 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
     for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
   // chunk column of MFMA j's k = tq, and its staged position
   auto kcol = [&](int j) { return V16 ? 8 * (j >> 1) + 2 * tq + (j & 1) : tq + 4 * j; };
-  auto kpos = [&](int k) { return V16 ? (k & 1) * 16 + (k >> 1) : k; };
+  auto kpos = [&](int k) { return V16 ? (k & 1) * (KC / 2) + (k >> 1) : k; };
   for (int kc = kb; kc < ke; kc += KC) {
     const size_t base = (size_t)f * N + kc + tq;
-    double sfv[8], smv[NC][8], sv[NC][8];
+    double sfv[NJ], smv[NC][NJ], sv[NC][NJ];
     if constexpr (V16) {
       typedef double dv2 __attribute__((ext_vector_type(2)));
       const size_t b2 = (size_t)f * N + kc + 2 * tq;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ / 2; ++j) {
         const bool ok = fin && kc + 8 * j + 2 * tq < ke;   // pairs never straddle ke (even)
         const dv2 z = {0.0, 0.0};
         const dv2 a0 = ok ? *(const dv2 *)(p.SF0 + b2 + 8 * j) : z;
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const bool ok = fin && kc + tq + 4 * j < ke;
         // plain (cached) loads: a lane group reads 32 bytes of a row per
         // instruction, the rest of the line arrives with the next j's
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int kk = kcol(j), kq = kpos(kk);
       const bool ok = fin && kc + kk < ke;
       if (p.SF0w) {   // (plain store: the line's four 32-byte pieces merge in L2)
@@ -987,6 +989,7 @@ struct simm_ctx {
   // fasst_dgemm2.h), 2 = the generic k_gemm (A/B and parity reference);
   // both parity-tested against the oracle
   int gemm_kind = 0;
+  int hmt_kc = 32;   // k_simm_xy_hmt frames per staged chunk (FASST_HMT_KC=16: A/B)
   int Fp = 0, NF0p = 0;   // even (16-byte) row pitches of the WF0 copies below
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
@@ -1205,7 +1208,9 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
   kdispatch(c->K, [&](auto km) {
     constexpr int KM = decltype(km)::value;
     if (c->stereo)
-      if (v16)
+      if (v16 && c->hmt_kc == 16)
+        k_simm_xy_hmt<true, KM, true, 16><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
+      else if (v16)
         k_simm_xy_hmt<true, KM, true><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
       else
         k_simm_xy_hmt<true, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
@@ -1460,6 +1465,7 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
   if (const char *v = getenv("FASST_SIMM_GEMM")) c->gemm_kind = atoi(v) == 2 ? 2 : 0;
+  if (const char *v = getenv("FASST_HMT_KC")) c->hmt_kc = atoi(v) == 16 ? 16 : 32;
   c->Fp = (F + 15) / 16 * 16;
   c->NF0p = (NF0 + 15) / 16 * 16;
   size_t gw = 0;

@@ -527,6 +527,10 @@ int fasst_suff_stat(fasst_ctx *c, int R, const double *V, const double *mix, con
     set_error("fasst_suff_stat: bad arguments (R %d <= %d)", R, kMaxR);
     return FASST_ERR_SHAPE;
   }
+  if (!c->cx_ready || !c->cx.p || c->F < 1 || c->T < 1) {
+    set_error("fasst_suff_stat: no observation resident (upload Cx first)");
+    return FASST_ERR_SHAPE;
+  }
   DeviceGuard g(c->device);
   const size_t FT = (size_t)c->F * c->T;
   DBuf<double> dV, dws, dpsd, dllb, dll;

@@ -709,6 +709,7 @@ int fasst_set_audio(fasst_ctx *c, const double *data, int L, const double *windo
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipStreamSynchronize(c->stream));
   c->have_X = true;
+  c->cx_ready = true;
   return FASST_OK;
 }
 
@@ -739,6 +740,7 @@ int fasst_set_cx(fasst_ctx *c, const double *cx) {
   k_cx_unpack<<<dim3(c->ntt, c->nft), 256, 0, c->stream>>>(h.p, c->cx.p, c->F, c->T, c->Fp, c->Tp);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipStreamSynchronize(c->stream));
+  c->cx_ready = true;
   return FASST_OK;
 }
 
@@ -782,6 +784,7 @@ int fasst_set_stft(fasst_ctx *c, const double *X) {
   k_cx_from_X<<<2048, 256, 0, c->stream>>>(c->X.p, c->cx.p, (size_t)c->Tp * c->Fp);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipStreamSynchronize(c->stream));
+  c->cx_ready = true;
   return FASST_OK;
 }
 

@@ -197,3 +197,19 @@ def test_column_sets_past_64_vs_oracle():
     So = o.separated_images(X, groups)
     assert S.shape == So.shape
     assert rel(np.abs(S), np.abs(So)) < 1e-11
+
+
+def test_suff_stat_refuses_a_context_without_observation():
+    """fasst_suff_stat on a context that never received Cx returns
+    FASST_ERR_SHAPE (ValueError) before any launch, like the other step entry
+    points' host-side guards."""
+    from pyfasst_amd.engine import Engine
+    F, T, Rk = 9, 11, 2
+    e = Engine(F, T)
+    try:
+        V = np.ones((Rk, F, T))
+        mix = np.ones((Rk, 2, F), complex)
+        with pytest.raises(ValueError, match="no observation"):
+            e.suff_stat(V, mix, 1.0)
+    finally:
+        e.close()
