@@ -99,7 +99,6 @@ struct fasst_ctx {
   // TW contraction form: 0 = k_tw_contract (W operands from L2 per lane),
   // 1 = k_tw_contract_lds (FASST_TWL, read at creation)
   int twl = 1;
-  int twub = 0;   // FASST_TWU_BATCH: k_tw_update's batched element loops (A/B)
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart

@@ -59,43 +59,7 @@ struct Dgemm2Args {
   double *C;             // [M][ldc]
   int lda, ldb, ldc, M, N, K;
   int mt, nt;            // tile counts
-  int light_last;        // edge tiles (M / N remainders) dispatched after the full ones
 };
-
-// tile of the XCD-aware order: workgroups b, b + 8, ... share an XCD (and its
-// L2); each XCD gets a contiguous run of the m-fastest tile sequence, so the
-// tiles reading one B column panel meet in one L2 (bijective for any count).
-// light_last: each XCD's run is its share of the full tiles, then its share
-// of the edge tiles (the partial last m row / n column), so the cheap edge
-// tiles fill the dispatch tail instead of full tiles starting last
-__device__ __forceinline__ void d2_tile(const Dgemm2Args &g, int BM, int BN, int &m0, int &n0) {
-  const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8, i = blockIdx.x / 8;
-  const int cpre = xcd * q8 + min(xcd, r8);
-  if (!g.light_last) {
-    const int tile = cpre + i;
-    m0 = (tile % g.mt) * BM;
-    n0 = (tile / g.mt) * BN;
-    return;
-  }
-  const int mtf = g.M % BM ? g.mt - 1 : g.mt, ntf = g.N % BN ? g.nt - 1 : g.nt;
-  const int FT = mtf * ntf;
-  const int fx = FT / 8 + (xcd < FT % 8), fpre = xcd * (FT / 8) + min(xcd, FT % 8);
-  if (i < fx) {
-    const int t = fpre + i;
-    m0 = (t % mtf) * BM;
-    n0 = (t / mtf) * BN;
-    return;
-  }
-  const int l = (cpre - fpre) + (i - fx);   // edge tile: the m-partial row, then the n-partial column
-  const int nrow = g.mt > mtf ? g.nt : 0;
-  if (l < nrow) {
-    m0 = mtf * BM;
-    n0 = l * BN;
-  } else {
-    m0 = (l - nrow) * BM;
-    n0 = ntf * BN;
-  }
-}
 
 typedef __attribute__((address_space(3))) void d2_lds_t;
 typedef __attribute__((address_space(1))) void d2_gbl_t;
@@ -125,8 +89,12 @@ void k_dgemm2(const Dgemm2Args g) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int X = lane >> 4, bq = (lane >> 2) & 3, Y = lane & 3;
   const int wm = wv / CF::WGN, wn = wv % CF::WGN;
-  int m0, n0;
-  d2_tile(g, BM, BN, m0, n0);
+  // XCD-aware tile order: workgroups b, b + 8, ... share an XCD (and its L2);
+  // give each XCD a contiguous run of the m-fastest tile sequence, so the
+  // tiles reading one B column panel meet in one L2 (bijective for any count)
+  const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+  const int m0 = (tile % g.mt) * BM, n0 = (tile / g.mt) * BN;
 
   // one 1 KB piece (128 doubles of a row): one global_load_lds_dwordx4, or,
   // for an operand whose rows are not 16-byte aligned (odd leading

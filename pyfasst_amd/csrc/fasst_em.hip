@@ -27,7 +27,6 @@
 
 #include <cmath>
 #include <cstring>
-#include <type_traits>
 #include <mutex>
 
 namespace fasst {
@@ -2088,7 +2087,6 @@ struct TUArgs {
   // [J][KP][ntb] (k_tw_rowsum's; reduced in k_renorm_tail)
   const double *FW;
   double *FWHt, *hpart;
-  int batch;   // (FASST_TWU_BATCH) the element loops with all loads issued first
   const int *halt;
 };
 // TW *= (sum_chunks num / max(sum_chunks den, eps))^omega   (:1718-1726)
@@ -2108,62 +2106,6 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
     double tsum = 0.0;
     for (int kb = 0; kb < a.K[j]; kb += 64) {
       const int kn = min(64, a.K[j] - kb);
-      // batch (64 kn = 2048 or 4096 elements, E per thread): every split
-      // load of the thread's E elements in flight before the first use, and
-      // the TW read-modify-write likewise (the plain loops below make one
-      // memory round trip per element); same sums in the same order
-      auto batched = [&](auto e_tag) {
-        constexpr int E = decltype(e_tag)::value;
-        const int n = 64 * kn;
-        if (fr) {
-          double nu[E], de[E];
-#pragma unroll
-          for (int u = 0; u < E; ++u) nu[u] = de[u] = 0.0;
-          for (int c = 0; c < a.nsplit; ++c)
-#pragma unroll
-            for (int u = 0; u < E; ++u) {
-              const int idx = threadIdx.x + 256 * u, tl = idx / kn, kl = idx % kn;
-              const size_t o = (((size_t)c * a.J + j) * a.Tp + min(t0 + tl, a.T - 1)) * a.KP + kb + kl;
-              nu[u] += a.tnum[o];
-              de[u] += a.tden[o];
-            }
-#pragma unroll
-          for (int u = 0; u < E; ++u) {
-            const int idx = threadIdx.x + 256 * u, tl = idx / kn, kl = idx % kn;
-            const double ratio = nu[u] / fmax(de[u], kEps);
-            s_r[kl][tl] = t0 + tl < a.T ? (a.omega == 1.0 ? ratio : pow(ratio, a.omega)) : 1.0;
-          }
-        }
-        __syncthreads();
-        double x[E];
-#pragma unroll
-        for (int u = 0; u < E; ++u) {
-          const int idx = threadIdx.x + 256 * u, kl = idx / 64, tl = idx % 64;
-          x[u] = a.TW[((size_t)j * a.KP + kb + kl) * a.Tp + min(t0 + tl, a.T - 1)];
-        }
-#pragma unroll
-        for (int u = 0; u < E; ++u) {
-          const int idx = threadIdx.x + 256 * u, kl = idx / 64, tl = idx % 64, t = t0 + tl, k = kb + kl;
-          if (t < a.T) {
-            double y = x[u];
-            if (fr && k >= a.kb0[j] && k < a.kb1[j]) y *= s_r[kl][tl];
-            y *= w2[k];
-            a.TW[((size_t)j * a.KP + k) * a.Tp + t] = y;
-            tsum += y;
-            if (prep) s_y[k * 64 + tl] = y;
-          }
-        }
-        __syncthreads();
-        (void)n;
-      };
-      if (a.batch && kn == 32) {
-        batched(std::integral_constant<int, 8>{});
-        continue;
-      }
-      if (a.batch && kn == 64) {
-        batched(std::integral_constant<int, 16>{});
-        continue;
-      }
       if (fr)
         for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
           const int tl = idx / kn, kl = idx % kn, t = t0 + tl;
@@ -3968,7 +3910,6 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   u.convm = c->convm;
   for (int j = 0; j <= kMaxJ; ++j) u.roff[j] = j <= J ? c->roff[j] : c->R;
   tu.scal = tail ? c->rscal.p : nullptr;
-  tu.batch = c->twub;
   tu.tpart = c->rtpart2.p;
   tu.ntb = c->ntb;
   // the next iteration's FWHt / TW row sums formed here too (KP <= 64)
@@ -4273,7 +4214,6 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v);
   if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
   if (const char *v = getenv("FASST_TWL")) c->twl = atoi(v);
-  if (const char *v = getenv("FASST_TWU_BATCH")) c->twub = atoi(v);
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||

@@ -167,10 +167,6 @@ int dgemm2(hipStream_t s, int M, int N, int K, const double *A, int lda, const d
   g.M = M;
   g.N = N;
   g.K = K;
-  {
-    const char *e = getenv("FASST_D2_ORDER");
-    g.light_last = e && atoi(e) > 0;
-  }
   const bool a16 = lda % 2 == 0 && ((uintptr_t)A & 15) == 0;
   const bool b16 = ldb % 2 == 0 && ((uintptr_t)B & 15) == 0;
   // raw-buffer LDS-DMA pieces (operands within 2 GB: 32-bit byte offsets);

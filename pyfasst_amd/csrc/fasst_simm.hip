@@ -989,7 +989,6 @@ struct simm_ctx {
   // fasst_dgemm2.h), 2 = the generic k_gemm (A/B and parity reference);
   // both parity-tested against the oracle
   int gemm_kind = 0;
-  int hmt_kc = 32;   // k_simm_xy_hmt frames per staged chunk (FASST_HMT_KC=16: A/B)
   int Fp = 0, NF0p = 0;   // even (16-byte) row pitches of the WF0 copies below
   int F = 0, N = 0, NF0 = 0, P = 0, K = 0, R = 0, stereo = 1;
   int nchunk_h = 1, fchunk_h = 1, nb_alpha = 1;
@@ -1208,10 +1207,8 @@ int xy_hmt(simm_ctx *c, double *const *dst) {
   kdispatch(c->K, [&](auto km) {
     constexpr int KM = decltype(km)::value;
     if (c->stereo)
-      if (v16 && c->hmt_kc == 16)
+      if (v16)   // (16-frame chunks: the 32-frame form spilled, 0.672 -> 0.646 ms at C5)
         k_simm_xy_hmt<true, KM, true, 16><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
-      else if (v16)
-        k_simm_xy_hmt<true, KM, true><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
       else
         k_simm_xy_hmt<true, KM><<<grid, 256, 0, c->stream>>>(p, c->HM.p, c->gwork.p, slab, R, sp.kchunk);
     else
@@ -1465,7 +1462,6 @@ int simm_create(int device, int F, int N, int NF0, int P, int K, int R, int ster
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) st = FASST_ERR_DEVICE;
   if (const char *v = getenv("FASST_SIMM_GEMM")) c->gemm_kind = atoi(v) == 2 ? 2 : 0;
-  if (const char *v = getenv("FASST_HMT_KC")) c->hmt_kc = atoi(v) == 16 ? 16 : 32;
   c->Fp = (F + 15) / 16 * 16;
   c->NF0p = (NF0 + 15) / 16 * 16;
   size_t gw = 0;
