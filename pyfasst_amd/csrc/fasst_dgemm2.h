@@ -10,7 +10,10 @@
 //   wait (counted vmcnt) for chunk c -> s_barrier -> issue the loads of chunk
 //   c + NS - 1 into the buffer chunk c - 1 left -> compute chunk c.
 // Block = 256 threads as 2 x 2 waves, block tile 128 x 128, wave tile 64 x 64.
-// The products run on v_mfma_f64_4x4x4_4b: lane (X, b, Y) of one instruction
+// Two MFMA forms (D2Cfg::MF).  The product shape (D2Prod, two waves per SIMD)
+// runs v_mfma_f64_16x16x4f64, a wave's 64 x 64 tile as 4 x 4 four-double
+// accumulators fed by 8 LDS reads per k-step of 4 (16 MFMAs).  The odd-pitch
+// shape (D2Odd, one wave per SIMD) runs v_mfma_f64_4x4x4_4b: lane (X, b, Y) of one instruction
 // supplies A[m = Y][k = X] and B[k = X][n = Y] of block b and receives
 // D[m = X][n = Y]; the four blocks are 2 (m) x 2 (n) sub-blocks of an 8 x 8
 // patch, so one A register covers 8 rows, one B register 8 columns, and a
@@ -51,7 +54,10 @@ struct D2Cfg {
 // row loads; and the one for operands loaded in 4-byte pieces (odd leading
 // dimension), where the two-stage shape drained its loads every chunk
 // (8 vs 42-46 TF at the C5 sizes, profiles/r3_ubench_dgemm3.txt)
-using D2Prod = D2Cfg<2, 16, 2, 2, 2>;
+// (the product shape on 16x16x4 since round 5: C5 8.56 -> 8.46 ms per iteration
+// with the raw-buffer pieces, profiles/r5_ab_round5b.txt; the 4x4x4_4b form was
+// ahead before them, profiles/r3_ubench_dgemm3.txt)
+using D2Prod = D2Cfg<2, 16, 2, 2, 2, 1>;
 using D2Odd = D2Cfg<4, 8, 4, 2, 1>;
 
 struct Dgemm2Args {
