@@ -110,6 +110,27 @@ __global__ __launch_bounds__(256) void k_w_from_fb(const double *__restrict__ FB
     const int fl = idx / KP, q = idx % KP;
     s_fb[fl * (KP + 1) + q] = FB[((size_t)j * Fp + f0 + fl) * KP + q];
   }
+  if constexpr (fwg) {
+    // KP = 128 on the matrix cores: D[k][f] = sum_q FW[q][k] FB[f][q] per
+    // 16 x 16 tile (16x16x4: A = FW^T rows from L2, B = the FB tile in LDS),
+    // wave w forming the k tiles w, w + 4, ...; lane (fl, tq) then holds
+    // W[k = 16 kc + tq + 4 i][f0 + fl] (128-byte Wkf row pieces)
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
+    for (int kc = wv; kc < KP / 16; kc += 4) {
+      d4 d = d4{0.0, 0.0, 0.0, 0.0};
+      for (int q0 = 0; q0 < KP; q0 += 4)
+        d = __builtin_amdgcn_mfma_f64_16x16x4f64(fw[(size_t)(q0 + tq) * KP + 16 * kc + fl],
+                                                 s_fb[fl * (KP + 1) + q0 + tq], d, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 16 * kc + tq + 4 * i;
+        Wkf[((size_t)j * KP + k) * Fp + f0 + fl] = d[i];
+        if (Wfk) Wfk[((size_t)j * Fp + f0 + fl) * KP + k] = d[i];
+      }
+    }
+    return;
+  }
   if (!fwg)
     for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
       s_fw[idx] = FW[(size_t)j * KP * KP + idx];
@@ -139,7 +160,7 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
   // J = 8, K = 128)
   constexpr bool fwg = FWG;
   double *s_fw = s_f;                                  // [QH][KP] (q-major, transposed)
-  double *s_tw = s_f + (fwg ? 64 * KP : KP * KP);      // [KP][64]
+  double *s_tw = s_f + (fwg ? 16 * KP : KP * KP);      // [KP][64]
   const int j = blockIdx.y, t0 = blockIdx.x * 64;
   const int tn = min(64, Tp - t0);
   for (int idx = threadIdx.x; idx < KP * 64; idx += blockDim.x) {
@@ -147,33 +168,40 @@ __global__ __launch_bounds__(256) void k_fwh_t(const double *__restrict__ FW,
     s_tw[idx] = tl < tn ? TW[((size_t)j * KP + q) * Tp + t0 + tl] : 0.0;
   }
   if constexpr (fwg) {
-    constexpr int KPG = 128, NO = 64 * KPG / 256;   // outputs per thread
-    double acc[NO];
+    // KP = 128 on the matrix cores: wave w forms frames 16 w .. 16 w + 15,
+    // D[k][t] = sum_q FW[k][q] TW[q][t] per 16 x 16 tile (16x16x4: A = FW
+    // through LDS transposed, QB rows q at a time; B = the TW tile); lane
+    // (fl, tq) then holds FWHt[t0 + 16 w + fl][16 kc + tq + 4 i]
+    constexpr int KPG = 128, QB = 16;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
+    d4 d[KPG / 16];
 #pragma unroll
-    for (int m = 0; m < NO; ++m) acc[m] = 0.0;
-    for (int h = 0; h < 2; ++h) {
-      __syncthreads();   // (h = 1: the first half's reads are done)
-      for (int idx = threadIdx.x; idx < 64 * KPG; idx += blockDim.x) {
-        const int k = idx / 64, ql = idx % 64;  // coalesced over q in FW's rows
-        s_fw[ql * KPG + k] = FW[((size_t)j * KPG + k) * KPG + 64 * h + ql];
+    for (int kc = 0; kc < KPG / 16; ++kc) d[kc] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int qb = 0; qb < KPG; qb += QB) {
+      __syncthreads();   // (qb > 0: the previous chunk's reads are done)
+      for (int idx = threadIdx.x; idx < QB * KPG; idx += blockDim.x) {
+        const int k = idx / QB, q = idx % QB;   // (coalesced over q in FW's rows)
+        s_fw[q * KPG + k] = FW[((size_t)j * KPG + k) * KPG + qb + q];
       }
       __syncthreads();
 #pragma unroll
-      for (int m = 0; m < NO; ++m) {
-        const int idx = threadIdx.x + 256 * m, tl = idx / KPG, k = idx % KPG;
-        double s = 0.0;
-        for (int ql = 0; ql < 64; ++ql) s += s_fw[ql * KPG + k] * s_tw[(64 * h + ql) * 64 + tl];
-        acc[m] += s;
-      }
-    }
+      for (int kc = 0; kc < KPG / 16; ++kc)
 #pragma unroll
-    for (int m = 0; m < NO; ++m) {
-      const int idx = threadIdx.x + 256 * m, tl = idx / KPG, k = idx % KPG;
-      if (tl < tn) {
-        FWHt[((size_t)j * Tp + t0 + tl) * KPG + k] = acc[m];
-        if (TWt) TWt[((size_t)j * Tp + t0 + tl) * KPG + k] = s_tw[k * 64 + tl];
-      }
+        for (int q0 = 0; q0 < QB; q0 += 4)
+          d[kc] = __builtin_amdgcn_mfma_f64_16x16x4f64(s_fw[(q0 + tq) * KPG + 16 * kc + fl],
+                                                       s_tw[(qb + q0 + tq) * 64 + 16 * wv + fl], d[kc], 0, 0,
+                                                       0);
     }
+    const int tl = 16 * wv + fl;
+    if (tl < tn)
+#pragma unroll
+      for (int kc = 0; kc < KPG / 16; ++kc)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 16 * kc + tq + 4 * i;
+          FWHt[((size_t)j * Tp + t0 + tl) * KPG + k] = d[kc][i];
+          if (TWt) TWt[((size_t)j * Tp + t0 + tl) * KPG + k] = s_tw[k * 64 + tl];
+        }
     return;
   }
   for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x) {
@@ -1463,14 +1491,15 @@ __device__ double block_sum(double x, double *s);
 template <bool FWG>
 __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   HALT_GUARD(a.halt);
-  // LDS: FW [KP][KP] | FB rows [16][KP] | den [KP] | W_new rows [16][KP + 1]
+  // LDS: FW [KP][KP] | FB rows [16][PB] | den [KP] | W_new rows [16][KP + 1]
   extern __shared__ __attribute__((aligned(16))) double s_fw[];
   const int f0 = blockIdx.x * 16, j = blockIdx.y;
   const int KP = a.KP;
   constexpr bool fwg = FWG;   // FW read from L2 (its [KP][KP] copy would not fit)
+  const int PB = fwg ? KP + 1 : KP;   // (odd pitch: the MFMA B reads of 16 rows)
   const double *fw = fwg ? a.FW + (size_t)j * KP * KP : s_fw;
   double *s_fb = s_fw + (fwg ? 0 : KP * KP);
-  double *s_den = s_fb + 16 * KP;
+  double *s_den = s_fb + 16 * PB;
   double *s_wn = s_den + KP;
   if (!fwg)
     for (int idx = threadIdx.x; idx < KP * KP; idx += blockDim.x)
@@ -1498,17 +1527,35 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
       fb *= a.omega == 1.0 ? ratio : pow(ratio, a.omega);
       a.FB[o] = fb;
     }
-    s_fb[idx] = fb;
+    s_fb[fl * PB + k] = fb;
   }
   __syncthreads();
   // W_new = FB . FW: [f][k] rows written coalesced over k here, the [k][f]
   // layout from the LDS copy below (coalesced over the 16 bins)
-  for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
-    const int fl = idx / KP, k = idx % KP, f = f0 + fl;
-    double s = 0.0;
-    for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * fw[q * KP + k];
-    a.Wfk_new[((size_t)j * a.Fp + f) * KP + k] = s;
-    s_wn[fl * (KP + 1) + k] = s;
+  if constexpr (fwg) {
+    // KP = 128 on the matrix cores (as k_w_from_fb): D[k][f] = sum_q FW[q][k]
+    // FB[f][q] per 16 x 16 tile, wave w forming the k tiles w, w + 4, ...
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fl = lane & 15, tq = lane >> 4;
+    for (int kc = wv; kc < KP / 16; kc += 4) {
+      d4 d = d4{0.0, 0.0, 0.0, 0.0};
+      for (int q0 = 0; q0 < KP; q0 += 4)
+        d = mfma4(fw[(size_t)(q0 + tq) * KP + 16 * kc + fl], s_fb[fl * PB + q0 + tq], d);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_wn[fl * (KP + 1) + 16 * kc + tq + 4 * i] = d[i];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+      const int fl = idx / KP, k = idx % KP;
+      a.Wfk_new[((size_t)j * a.Fp + f0 + fl) * KP + k] = s_wn[fl * (KP + 1) + k];
+    }
+  } else {
+    for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
+      const int fl = idx / KP, k = idx % KP, f = f0 + fl;
+      double s = 0.0;
+      for (int q = 0; q < KP; ++q) s += s_fb[fl * KP + q] * fw[q * KP + k];
+      a.Wfk_new[((size_t)j * a.Fp + f) * KP + k] = s;
+      s_wn[fl * (KP + 1) + k] = s;
+    }
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < 16 * KP; idx += blockDim.x) {
@@ -1521,7 +1568,7 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
   const int nb = min(16, a.F - f0);
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
     double m = -INFINITY;
-    for (int fl = 0; fl < nb; ++fl) m = fmax(m, s_fb[fl * KP + k]);
+    for (int fl = 0; fl < nb; ++fl) m = fmax(m, s_fb[fl * PB + k]);
     a.pmax[((size_t)j * gridDim.x + blockIdx.x) * KP + k] = m;
   }
   if (a.convm >> j & 1u) {
@@ -3666,7 +3713,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     FASST_LAUNCH_CHECK();
     if (int st = check_tail_args(c, u, tu)) return st;
     (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
-                  fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
+                  fw_lds(c, 16 * (c->KP + 1) + c->KP + 16 * (c->KP + 1)),
                   c->stream>>>(u);
     FASST_LAUNCH_CHECK();
     bool any_fw = false;
@@ -3809,11 +3856,11 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
   prof_begin(c, KFWH, side);
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-  if (c->KP > 64)   // FW halves + TW tile: 128 KB of LDS
+  if (c->KP > 64)   // 16-row FW chunk + TW tile: 80 KB of LDS (two blocks per CU)
     FASST_HIP(hipFuncSetAttribute((const void *)k_fwh_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((64 + 64) * c->KP * sizeof(double))));
+                                  (int)((16 + 64) * c->KP * sizeof(double))));
   (c->KP > 64 ? k_fwh_t<true> : k_fwh_t<false>)<<<dim3((c->Tp + 63) / 64, J), 256,
-            c->KP > 64 ? (64 + 64) * c->KP * sizeof(double) : fw_lds(c, c->KP * 64),
+            c->KP > 64 ? (16 + 64) * c->KP * sizeof(double) : fw_lds(c, c->KP * 64),
             side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
                     c->halt);
   prof_end(c, KFWH, side);
@@ -3940,7 +3987,7 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   if (int st = check_tail_args(c, u, tu)) return st;
   prof_begin(c, KFBU);
   (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
-                fw_lds(c, 16 * c->KP + c->KP + 16 * (c->KP + 1)),
+                fw_lds(c, 16 * (c->KP + 1) + c->KP + 16 * (c->KP + 1)),
                 c->stream>>>(u);
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
