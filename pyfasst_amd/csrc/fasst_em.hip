@@ -3006,6 +3006,9 @@ static int estep_occupancy(const fasst_ctx *c);
 static int contract_occupancy(const fasst_ctx *c, bool fb);
 static int twl_occupancy(const fasst_ctx *c, int *units);
 static int tpw_of(const fasst_ctx *c);
+// bins per block of the FW update's f-contraction (k_fw_reduce holds three
+// [fpc][KP] tiles in LDS: 96 KB at KP = 128 with 32 bins)
+static int fw_fpc(const fasst_ctx *c) { return c->KP > 64 ? 32 : kFwFpc; }
 // dynamic LDS of the kernels that stage FW ([KP][KP] when KP <= 64) next to
 // `rest` doubles
 static size_t fw_lds(const fasst_ctx *c, int rest) {
@@ -3160,8 +3163,8 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   // FW update (free FW only, allocated with the model so set_spectral may switch it on)
   ALLOC(gden, (size_t)c->nchunk_b * J * Fp * KP);
   ALLOC(TWt, (size_t)J * Tp * KP);
-  ALLOC(pnum, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
-  ALLOC(pden, (size_t)((c->F + kFwFpc - 1) / kFwFpc) * J * KP * KP);
+  ALLOC(pnum, (size_t)((c->F + fw_fpc(c) - 1) / fw_fpc(c)) * J * KP * KP);
+  ALLOC(pden, (size_t)((c->F + fw_fpc(c) - 1) / fw_fpc(c)) * J * KP * KP);
   ALLOC(tnum, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(tden, (size_t)c->nsplit_t * J * Tp * KP);
   ALLOC(rss, conv ? 0 : (size_t)Fp * R * R);
@@ -3472,6 +3475,12 @@ template <int NKC>
 constexpr int tpw_for() { return NKC > 4 ? 1 : kTPW; }
 static int tpw_of(const fasst_ctx *c) { return c->KP > 64 ? 1 : kTPW; }
 
+static void launch_fw_reduce(fasst_ctx *c, const FWArgs &w) {
+  const size_t lds = (size_t)3 * w.fpc * c->KP * sizeof(double);
+  (void)hipFuncSetAttribute((const void *)k_fw_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  k_fw_reduce<<<dim3(w.nfc, c->J), 256, lds, c->stream>>>(w);
+}
+
 // k_tw_contract_lds shapes (NW waves per block, TPW frame tiles per wave, NS
 // stages); c->twl picks one (0: the register-operand k_tw_contract)
 template <class CF>
@@ -3692,7 +3701,7 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
     }
     const dim3 gp(c->nft, J, c->nchunk_b);
     const dim3 gb((c->nft + kFPW - 1) / kFPW, J, c->nchunk_b);
-    const dim3 gt((c->ntt + kTPW - 1) / kTPW, J, c->nsplit_t);
+    const dim3 gt((c->ntt + tpw_of(c) - 1) / tpw_of(c), J, c->nsplit_t);
     switch (nkc) {
       case 1:
         if (lam) k_multi_prep<1, true><<<gp, 64, 0, c->stream>>>(mp);
@@ -3704,10 +3713,15 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
         else k_multi_prep<2><<<gp, 64, 0, c->stream>>>(mp);
         k_fb_contract<2, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
         break;
-      default:
+      case 4:
         if (lam) k_multi_prep<4, true><<<gp, 64, 0, c->stream>>>(mp);
         else k_multi_prep<4><<<gp, 64, 0, c->stream>>>(mp);
         k_fb_contract<4, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
+        break;
+      default:   // KP = 128
+        if (lam) k_multi_prep<8, true><<<gp, 64, 0, c->stream>>>(mp);
+        else k_multi_prep<8><<<gp, 64, 0, c->stream>>>(mp);
+        k_fb_contract<8, kFPW, true><<<gb, 64, 0, c->stream>>>(bb);
         break;
     }
     FASST_LAUNCH_CHECK();
@@ -3742,8 +3756,8 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
       w.ntt = c->ntt;
       w.tpc = c->tpc_b;
       w.nchunk = c->nchunk_b;
-      w.fpc = kFwFpc;
-      w.nfc = (c->F + kFwFpc - 1) / kFwFpc;
+      w.fpc = fw_fpc(c);
+      w.nfc = (c->F + w.fpc - 1) / w.fpc;
       w.omega = omega;
       w.halt = c->halt;
       w.cp = mp.rcp;
@@ -3765,12 +3779,16 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
           if (lam) k_fw_contract<2, true, true><<<gc, 64, 0, c->stream>>>(w);
           else k_fw_contract<2, true><<<gc, 64, 0, c->stream>>>(w);
           break;
-        default:
+        case 4:
           if (lam) k_fw_contract<4, true, true><<<gc, 64, 0, c->stream>>>(w);
           else k_fw_contract<4, true><<<gc, 64, 0, c->stream>>>(w);
           break;
+        default:
+          if (lam) k_fw_contract<8, true, true><<<gc, 64, 0, c->stream>>>(w);
+          else k_fw_contract<8, true><<<gc, 64, 0, c->stream>>>(w);
+          break;
       }
-      k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
+      launch_fw_reduce(c, w);
       k_fw_final<<<J, 256, 0, c->stream>>>(w);
       (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
                     c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
@@ -3786,9 +3804,13 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
         if (lam) k_tw_contract<2, kTPW, true, true><<<gt, 64, 0, c->stream>>>(t);
         else k_tw_contract<2, kTPW, true><<<gt, 64, 0, c->stream>>>(t);
         break;
-      default:
+      case 4:
         if (lam) k_tw_contract<4, kTPW, true, true><<<gt, 64, 0, c->stream>>>(t);
         else k_tw_contract<4, kTPW, true><<<gt, 64, 0, c->stream>>>(t);
+        break;
+      default:   // (one frame tile per wave at KP = 128)
+        if (lam) k_tw_contract<8, 1, true, true><<<gt, 64, 0, c->stream>>>(t);
+        else k_tw_contract<8, 1, true><<<gt, 64, 0, c->stream>>>(t);
         break;
     }
     FASST_LAUNCH_CHECK();
@@ -3814,9 +3836,13 @@ static int multi_step(fasst_ctx *c, double omega, int b, int only_j) {
           if (lam) k_tw_contract<2, kTPW, true, true, true><<<gt, 64, 0, c->stream>>>(t2);
           else k_tw_contract<2, kTPW, true, false, true><<<gt, 64, 0, c->stream>>>(t2);
           break;
-        default:
+        case 4:
           if (lam) k_tw_contract<4, kTPW, true, true, true><<<gt, 64, 0, c->stream>>>(t2);
           else k_tw_contract<4, kTPW, true, false, true><<<gt, 64, 0, c->stream>>>(t2);
+          break;
+        default:
+          if (lam) k_tw_contract<8, 1, true, true, true><<<gt, 64, 0, c->stream>>>(t2);
+          else k_tw_contract<8, 1, true, false, true><<<gt, 64, 0, c->stream>>>(t2);
           break;
       }
       k_tb_tb_upd<<<dim3((c->T + 63) / 64, J), 64,
@@ -4017,8 +4043,8 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
     w.ntt = c->ntt;
     w.tpc = c->tpc_b;
     w.nchunk = c->nchunk_b;
-    w.fpc = kFwFpc;
-    w.nfc = (c->F + kFwFpc - 1) / kFwFpc;
+    w.fpc = fw_fpc(c);
+    w.nfc = (c->F + w.fpc - 1) / w.fpc;
     w.omega = omega;
     w.halt = c->halt;
     for (int j = 0; j < kMaxJ; ++j) {
@@ -4032,9 +4058,10 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
     switch (nkc) {
       case 1: k_fw_contract<1><<<gc, 64, 0, c->stream>>>(w); break;
       case 2: k_fw_contract<2><<<gc, 64, 0, c->stream>>>(w); break;
-      default: k_fw_contract<4><<<gc, 64, 0, c->stream>>>(w); break;
+      case 4: k_fw_contract<4><<<gc, 64, 0, c->stream>>>(w); break;
+      default: k_fw_contract<8><<<gc, 64, 0, c->stream>>>(w); break;
     }
-    k_fw_reduce<<<dim3(w.nfc, J), 256, (size_t)3 * kFwFpc * c->KP * sizeof(double), c->stream>>>(w);
+    launch_fw_reduce(c, w);
     k_fw_final<<<J, 256, 0, c->stream>>>(w);
     (c->KP > 64 ? k_w_from_fb<true> : k_w_from_fb<false>)<<<dim3(c->nft, J), 256, fw_lds(c, 16 * (c->KP + 1)),
                   c->stream>>>(c->FB.p, c->FW.p, c->Wkf_new.p, c->Wfk_new.p, J, c->Fp, c->KP,
@@ -4076,16 +4103,6 @@ __global__ void k_rho_from_hatw(const double *__restrict__ hw, const double *__r
 static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, double omega,
                          int iter) {
   const int J = c->J;
-  if (c->KP > 64) {
-    // K > 64 per source: the single-component path (the constructors' models)
-    bool any_fw = false;
-    for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-    if (c->multi || any_fw) {
-      set_error("K > 64 NMF components on a spatial component is on the HIP path with one "
-                "spectral component each, fixed FW, lambdaCorr = 0 and no time blobs");
-      return FASST_ERR_UNSUPPORTED;
-    }
-  }
   if (!c->conv) {
     // a free 'conv' component next to other components: the reference's conv
     // solve (audioModel.py:856-857) passes the full hat_Rss[f].T against the
@@ -4643,10 +4660,6 @@ int fasst_spectral_update(fasst_ctx *c, const double *hat_W, double omega) {
   int st = need_model(c, 0);
   if (st) return st;
   if (!hat_W) return FASST_ERR_SHAPE;
-  if (c->KP > 64 && c->multi) {
-    set_error("K > 64: the single-component spectral path only");
-    return FASST_ERR_UNSUPPORTED;
-  }
   DeviceGuard g(c->device);
   const size_t n = (size_t)c->J * c->F * c->T;
   DBuf<double> dh;

@@ -239,13 +239,54 @@ def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     assert rel(np.abs(S), np.abs(So)) < 1e-8
 
 
-def test_k_above_64_outside_single_component_path_fails_loudly():
-    """K > 64 runs the single-component path only (one spectral component per
-    spatial component, fixed FW): other structures raise instead of running."""
-    m, o, X = _c3_like(33, 40, 2, 70, 1, 1)
-    m.spec_comps[0]['factor'][0]['FW_frdm_prior'] = 'free'
+def test_k_above_128_fails_loudly():
+    """More than 128 NMF columns on one spatial component is outside the HIP
+    path: it raises instead of running (no CPU fallback)."""
     with pytest.raises(NotImplementedError):
+        m, o, X = _c3_like(33, 40, 2, 130, 1, 1)
         m.estim_param_a_post_model()
+
+
+@pytest.mark.parametrize("what", ["free_fw", "multi", "multi_free_fw", "lambda", "time_blobs"])
+def test_k_above_64_every_structure_vs_oracle(what):
+    """K > 64 (KP = 128: the NKC = 8 forms of k_multi_prep, the DEN FB
+    contraction, the FW contraction and the BLK / LAM / TBQ TW contractions,
+    k_fw_reduce on 32-bin chunks) on every structure, not only the
+    single-component path: free FW, several spectral components, free FW on
+    some of them, lambdaCorr, time blobs; against the oracle."""
+    m, o, X = _c3_like(65, 77, 2, 100, 1, 2)
+    tb = {}
+    for mod in (m, o):
+        if what in ("free_fw", "multi_free_fw"):
+            keys = [0] if what == "free_fw" else [0, 2]
+            if what == "multi_free_fw":
+                _split_spec(mod, {0: [40, 60], 1: [100]})
+            for k in keys:
+                fac = mod.spec_comps[k]['factor'][0]
+                n = fac['FW'].shape[0]
+                fac['FW'] = fac['FW'] + 0.2 * np.abs(np.random.RandomState(80 + k).randn(n, n))
+                fac['FW_frdm_prior'] = 'free'
+        elif what == "multi":
+            _split_spec(mod, {0: [40, 60], 1: [30, 70]}, ((3, 'FB'),))
+        elif what == "lambda":
+            mod.lambdaCorr = 0.3
+            _split_spec(mod, {0: [100], 1: [50, 50]})
+        else:
+            _split_spec(mod, {0: [40, 60], 1: [100]})
+            tb = {0: (6, 'free', 'free'), 1: (4, 'free', 'free'), 2: (3, 'fixed', 'free')}
+            _time_blobs(mod, tb)
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for k in sorted(o.spec_comps):
+        keys = ('FB', 'FW', 'TW', 'TB') if k in tb else ('FB', 'FW', 'TW')
+        for key in keys:
+            assert rel(m.spec_comps[k]['factor'][0][key], o.spec_comps[k]['factor'][0][key]) < 1e-8, \
+                (k, key)
+    for j in range(2):
+        assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+    groups = _spatial_groups(m)
+    assert rel(np.abs(m.separated_images(groups)), np.abs(o.separated_images(X, groups))) < 1e-8
 
 
 def test_fixed_components_vs_oracle():
