@@ -22,7 +22,7 @@ namespace fasst {
 #endif
 
 constexpr double kEps = 1e-10;  // audioModel.py:61, tools/signalTools.py:11
-constexpr int kMaxJ = 8;        // sources (spatial components)
+constexpr int kMaxJ = 16;       // sources (spatial components; > 8: the two-pass E-step)
 constexpr int kMaxR = 16;       // total spatial rank
 constexpr int kMaxKP = 128;     // padded NMF components (K > 64: one spectral
                                 // component per source, fixed FW, no lambdaCorr / TB)

@@ -32,6 +32,7 @@ struct fasst_ctx {
   // observation
   int F = 0, T = 0, Fp = 0, Tp = 0, nft = 0, ntt = 0;
   fasst::DBuf<double> cx;        // 4*Tp*Fp
+  fasst::DBuf<double> vgen, npgen, lgen;   // J > 8: the two-pass E-step's scratch planes
   bool cx_ready = false;          // an observation was written (set_cx / set_stft / set_audio)
   fasst::DBuf<double2> X;        // 2*Tp*Fp (resident STFT, optional)
   bool have_X = false;

@@ -994,6 +994,187 @@ void k_estep_mx(const EArgs a) {
     a.llpart[(a.ybase + bi.y) * a.nft + bi.x] = ((s_ll[0] + s_ll[1]) + s_ll[2]) + s_ll[3];
 }
 
+// ---------------------------------------------------------------- E-step, J > 8
+// More than 8 sources (up to kMaxJ): the statistics no longer fit the
+// single-pass kernel's registers (J (J + 1) / 2 pair and 8 J cross sums per
+// bin), so the E-step runs in two passes over a scratch copy of its point
+// quantities.  k_egen_point: one wave per 16 x 16 (bin, frame) tile, V_j on
+// 16x16x4 MFMA (the k_estep_mx / k_wiener tile), then per point Sigma_x, its
+// guarded inverse, the loglik term, P = Cx S, N = S Cx S - S and rho, with V_j,
+// N and P written to frame-major scratch planes.  k_egen_stats: one block per
+// (16-bin tile, frame chunk) sums the pair statistics V_j1 V_j2 N_c and the
+// cross statistics V_j P_c over its frames (tiles staged in LDS) into the
+// k_estep_mx partial layout, so k_mix reads it unchanged.
+struct GArgs {
+  double *V;     // [J][Tp][Fp]
+  double *NP;    // [12][Tp][Fp]: N0..N3, P0..P7
+  double *lw;    // [ntt][nft] per-wave loglik partials
+  int J;
+};
+
+__global__ __launch_bounds__(64) void k_egen_point(const EArgs a, const GArgs g) {
+  HALT_GUARD(a.halt);
+  const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
+  const int tt = blockIdx.x, ft = blockIdx.y, t0 = tt * 16, f0 = ft * 16, f = f0 + fl;
+  const int J = g.J, nks = a.KP >> 2;
+  __shared__ double s_c[kMaxJ][4][16];   // Sigma_x coefficients of the tile's bins
+  __shared__ double s_irk[kMaxJ];
+  if (tq == 0)
+    for (int j = 0; j < J; ++j) {
+      double al = 0, be = 0, gr = 0, gi = 0;
+      for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
+        const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + f];
+        const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + f];
+        al += a0.x * a0.x + a0.y * a0.y;
+        be += a1.x * a1.x + a1.y * a1.y;
+        gr += a0.x * a1.x + a0.y * a1.y;
+        gi += a0.y * a1.x - a0.x * a1.y;
+      }
+      s_c[j][0][fl] = al;
+      s_c[j][1][fl] = be;
+      s_c[j][2][fl] = gr;
+      s_c[j][3][fl] = gi;
+    }
+  if (lane < J) s_irk[lane] = 1.0 / (double)(a.roff[lane + 1] - a.roff[lane]);
+  __syncthreads();
+  d4 v[kMaxJ];
+#pragma unroll
+  for (int j = 0; j < kMaxJ; ++j) {
+    v[j] = d4{0.0, 0.0, 0.0, 0.0};
+    if (j < J) {   // (wave-uniform)
+      const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
+      const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
+      for (int s = 0; s < nks; ++s) v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v[j]);
+    }
+  }
+  const size_t plane = (size_t)a.Tp * a.Fp;
+  const double psd = a.psd[f];
+  double ll = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + tq + 4 * i;
+    const size_t o = (size_t)t * a.Fp + f;
+    const double x00 = a.cx00[o], x11 = a.cx11[o], xr = a.cxr[o], xi = a.cxi[o];
+    double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j)
+      if (j < J) {
+        d0 += s_c[j][0][fl] * v[j][i];
+        d1 += s_c[j][1][fl] * v[j][i];
+        ore += s_c[j][2][fl] * v[j][i];
+        oim += s_c[j][3][fl] * v[j][i];
+      }
+    // inv_herm_mat_2d (signalTools.py:177-194)
+    double det = d0 * d1 - (ore * ore + oim * oim);
+    const double dg = det + kEps;
+    det = (dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0)) * fmax(fabs(det), kEps);
+    const double rdet = rcp_nr(det);
+    const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
+    if (f < a.F && t < a.T) ll += log(det * M_PI) + (i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi));
+    double P[8], N[4];
+    P[0] = x00 * i0 + xr * ior + xi * ioi;
+    P[1] = xi * ior - xr * ioi;
+    P[2] = x00 * ior + xr * i1;
+    P[3] = x00 * ioi + xi * i1;
+    P[4] = xr * i0 + x11 * ior;
+    P[5] = -xi * i0 - x11 * ioi;
+    P[6] = xr * ior + xi * ioi + x11 * i1;
+    P[7] = xr * ioi - xi * ior;
+    N[0] = P[0] * i0 + (P[4] * ior - P[5] * ioi) - i0;
+    N[1] = (P[2] * ior + P[3] * ioi) + P[6] * i1 - i1;
+    N[2] = P[0] * ior + P[1] * ioi + P[4] * i1 - ior;
+    N[3] = P[0] * ioi - P[1] * ior - P[5] * i1 - ioi;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) g.NP[c * plane + o] = N[c];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) g.NP[(4 + c) * plane + o] = P[c];
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j)
+      if (j < J) {
+        const double Vj = v[j][i];
+        g.V[j * plane + o] = Vj;
+        // rho = |V^2 q + V| / max(V, eps) = |V q + 1| min(V / eps, 1), q the
+        // rank-merged quadratic form (as k_estep_mx)
+        const double q = ((s_c[j][0][fl] * N[0] + s_c[j][1][fl] * N[1]) +
+                          2.0 * (s_c[j][2][fl] * N[2] + s_c[j][3][fl] * N[3])) * s_irk[j];
+        a.hatW[j * plane + o] = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
+      }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) ll += __shfl_xor(ll, m, 64);
+  if (lane == 0) g.lw[(size_t)tt * a.nft + ft] = ll;
+}
+
+__global__ __launch_bounds__(256) void k_egen_stats(const EArgs a, const GArgs g) {
+  HALT_GUARD(a.halt);
+  constexpr int MU = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 15) / 16;   // sums per thread
+  const int J = g.J, NP = J * (J + 1) / 2, NACC = 4 * NP + 8 * J;
+  const int tid = threadIdx.x, b = tid & 15, ug = tid >> 4;
+  const int ft = blockIdx.x, f0 = ft * 16, y = blockIdx.y;
+  extern __shared__ __attribute__((aligned(16))) double s_t[];   // [J + 12][16 frames][16 bins]
+  __shared__ unsigned char s_a[4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ][3];
+  for (int u = tid; u < NACC; u += 256) {
+    int r0, r1, r2;
+    if (u < 4 * NP) {   // pair p = (lo, hi) canonical (lo major), component n
+      int p = u >> 2, lo = 0;
+      while (p >= J - lo) {
+        p -= J - lo;
+        ++lo;
+      }
+      r0 = lo;
+      r1 = lo + p;
+      r2 = J + (u & 3);          // N_n
+    } else {
+      const int q = u - 4 * NP;
+      r0 = q >> 3;
+      r1 = -1;
+      r2 = J + 4 + (q & 7);      // P_c
+    }
+    s_a[u][0] = (unsigned char)r0;
+    s_a[u][1] = (unsigned char)(r1 < 0 ? 255 : r1);
+    s_a[u][2] = (unsigned char)r2;
+  }
+  double acc[MU];
+#pragma unroll
+  for (int m = 0; m < MU; ++m) acc[m] = 0.0;
+  const size_t plane = (size_t)a.Tp * a.Fp;
+  const int tb = a.tbase + y * a.tpc, te = min(tb + a.tpc, a.ntt);
+  const int nr = J + 12;
+  for (int tt = tb; tt < te; ++tt) {
+    __syncthreads();   // (the previous tile's reads; the first: s_a)
+    for (int idx = tid; idx < nr * 256; idx += 256) {
+      const int r = idx >> 8, e = idx & 255, tl = e >> 4, fl = e & 15;
+      const size_t o = (size_t)(tt * 16 + tl) * a.Fp + f0 + fl;
+      s_t[idx] = r < J ? g.V[r * plane + o] : g.NP[(r - J) * plane + o];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MU; ++m) {
+      const int u = ug + 16 * m;
+      if (u < NACC) {
+        const int r0 = s_a[u][0], r1 = s_a[u][1], r2 = s_a[u][2];
+        double x = acc[m];
+        for (int tl = 0; tl < 16; ++tl) {
+          const double w = r1 == 255 ? s_t[(r0 * 16 + tl) * 16 + b]
+                                     : s_t[(r0 * 16 + tl) * 16 + b] * s_t[(r1 * 16 + tl) * 16 + b];
+          x = fma(w, s_t[(r2 * 16 + tl) * 16 + b], x);
+        }
+        acc[m] = x;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MU; ++m) {
+    const int u = ug + 16 * m;
+    if (u < NACC) a.part[((size_t)(a.ybase + y) * a.Fp + f0 + b) * NACC + u] = acc[m];
+  }
+  if (tid == 0) {   // the chunk's loglik, its tiles in order
+    double l = 0.0;
+    for (int tt = tb; tt < te; ++tt) l += g.lw[(size_t)tt * a.nft + ft];
+    a.llpart[(a.ybase + y) * a.nft + ft] = l;
+  }
+}
+
 // sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
 __global__ void k_tw_rowsum(const double *__restrict__ TW, double *__restrict__ hsum, int T,
                             int Tp, const int *halt) {
@@ -1084,6 +1265,9 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 // (:854-863) by LU with partial pivoting on |re|+|im| (LAPACK zgesv), the
 // matrix entries spread over the lanes; for 'inst' the per-bin statistics are
 // stored for k_mix_inst.
+// QM: statistics per lane, ceil(NACC / 64) (2 at J = 4; the J > 8 models
+// take the kMaxJ ceiling, the others stay at their own register count)
+template <int QM>
 __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   HALT_GUARD(a.halt);
   // LDS sized by this model's J, R, KP (mix_smem): with the kMaxJ / kMaxR /
@@ -1104,7 +1288,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   const int NP = J * (J + 1) / 2;
   {  // NACC = 72 > 64 lanes for J = 4: a lane sums up to 4 statistics, the
      // loads of all of them for 8 chunks in flight together (chunk order kept)
-    constexpr int kQ = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64;
+    constexpr int kQ = QM;
     double x[kQ] = {};
     const size_t cs = (size_t)a.Fp * NACC;
     const double *p0 = a.part + (size_t)f * NACC + lane;
@@ -1267,10 +1451,11 @@ __global__ void k_mix_inst(const IArgs a) {
   const int nu = a.nu, R = a.R;
   const int tid = threadIdx.x;
   const int nb = 2 * nu, nm = nu * nu;
-  if (tid < nb + nm) {
+  // (2 nu + nu^2 reaches 288 at nu = 16: more entries than threads)
+  for (int idx = tid; idx < nb + nm; idx += blockDim.x) {
     double s = 0.0;
-    if (tid < nb) {
-      const int c = tid / nu, u = tid % nu, ru = a.upd[u];
+    if (idx < nb) {
+      const int c = idx / nu, u = idx % nu, ru = a.upd[u];
       for (int f = 0; f < a.F; ++f) {
         double2 x = a.rxs[((size_t)f * 2 + c) * R + ru];
         for (int o = 0; o < a.no; ++o) {
@@ -1281,7 +1466,7 @@ __global__ void k_mix_inst(const IArgs a) {
       }
       s_b[u][c] = s / a.F;
     } else {
-      const int e = tid - nb, u1 = e / nu, u2 = e % nu;
+      const int e = idx - nb, u1 = e / nu, u2 = e % nu;
       for (int f = 0; f < a.F; ++f) s += a.rss[((size_t)f * R + a.upd[u1]) * R + a.upd[u2]].x;
       s_m[u1][u2] = s / a.F;
     }
@@ -3184,6 +3369,15 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(rtpart2, (size_t)kMaxSlot * c->ntb);
   ALLOC(Wkf_next, (size_t)J * KP * Fp);
   ALLOC(hpart, (size_t)J * KP * c->ntb);
+  if (J > 8) {   // the two-pass E-step's scratch: V_j, N, P planes and per-tile logliks
+    ALLOC(vgen, (size_t)J * Tp * Fp);
+    ALLOC(npgen, (size_t)12 * Tp * Fp);
+    ALLOC(lgen, (size_t)c->ntt * c->nft);
+  } else {
+    c->vgen.release();
+    c->npgen.release();
+    c->lgen.release();
+  }
   c->w_ready = c->prep_ready = 0;
 #undef ALLOC
   c->configured = 1;
@@ -4154,7 +4348,21 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.nft = c->nft;
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
   e.ybase = e.tbase = 0;
-  launch_estep(c, e, c->nchunk_e);
+  if (J > 8) {   // the two-pass E-step (k_egen_point / k_egen_stats)
+    GArgs gg{};
+    gg.V = c->vgen.p;
+    gg.NP = c->npgen.p;
+    gg.lw = c->lgen.p;
+    gg.J = J;
+    prof_begin(c, KESTEP);
+    k_egen_point<<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg);
+    const size_t lds = (size_t)(J + 12) * 256 * sizeof(double);
+    (void)hipFuncSetAttribute((const void *)k_egen_stats, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    k_egen_stats<<<dim3(c->nft, c->nchunk_e), 256, lds, c->stream>>>(e, gg);
+    prof_end(c, KESTEP);
+  } else {
+    launch_estep(c, e, c->nchunk_e);
+  }
   FASST_LAUNCH_CHECK();
   if (fork && !prep_ready) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
   const bool ft = fast_tail(c);
@@ -4193,7 +4401,16 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     for (int j = 0; j < J; ++j)
       for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
     prof_begin(c, KMIX);
-    k_mix<<<c->F, 64, mix_smem(J, c->R, c->KP, c->nacc), c->stream>>>(m);
+    {
+      const size_t ms = mix_smem(J, c->R, c->KP, c->nacc);
+      const int q = (c->nacc + 63) / 64;
+      if (q <= 2)
+        k_mix<2><<<c->F, 64, ms, c->stream>>>(m);
+      else if (q <= 4)   // (J <= 8: 4 J (J + 1) / 2 + 8 J <= 208)
+        k_mix<4><<<c->F, 64, ms, c->stream>>>(m);
+      else
+        k_mix<(4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64><<<c->F, 64, ms, c->stream>>>(m);
+    }
     prof_end(c, KMIX);
     FASST_LAUNCH_CHECK();
     if (!c->conv) {
@@ -4356,6 +4573,9 @@ int fasst_destroy(fasst_ctx *c) {
     c->rpe2.release();
     c->rtpart2.release();
     c->hpart.release();
+    c->vgen.release();
+    c->npgen.release();
+    c->lgen.release();
     c->Wkf_next.release();
     c->mplanes.release();
     c->bden.release();

@@ -284,6 +284,7 @@ struct WArgs {
   const double2 *X;  // [2][Tp][Fp]
   double2 *S;        // [J][2][Tp][Fp]
   int F, T, Fp, Tp, KP;
+  int nj;            // sources (the kMaxJ instantiation's runtime bound)
 };
 
 // one wave per 16x16 (frame, bin) tile; V^T from FP64 MFMA (V = W.H, no eps,
@@ -293,10 +294,13 @@ __global__ __launch_bounds__(64) void k_wiener(const WArgs a) {
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
   const int t0 = blockIdx.x * 16, f0 = blockIdx.y * 16, f = f0 + fl;
   const int nks = a.KP >> 2;
+  // (J = kMaxJ: J > 8 sources, the loops bounded by a.nj at run time)
+  const int JR = J == kMaxJ ? a.nj : J;
   d4 v[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     v[j] = d4{0.0, 0.0, 0.0, 0.0};
+    if (j >= JR) continue;
     const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
     const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
     for (int s = 0; s < nks; ++s) v[j] = mfma4b(tw[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v[j]);
@@ -304,6 +308,10 @@ __global__ __launch_bounds__(64) void k_wiener(const WArgs a) {
   double cal[J], cbe[J], cgr[J], cgi[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
+    if (j >= JR) {
+      cal[j] = cbe[j] = cgr[j] = cgi[j] = 0.0;
+      continue;
+    }
     cal[j] = a.coef[(size_t)(j * 4 + 0) * a.Fp + f];
     cbe[j] = a.coef[(size_t)(j * 4 + 1) * a.Fp + f];
     cgr[j] = a.coef[(size_t)(j * 4 + 2) * a.Fp + f];
@@ -333,6 +341,7 @@ __global__ __launch_bounds__(64) void k_wiener(const WArgs a) {
     const double2 x0 = a.X[o], x1 = a.X[plane + o];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
+      if (j >= JR) continue;
       const double vv = v[j][i];
       const double s0 = cal[j] * vv, s1 = cbe[j] * vv, sr = cgr[j] * vv, si = cgi[j] * vv;
       // WG00 = so conj(iso) + sd0 isd0 ; WG11 = conj(so conj(iso)) + sd1 isd1
@@ -502,6 +511,7 @@ static int launch_wiener(fasst_ctx *c, const double *coef, const double *dpsd, d
   w.Fp = c->Fp;
   w.Tp = c->Tp;
   w.KP = c->KP;
+  w.nj = c->J;
   switch (c->J) {
     case 1: k_wiener<1><<<grid, 64, 0, c->stream>>>(w); break;
     case 2: k_wiener<2><<<grid, 64, 0, c->stream>>>(w); break;
@@ -510,7 +520,8 @@ static int launch_wiener(fasst_ctx *c, const double *coef, const double *dpsd, d
     case 5: k_wiener<5><<<grid, 64, 0, c->stream>>>(w); break;
     case 6: k_wiener<6><<<grid, 64, 0, c->stream>>>(w); break;
     case 7: k_wiener<7><<<grid, 64, 0, c->stream>>>(w); break;
-    default: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
+    case 8: k_wiener<8><<<grid, 64, 0, c->stream>>>(w); break;
+    default: k_wiener<kMaxJ><<<grid, 64, 0, c->stream>>>(w); break;   // 9 .. kMaxJ
   }
   FASST_LAUNCH_CHECK();
   return FASST_OK;

@@ -222,6 +222,12 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (65, 77, 8, 128, 1, 2),      # J = 8, K = 128
     (33, 40, 5, 70, 2, 2),       # J = 5, K = 70, total rank 10
     (49, 52, 6, 100, [1, 2, 1, 2, 1, 2], 2),  # J = 6, K = 100, mixed ranks
+    # more than 8 sources (the two-pass E-step, k_egen_point / k_egen_stats;
+    # k_wiener's runtime-bounded kMaxJ form)
+    (49, 60, 12, 8, 1, 2),       # J = 12
+    (33, 40, 16, 4, 1, 2),       # J = 16, total rank 16
+    (65, 77, 10, 100, 1, 2),     # J = 10, K = 100 (KP = 128)
+    (40, 45, 9, 20, [2, 1, 2, 1, 2, 1, 2, 1, 2], 2),  # J = 9, mixed ranks, total 14
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
@@ -347,7 +353,7 @@ def test_free_fw_vs_oracle(F, T, J, K, rank, iters, omega, which):
     assert rel(np.abs(m.separated_images()), np.abs(o.separated_images(X))) < 1e-8
 
 
-@pytest.mark.parametrize("J,rank", [(6, 2), (8, 1)])
+@pytest.mark.parametrize("J,rank", [(6, 2), (8, 1), (12, 1), (16, 1)])
 def test_inst_many_sources_vs_oracle(J, rank):
     """'inst' mixing with more than 4 sources (total rank up to 12): the
     f-averaged real R x R solve of update_mix_matrix (audioModel.py:808-839)."""
@@ -632,6 +638,15 @@ def test_tw_restart_vs_oracle():
     assert rel(ll, llo) < 1e-10
     for j in range(2):
         assert rel(m.spec_comps[j]['factor'][0]['TW'], o.spec_comps[j]['factor'][0]['TW']) < 1e-8
+
+
+def test_sources_past_the_hip_path_fail_loudly():
+    """More than 16 sources, or a total spatial rank above 16, raise instead of
+    running."""
+    for J, rank in ((17, 1), (9, 2)):
+        with pytest.raises(NotImplementedError):
+            m, o, X = _c3_like(33, 40, J, 4, rank, 1)
+            m.estim_param_a_post_model()
 
 
 def test_unsupported_structures_fail_loudly():
