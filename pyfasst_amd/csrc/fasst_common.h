@@ -23,7 +23,8 @@ namespace fasst {
 
 constexpr double kEps = 1e-10;  // audioModel.py:61, tools/signalTools.py:11
 constexpr int kMaxJ = 16;       // sources (spatial components; > 8: the two-pass E-step)
-constexpr int kMaxR = 16;       // total spatial rank
+constexpr int kMaxR = 32;       // total spatial rank (the GEM path; the step calls: kStepMaxR)
+constexpr int kStepMaxR = 16;   // total spatial rank of fasst_suff_stat / fasst_mix_solve
 constexpr int kMaxKP = 128;     // padded NMF components (K > 64: one spectral
                                 // component per source, fixed FW, no lambdaCorr / TB)
 constexpr int kFwFpc = 64;      // bins per block of the FW update's f-contraction

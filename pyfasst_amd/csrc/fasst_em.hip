@@ -1267,7 +1267,8 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 // stored for k_mix_inst.
 // QM: statistics per lane, ceil(NACC / 64) (2 at J = 4; the J > 8 models
 // take the kMaxJ ceiling, the others stay at their own register count)
-template <int QM>
+// RQ: hat_Rss entries per lane, ceil(R^2 / 64) (4 up to R = 16)
+template <int QM, int RQ = 4>
 __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
   HALT_GUARD(a.halt);
   // LDS sized by this model's J, R, KP (mix_smem): with the kMaxJ / kMaxR /
@@ -1341,9 +1342,9 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     s_H[(r1) * R + (r2)] = v;
   }
   __syncthreads();
-  double2 hv[4];  // hermitised entries of this lane (e = lane + 64 q)
+  double2 hv[RQ];  // hermitised entries of this lane (e = lane + 64 q)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < RQ; ++q) {
     const int e = lane + 64 * q;
     hv[q] = make_double2(0.0, 0.0);
     if (e < R * R) {
@@ -1363,7 +1364,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     __syncthreads();
     if (a.rss) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < RQ; ++q) {
         const int e = lane + 64 * q;
         if (e < R * R) a.rss[((size_t)f * R + e / R) * R + e % R] = hv[q];
       }
@@ -1375,7 +1376,7 @@ __global__ __launch_bounds__(64) void k_mix(const MArgs a) {
     return;
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {  // L = hermitised(hat_Rss)^T
+  for (int q = 0; q < RQ; ++q) {  // L = hermitised(hat_Rss)^T
     const int e = lane + 64 * q;
     if (e < R * R) s_L[(e % R) * W + (e / R)] = hv[q];
   }
@@ -1473,7 +1474,8 @@ __global__ void k_mix_inst(const IArgs a) {
   }
   __syncthreads();
   if (tid != 0) return;
-  double Lm[kMaxR][kMaxR], B[kMaxR][2];
+  // (the serial solve on LDS copies: up to 32 x 32 would not fit registers)
+  __shared__ double Lm[kMaxR][kMaxR], B[kMaxR][2];
   for (int i = 0; i < nu; ++i) {
     for (int k = 0; k < nu; ++k) Lm[i][k] = s_m[k][i];  // rm^T
     B[i][0] = s_b[i][0];
@@ -4404,12 +4406,18 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     {
       const size_t ms = mix_smem(J, c->R, c->KP, c->nacc);
       const int q = (c->nacc + 63) / 64;
-      if (q <= 2)
+      constexpr int QX = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64;
+      if (c->R > 16) {   // (R^2 > 256 hat_Rss entries: 16 per lane; up to ~73 KB of LDS)
+        (void)hipFuncSetAttribute((const void *)k_mix<QX, (kMaxR * kMaxR + 63) / 64>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)ms);
+        k_mix<QX, (kMaxR * kMaxR + 63) / 64><<<c->F, 64, ms, c->stream>>>(m);
+      }
+      else if (q <= 2)
         k_mix<2><<<c->F, 64, ms, c->stream>>>(m);
       else if (q <= 4)   // (J <= 8: 4 J (J + 1) / 2 + 8 J <= 208)
         k_mix<4><<<c->F, 64, ms, c->stream>>>(m);
       else
-        k_mix<(4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64><<<c->F, 64, ms, c->stream>>>(m);
+        k_mix<QX><<<c->F, 64, ms, c->stream>>>(m);
     }
     prof_end(c, KMIX);
     FASST_LAUNCH_CHECK();

@@ -53,7 +53,7 @@ __global__ void k_source_powers(const double *__restrict__ Wkf, const double *__
 //   sV[r] = sum_t V_r
 // and hat_Rss / hat_Rxs follow per bin (see the header of fasst_em.hip).
 constexpr int kSsTile = 256;
-constexpr int kSsMaxOut = 4 * (kMaxR * (kMaxR + 1) / 2) + 8 * kMaxR + kMaxR;
+constexpr int kSsMaxOut = 4 * (kStepMaxR * (kStepMaxR + 1) / 2) + 8 * kStepMaxR + kStepMaxR;
 struct SSArgs {
   const double *cx00, *cx11, *cxr, *cxi;  // [Tp][Fp]
   const double *V;                        // [R][F][T]
@@ -69,14 +69,14 @@ struct SSArgs {
 __global__ __launch_bounds__(kSsTile) void k_suff_stat(const SSArgs a) {
   const int f = blockIdx.x, tid = threadIdx.x, R = a.R;
   const int NPAIR = R * (R + 1) / 2, NOUT = 4 * NPAIR + 8 * R + R;
-  __shared__ double2 s_a[kMaxR][2];
-  __shared__ double s_c[kMaxR][4];
-  __shared__ double s_v[kMaxR][kSsTile];
+  __shared__ double2 s_a[kStepMaxR][2];
+  __shared__ double s_c[kStepMaxR][4];
+  __shared__ double s_v[kStepMaxR][kSsTile];
   __shared__ double s_np[12][kSsTile];   // N (4) then P (8)
   __shared__ double s_out[kSsMaxOut];
   __shared__ double s_red[kSsTile];
   __shared__ unsigned char s_p1[kSsMaxOut], s_p2[kSsMaxOut];
-  __shared__ double2 s_m[kMaxR * kMaxR];
+  __shared__ double2 s_m[kStepMaxR * kStepMaxR];
   if (tid < R) {
     const double2 a0 = a.mix[((size_t)tid * 2 + 0) * a.F + f], a1 = a.mix[((size_t)tid * 2 + 1) * a.F + f];
     s_a[tid][0] = a0;
@@ -264,9 +264,9 @@ __global__ void k_ss_loglik(const double *__restrict__ llb, int F, double inv_ft
 __global__ void k_mix_solve_inst(const double2 *__restrict__ rss, const double2 *__restrict__ rxs,
                                  double2 *__restrict__ mix, int F, int R, const int *__restrict__ kind,
                                  int *singular) {
-  __shared__ double s_b[kMaxR][2], s_m[kMaxR][kMaxR];
-  __shared__ int s_u[kMaxR], s_o[kMaxR], s_nu, s_no, s_sing;
-  __shared__ double s_x[kMaxR][2];
+  __shared__ double s_b[kStepMaxR][2], s_m[kStepMaxR][kStepMaxR];
+  __shared__ int s_u[kStepMaxR], s_o[kStepMaxR], s_nu, s_no, s_sing;
+  __shared__ double s_x[kStepMaxR][2];
   const int tid = threadIdx.x;
   if (tid == 0) {
     int nu = 0, no = 0;
@@ -304,7 +304,7 @@ __global__ void k_mix_solve_inst(const double2 *__restrict__ rss, const double2 
   }
   __syncthreads();
   if (tid == 0) {
-    double L[kMaxR][kMaxR], B[kMaxR][2];
+    double L[kStepMaxR][kStepMaxR], B[kStepMaxR][2];
     for (int i = 0; i < nu; ++i) {
       for (int k = 0; k < nu; ++k) L[i][k] = s_m[k][i];   // m^T
       B[i][0] = s_b[i][0];
@@ -364,7 +364,7 @@ __global__ void k_mix_solve_conv(const double2 *__restrict__ rss, const double2 
                                  double2 *__restrict__ mix, int F, int R, int *singular) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
-  double2 L[kMaxR][kMaxR], B[kMaxR][2];
+  double2 L[kStepMaxR][kStepMaxR], B[kStepMaxR][2];
   for (int i = 0; i < R; ++i) {
     for (int k = 0; k < R; ++k) L[i][k] = rss[((size_t)f * R + k) * R + i];   // hat_Rss[f]^T
     for (int c = 0; c < 2; ++c) B[i][c] = rxs[((size_t)f * 2 + c) * R + i];  // hat_Rxs[f]^T
@@ -523,9 +523,13 @@ int fasst_source_powers(fasst_ctx *c, int j0, int nj, const unsigned long long *
 
 int fasst_suff_stat(fasst_ctx *c, int R, const double *V, const double *mix, const double *psd,
                     double *rxx, double *rxs, double *rss, double *ws, double *loglik) {
-  if (!c || R < 1 || R > kMaxR || !V || !mix || !psd || !rxx || !rxs || !rss || !ws || !loglik) {
-    set_error("fasst_suff_stat: bad arguments (R %d <= %d)", R, kMaxR);
+  if (!c || R < 1 || !V || !mix || !psd || !rxx || !rxs || !rss || !ws || !loglik) {
+    set_error("fasst_suff_stat: bad arguments (R %d <= %d)", R, kStepMaxR);
     return FASST_ERR_SHAPE;
+  }
+  if (R > kStepMaxR) {
+    set_error("fasst_suff_stat: total rank %d above the step call's %d", R, kStepMaxR);
+    return FASST_ERR_UNSUPPORTED;
   }
   if (!c->cx_ready || !c->cx.p || c->F < 1 || c->T < 1) {
     set_error("fasst_suff_stat: no observation resident (upload Cx first)");
@@ -579,9 +583,13 @@ int fasst_suff_stat(fasst_ctx *c, int R, const double *V, const double *mix, con
 
 int fasst_mix_solve(int device, int F, int R, const double *rss, const double *rxs, double *mix,
                     const int *kind) {
-  if (F < 1 || R < 1 || R > kMaxR || !rss || !rxs || !mix || !kind) {
-    set_error("fasst_mix_solve: bad arguments (R %d <= %d)", R, kMaxR);
+  if (F < 1 || R < 1 || !rss || !rxs || !mix || !kind) {
+    set_error("fasst_mix_solve: bad arguments (R %d <= %d)", R, kStepMaxR);
     return FASST_ERR_SHAPE;
+  }
+  if (R > kStepMaxR) {
+    set_error("fasst_mix_solve: total rank %d above the step call's %d", R, kStepMaxR);
+    return FASST_ERR_UNSUPPORTED;
   }
   int nconv = 0;
   for (int r = 0; r < R; ++r) nconv += kind[r] == 2;

@@ -228,6 +228,8 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (33, 40, 16, 4, 1, 2),       # J = 16, total rank 16
     (65, 77, 10, 100, 1, 2),     # J = 10, K = 100 (KP = 128)
     (40, 45, 9, 20, [2, 1, 2, 1, 2, 1, 2, 1, 2], 2),  # J = 9, mixed ranks, total 14
+    (33, 40, 12, 6, 2, 2),       # J = 12 'conv' at rank 2: total rank 24 (k_mix's 32-rank form)
+    (33, 36, 16, 4, 2, 2),       # J = 16 at rank 2: total rank 32
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
@@ -353,7 +355,7 @@ def test_free_fw_vs_oracle(F, T, J, K, rank, iters, omega, which):
     assert rel(np.abs(m.separated_images()), np.abs(o.separated_images(X))) < 1e-8
 
 
-@pytest.mark.parametrize("J,rank", [(6, 2), (8, 1), (12, 1), (16, 1)])
+@pytest.mark.parametrize("J,rank", [(6, 2), (8, 1), (8, 2), (12, 1), (16, 1), (12, 2)])
 def test_inst_many_sources_vs_oracle(J, rank):
     """'inst' mixing with more than 4 sources (total rank up to 12): the
     f-averaged real R x R solve of update_mix_matrix (audioModel.py:808-839)."""
@@ -641,9 +643,9 @@ def test_tw_restart_vs_oracle():
 
 
 def test_sources_past_the_hip_path_fail_loudly():
-    """More than 16 sources, or a total spatial rank above 16, raise instead of
+    """More than 16 sources, or a total spatial rank above 32, raise instead of
     running."""
-    for J, rank in ((17, 1), (9, 2)):
+    for J, rank in ((17, 1), (16, [2] * 15 + [3])):
         with pytest.raises(NotImplementedError):
             m, o, X = _c3_like(33, 40, J, 4, rank, 1)
             m.estim_param_a_post_model()
