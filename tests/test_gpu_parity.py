@@ -297,6 +297,39 @@ def test_k_above_64_every_structure_vs_oracle(what):
     assert rel(np.abs(m.separated_images(groups)), np.abs(o.separated_images(X, groups))) < 1e-8
 
 
+@pytest.mark.parametrize("what", ["multi_fw", "lambda_tb"])
+def test_many_sources_every_structure_vs_oracle(what):
+    """J = 10 (the two-pass E-step) with several spectral components per
+    spatial component, free FW, lambdaCorr and time blobs, against the
+    oracle."""
+    m, o, X = _c3_like(49, 60, 10, 12, 1, 2)
+    tb = {}
+    for mod in (m, o):
+        _split_spec(mod, {0: [5, 7], 3: [6, 6], **{j: [12] for j in (1, 2, 4, 5, 6, 7, 8, 9)}})
+        if what == "multi_fw":
+            for k in (0, 3, 10):
+                fac = mod.spec_comps[k]['factor'][0]
+                n = fac['FW'].shape[0]
+                fac['FW'] = fac['FW'] + 0.2 * np.abs(np.random.RandomState(90 + k).randn(n, n))
+                fac['FW_frdm_prior'] = 'free'
+        else:
+            mod.lambdaCorr = 0.2
+            tb = {1: (4, 'free', 'free'), 11: (3, 'free', 'free')}
+            _time_blobs(mod, tb)
+    ll = m.estim_param_a_post_model()
+    llo = o.estim_param_a_post_model()
+    assert rel(ll, llo) < 1e-10
+    for k in sorted(o.spec_comps):
+        keys = ('FB', 'FW', 'TW', 'TB') if k in tb else ('FB', 'FW', 'TW')
+        for key in keys:
+            assert rel(m.spec_comps[k]['factor'][0][key], o.spec_comps[k]['factor'][0][key]) < 1e-8, \
+                (k, key)
+    for j in range(10):
+        assert rel(m.spat_comps[j]['params'], o.spat_comps[j]['params']) < 1e-8
+    groups = _spatial_groups(m)
+    assert rel(np.abs(m.separated_images(groups)), np.abs(o.separated_images(X, groups))) < 1e-8
+
+
 def test_fixed_components_vs_oracle():
     """frdm_prior 'fixed' paths: FB fixed, TW fixed, an instantaneous spatial
     component fixed (exercises the 'other' subtraction, audioModel.py:817-823)."""
