@@ -1105,69 +1105,72 @@ __global__ __launch_bounds__(64) void k_egen_point(const EArgs a, const GArgs g)
   if (lane == 0) g.lw[(size_t)tt * a.nft + ft] = ll;
 }
 
-__global__ __launch_bounds__(256) void k_egen_stats(const EArgs a, const GArgs g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_egen_stats(const EArgs a, const GArgs g) {
   HALT_GUARD(a.halt);
-  constexpr int MU = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 15) / 16;   // sums per thread
+  // wave wv, lane (bin b, component n): the pair sums V_j1 V_j2 N_n of
+  // j1 = wv + 4 q (q < 4; wave-uniform, each over j2 = j1 .. J - 1) and the
+  // cross sums V_j P_c of source j = 4 wv + n; per frame a lane reads its
+  // bin's V_j, N and P once (registers) and V_j1 of each task from LDS
   const int J = g.J, NP = J * (J + 1) / 2, NACC = 4 * NP + 8 * J;
-  const int tid = threadIdx.x, b = tid & 15, ug = tid >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, b = lane & 15, n = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), jx = 4 * wv + n;
   const int ft = blockIdx.x, f0 = ft * 16, y = blockIdx.y;
   extern __shared__ __attribute__((aligned(16))) double s_t[];   // [J + 12][16 frames][16 bins]
-  __shared__ unsigned char s_a[4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ][3];
-  for (int u = tid; u < NACC; u += 256) {
-    int r0, r1, r2;
-    if (u < 4 * NP) {   // pair p = (lo, hi) canonical (lo major), component n
-      int p = u >> 2, lo = 0;
-      while (p >= J - lo) {
-        p -= J - lo;
-        ++lo;
-      }
-      r0 = lo;
-      r1 = lo + p;
-      r2 = J + (u & 3);          // N_n
-    } else {
-      const int q = u - 4 * NP;
-      r0 = q >> 3;
-      r1 = -1;
-      r2 = J + 4 + (q & 7);      // P_c
-    }
-    s_a[u][0] = (unsigned char)r0;
-    s_a[u][1] = (unsigned char)(r1 < 0 ? 255 : r1);
-    s_a[u][2] = (unsigned char)r2;
-  }
-  double acc[MU];
+  double pacc[4][kMaxJ], xacc[8];
 #pragma unroll
-  for (int m = 0; m < MU; ++m) acc[m] = 0.0;
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j2 = 0; j2 < kMaxJ; ++j2) pacc[q][j2] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) xacc[c] = 0.0;
   const size_t plane = (size_t)a.Tp * a.Fp;
   const int tb = a.tbase + y * a.tpc, te = min(tb + a.tpc, a.ntt);
   const int nr = J + 12;
   for (int tt = tb; tt < te; ++tt) {
-    __syncthreads();   // (the previous tile's reads; the first: s_a)
+    __syncthreads();   // (the previous tile's reads)
     for (int idx = tid; idx < nr * 256; idx += 256) {
       const int r = idx >> 8, e = idx & 255, tl = e >> 4, fl = e & 15;
       const size_t o = (size_t)(tt * 16 + tl) * a.Fp + f0 + fl;
       s_t[idx] = r < J ? g.V[r * plane + o] : g.NP[(r - J) * plane + o];
     }
     __syncthreads();
+    for (int tl = 0; tl < 16; ++tl) {
+      const double *col = s_t + tl * 16 + b;   // row r at col[256 r]
+      double v[kMaxJ];
 #pragma unroll
-    for (int m = 0; m < MU; ++m) {
-      const int u = ug + 16 * m;
-      if (u < NACC) {
-        const int r0 = s_a[u][0], r1 = s_a[u][1], r2 = s_a[u][2];
-        double x = acc[m];
-        for (int tl = 0; tl < 16; ++tl) {
-          const double w = r1 == 255 ? s_t[(r0 * 16 + tl) * 16 + b]
-                                     : s_t[(r0 * 16 + tl) * 16 + b] * s_t[(r1 * 16 + tl) * 16 + b];
-          x = fma(w, s_t[(r2 * 16 + tl) * 16 + b], x);
+      for (int j = 0; j < kMaxJ; ++j) v[j] = j < J ? col[256 * j] : 0.0;
+      const double nn = col[256 * (J + n)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j1 = wv + 4 * q;   // (wave-uniform: scalar branches)
+        if (j1 < J) {
+          const double vn = col[256 * j1] * nn;   // V_j1 N_n
+#pragma unroll
+          for (int j2 = 0; j2 < kMaxJ; ++j2)
+            if (j2 >= j1 && j2 < J) pacc[q][j2] = fma(vn, v[j2], pacc[q][j2]);
         }
-        acc[m] = x;
+      }
+      if (jx < J) {
+        const double vj = col[256 * jx];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) xacc[c] = fma(vj, col[256 * (J + 4 + c)], xacc[c]);
       }
     }
   }
+  double *out = a.part + ((size_t)(a.ybase + y) * a.Fp + f0 + b) * NACC;
 #pragma unroll
-  for (int m = 0; m < MU; ++m) {
-    const int u = ug + 16 * m;
-    if (u < NACC) a.part[((size_t)(a.ybase + y) * a.Fp + f0 + b) * NACC + u] = acc[m];
+  for (int q = 0; q < 4; ++q) {
+    const int j1 = wv + 4 * q;
+    if (j1 < J) {
+      const int p0 = j1 * J - j1 * (j1 - 1) / 2;   // canonical index of (j1, j1)
+#pragma unroll
+      for (int j2 = 0; j2 < kMaxJ; ++j2)
+        if (j2 >= j1 && j2 < J) out[4 * (p0 + j2 - j1) + n] = pacc[q][j2];
+    }
   }
+  if (jx < J)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) out[4 * NP + 8 * jx + c] = xacc[c];
   if (tid == 0) {   // the chunk's loglik, its tiles in order
     double l = 0.0;
     for (int tt = tb; tt < te; ++tt) l += g.lw[(size_t)tt * a.nft + ft];
