@@ -83,9 +83,19 @@ def iteration_work(F, T, J, R, K):
 # the kernels one GEM iteration launches (each once), for the PMC traffic sum
 ITERATION_KERNELS = ("k_w_from_fb", "k_fwh_t", "k_tw_rowsum", "k_inst_A", "k_estep_part1",
                      "k_estep_part2", "k_estep", "k_loglik", "k_mix", "k_mix_inst",
-                     "k_fb_contract", "k_fb_update", "k_tw_contract", "k_tw_update",
+                     "k_fb_contract", "k_fb_update", "k_tw_contract", "k_tw_contract_lds",
+                     "k_tw_update",
                      "k_renorm_stats", "k_renorm_apply", "k_renorm_final", "k_renorm_scales",
                      "k_renorm_rows", "k_renorm_tail")
+
+
+def pmc_bytes(pmc, k):
+    """HBM bytes per launch of kernel k in a summarize_prof.py record (the
+    single-component TW contraction is profiled as k_tw_contract_lds)."""
+    for name in (k, k + "_lds"):
+        if pmc and name in pmc and pmc[name].get("hbm_bytes_per_launch"):
+            return pmc[name]["hbm_bytes_per_launch"]
+    return None
 
 
 PROF_STEPS = 64   # iterations of the per-kernel timing pass (two event rings)
@@ -432,15 +442,18 @@ def main(argv=None):
         step_s = dt / args.steps
         iter_traffic = None
         if pmc:
-            tot = [pmc[k]["hbm_bytes_per_launch"] for k in ITERATION_KERNELS
+            # each kernel weighted by its launches per E-step launch (k_fwh_t /
+            # k_tw_rowsum run only where k_tw_update's prep does not)
+            n_it = pmc.get("k_estep", {}).get("calls") or None
+            tot = [pmc[k]["hbm_bytes_per_launch"] *
+                   (min(1.0, pmc[k]["calls"] / n_it) if n_it and pmc[k].get("calls") else 1.0)
+                   for k in ITERATION_KERNELS
                    if k in pmc and pmc[k].get("hbm_bytes_per_launch")]
             iter_traffic = float(sum(tot)) if tot else None
         if dom in work:
             sec = times[dom][0] * 1e-3
             achieved = work[dom]["flops"] / sec / 1e12
-            traffic = None
-            if pmc and dom in pmc and pmc[dom].get("hbm_bytes_per_launch"):
-                traffic = pmc[dom]["hbm_bytes_per_launch"]
+            traffic = pmc_bytes(pmc, dom)
             # the binding roofline of the kernel: HBM when its algorithmic
             # bytes take longer at HBM_PEAK than its flops at the FP64 MFMA peak
             hbm_bound = work[dom]["bytes"] / HBM_PEAK > work[dom]["flops"] / FP64_MFMA_PEAK
@@ -479,7 +492,8 @@ def main(argv=None):
                     "gbps": round(work[k]["bytes"] / (times[k][0] * 1e-3) / 1e9, 1),
                     "hbm_frac": round(work[k]["bytes"] / (times[k][0] * 1e-3) / HBM_PEAK, 4),
                     "bound": "hbm" if work[k]["bytes"] / HBM_PEAK
-                    > work[k]["flops"] / FP64_MFMA_PEAK else "mfma"}
+                    > work[k]["flops"] / FP64_MFMA_PEAK else "mfma",
+                    "traffic": pmc_bytes(pmc, k)}
                 for k in ("k_estep", "k_tw_contract", "k_fb_contract") if k in times and k in work}
         out = {
             "metric": "EM iterations/sec (F=2049, T=10000, 2ch, 4src) at 1/2/4/8 MI355X",

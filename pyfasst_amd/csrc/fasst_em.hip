@@ -2343,6 +2343,19 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
     double tsum = 0.0;
     for (int kb = 0; kb < a.K[j]; kb += 64) {
       const int kn = min(64, a.K[j] - kb);
+      // the block's TW values in flight before the ratio loads (their two
+      // latency chains overlap); raw-buffer loads on the source's plane, an
+      // offset past it (elements past kn, frames past Tp) reads 0
+      const __amdgpu_buffer_rsrc_t rtw = __builtin_amdgcn_make_buffer_rsrc(
+          a.TW + (size_t)j * a.KP * a.Tp, 0, (int)((size_t)a.KP * a.Tp * 8), 0x00020000);
+      // (8 per thread: all of them at K <= 32; the rest load in place)
+      double xv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int idx = threadIdx.x + 256 * e, kl = idx / 64, tl = idx % 64;
+        const unsigned vo = idx < 64 * kn ? (unsigned)(((kb + kl) * a.Tp + t0 + tl) * 8) : 0x7ffffff0u;
+        xv[e] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rtw, (int)vo, 0, 0));
+      }
       if (fr)
         for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
           const int tl = idx / kn, kl = idx % kn, t = t0 + tl;
@@ -2360,11 +2373,13 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
           s_r[kl][tl] = r;
         }
       __syncthreads();
-      for (int idx = threadIdx.x; idx < 64 * kn; idx += blockDim.x) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int idx = threadIdx.x + 256 * e;
         const int kl = idx / 64, tl = idx % 64, t = t0 + tl, k = kb + kl;
-        if (t < a.T) {
+        if (idx < 64 * kn && t < a.T) {
           double *p = a.TW + ((size_t)j * a.KP + k) * a.Tp + t;
-          double x = *p;
+          double x = e < 8 ? xv[e < 8 ? e : 0] : *p;
           if (fr && k >= a.kb0[j] && k < a.kb1[j]) x *= s_r[kl][tl];
           const double y = x * w2[k];
           *p = y;
