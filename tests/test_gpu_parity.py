@@ -230,6 +230,12 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     (40, 45, 9, 20, [2, 1, 2, 1, 2, 1, 2, 1, 2], 2),  # J = 9, mixed ranks, total 14
     (33, 40, 12, 6, 2, 2),       # J = 12 'conv' at rank 2: total rank 24 (k_mix's 32-rank form)
     (33, 36, 16, 4, 2, 2),       # J = 16 at rank 2: total rank 32
+    # the full F = 2049 of BASELINE config 3, every point compared (the
+    # golden full-size fixtures keep a subsample): the production launch
+    # shapes -- E-step frame chunks, FB / TW splits, XCD block order -- of the
+    # headline structure and of 8 sources (oracle ~30 s / ~15 s on the host)
+    (2049, 1000, 4, 32, 2, 2),
+    (2049, 500, 8, 32, 1, 2),
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
