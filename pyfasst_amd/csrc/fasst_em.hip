@@ -2340,6 +2340,15 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
     const bool prep = a.FWHt != nullptr;
     if (prep)
       for (int idx = threadIdx.x; idx < a.KP * 64; idx += blockDim.x) s_y[idx] = 0.0;
+    // the prep's FW values (4 per thread: all of them at KP = 32) in flight
+    // from the start; the source's FW block is in range for every idx < KP^2
+    double fwv[4];
+    if (prep)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int idx = min((int)threadIdx.x + 256 * e, a.KP * a.KP - 1), k = idx / a.KP, q = idx % a.KP;
+        fwv[e] = a.FW[(size_t)j * a.KP * a.KP + (size_t)k * a.KP + q];
+      }
     double tsum = 0.0;
     for (int kb = 0; kb < a.K[j]; kb += 64) {
       const int kn = min(64, a.K[j] - kb);
@@ -2408,7 +2417,14 @@ __global__ __launch_bounds__(256) void k_tw_update(const TUArgs a) {
 #pragma unroll
     for (int kc = 0; kc < kMaxKP / 16; ++kc) d[kc] = d4{0.0, 0.0, 0.0, 0.0};
     for (int qb = 0; qb < KP; qb += QB) {
-      for (int idx = threadIdx.x; idx < QB * KP; idx += blockDim.x) {
+      if (QB == KP) {   // (qb = 0: the values loaded at entry, then the rest)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int idx = threadIdx.x + 256 * e;
+          if (idx < KP * KP) s_fw[(idx % KP) * KP + idx / KP] = fwv[e];
+        }
+      }
+      for (int idx = threadIdx.x + (QB == KP ? 1024 : 0); idx < QB * KP; idx += blockDim.x) {
         const int k = idx / QB, q = idx % QB;   // (coalesced over q in FW's rows)
         s_fw[q * KP + k] = gfw[(size_t)k * KP + qb + q];
       }
