@@ -1,11 +1,17 @@
 """The fused renormalisation tail (fasst_em.hip: k_fb_update statistics,
 k_renorm_scales / _rows on the side stream, TW rescale inside k_tw_update,
-k_renorm_tail; renormalize_parameters, audioModel.py:1980-2040) against the
-unfused kernels (FASST_FAST_TAIL=0, read when a context is created) and the
-oracle, on the structures it covers: one spectral component per source,
-fixed FW, no time blobs.  Halted batches (a TW restart raised mid-batch) are
-covered: the host swaps the W buffers of iterations the device skipped, and
-fasst_run rebuilds W from the parameters."""
+k_renorm_tail; renormalize_parameters, audioModel.py:1980-2040) and the FB
+numerator contracted inside the E-step (k_estep_mx FBF;
+update_spectral_components, audioModel.py:1521-1575) against the unfused
+kernels (FASST_FAST_TAIL=0, FASST_FBF=0, read when a context is created) and
+the oracle, on the structures they cover: one spectral component per source,
+fixed FW, no time blobs.  Every fused mode is run: FASST_FAST_TAIL=1 (the
+tail alone), 2 (the default: the tail also forms the next iteration's
+(FW.TW)^T and TW row sums, and the next iteration skips its prep), each with
+and without the fused FB numerator (the default for J <= 4, KP <= 32).
+Halted batches (a TW restart raised mid-batch) are covered in every mode:
+the host swaps the W buffers of iterations the device skipped, and fasst_run
+rebuilds W (and the prep) from the parameters."""
 import numpy as np
 import pytest
 
@@ -36,8 +42,14 @@ def _models(F, T, J, K, rank, iters, conv=True, seed=0):
     return m, o, X
 
 
-def _run(monkeypatch, fast, args, kw, prep=None, restart_seed=None):
-    monkeypatch.setenv("FASST_FAST_TAIL", "1" if fast else "0")
+# (FASST_FAST_TAIL, FASST_FBF); UNFUSED is the reference mode
+MODES = [("1", "0"), ("2", "0"), ("1", "1"), ("2", "1")]
+UNFUSED = ("0", "0")
+
+
+def _run(monkeypatch, mode, args, kw, prep=None, restart_seed=None):
+    monkeypatch.setenv("FASST_FAST_TAIL", mode[0])
+    monkeypatch.setenv("FASST_FBF", mode[1])
     m, o, X = _models(*args, **kw)
     if prep:
         prep(m)
@@ -50,18 +62,21 @@ def _run(monkeypatch, fast, args, kw, prep=None, restart_seed=None):
 
 CASES = [
     # (F, T, J, K, rank, iters), conv
-    ((129, 301, 4, 32, 2, 6), True),      # the C3 structure, ragged T
+    ((129, 301, 4, 32, 2, 6), True),      # the C3 structure, ragged T (and ragged 64-frame blocks)
     ((129, 301, 4, 32, 2, 6), False),     # 'inst' mixing
-    ((97, 203, 3, 40, [1, 2, 1], 4), True),   # mixed ranks, K padded to 64
+    ((97, 203, 3, 40, [1, 2, 1], 4), True),   # mixed ranks, K padded to 64 (the LDS prep path)
     ((97, 150, 2, 100, 2, 3), True),      # K > 64 (KP = 128: FW from L2)
     ((65, 77, 6, 8, 2, 3), True),         # J > 4
+    ((81, 181, 2, 16, 1, 5), True),       # J = 2, KP = 16: two waves own no source
+    ((70, 97, 4, 20, 2, 4), True),        # K = 20 padded to 32; 7 frame tiles: a wave idles in the last round
 ]
 
 
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail%s_fbf%s" % m)
 @pytest.mark.parametrize("args,conv", CASES)
-def test_fast_tail_vs_unfused_and_oracle(monkeypatch, args, conv):
-    mf, o, X, llf = _run(monkeypatch, True, args, dict(conv=conv))
-    ms, _, _, lls = _run(monkeypatch, False, args, dict(conv=conv))
+def test_fast_tail_vs_unfused_and_oracle(monkeypatch, args, conv, mode):
+    mf, o, X, llf = _run(monkeypatch, mode, args, dict(conv=conv))
+    ms, _, _, lls = _run(monkeypatch, UNFUSED, args, dict(conv=conv))
     llo = o.estim_param_a_post_model()
     J = args[2]
     # the fused form sums the spatial energy in another order: last bits only
@@ -85,14 +100,15 @@ def _dead_tw(mod):   # tiny but non-zero: the mixing solve stays regular
     mod.spec_comps[1]['factor'][0]['TW'][:] = 1e-30
 
 
-def test_fast_tail_restart_halts_the_batch(monkeypatch):
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail%s_fbf%s" % m)
+def test_fast_tail_restart_halts_the_batch(monkeypatch, mode):
     """sum(TW) < eps after the first iteration: k_renorm_tail raises the
     restart flag, the batch's later iterations return at entry, the host
     redraws TW (audioModel.py:2023-2028) and resumes; W is rebuilt after the
     halted batch (the buffers swapped for skipped iterations)."""
     args = (33, 40, 2, 4, 1, 5)
-    mf, o, X, llf = _run(monkeypatch, True, args, {}, prep=_dead_tw, restart_seed=11)
-    ms, _, _, lls = _run(monkeypatch, False, args, {}, prep=_dead_tw, restart_seed=11)
+    mf, o, X, llf = _run(monkeypatch, mode, args, {}, prep=_dead_tw, restart_seed=11)
+    ms, _, _, lls = _run(monkeypatch, UNFUSED, args, {}, prep=_dead_tw, restart_seed=11)
     np.random.seed(11)
     llo = o.estim_param_a_post_model()
     assert rel(llf, lls) < 1e-12
@@ -104,11 +120,12 @@ def test_fast_tail_restart_halts_the_batch(monkeypatch):
     assert rel(np.abs(Sf), np.abs(o.separated_images(X))) < 1e-8
 
 
-def test_fast_tail_second_run_after_restart(monkeypatch):
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail%s_fbf%s" % m)
+def test_fast_tail_second_run_after_restart(monkeypatch, mode):
     """A model run again after a restarted run starts from the host
     parameters (W rebuilt at the batch start, not a stale swapped buffer)."""
     args = (33, 40, 2, 4, 1, 3)
-    mf, o, X, _ = _run(monkeypatch, True, args, {}, prep=_dead_tw, restart_seed=5)
+    mf, o, X, _ = _run(monkeypatch, mode, args, {}, prep=_dead_tw, restart_seed=5)
     np.random.seed(5)
     o.estim_param_a_post_model()
     ll2 = mf.estim_param_a_post_model()
