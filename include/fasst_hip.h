@@ -37,6 +37,15 @@ extern "C" {
 
 typedef struct fasst_ctx fasst_ctx;
 
+/* ABI revision of this header.  A caller compares fasst_abi_version() with
+ * the FASST_ABI_VERSION it was built against and refuses a mismatch (the
+ * Python loader does, pyfasst_amd/_lib.py).  Revision 2: fasst_source_powers
+ * and fasst_sigma_comp take 128-bit column sets (two 64-bit words per
+ * spatial component; revision 1 read one word, and fasst_sigma_comp took its
+ * mask by value), so a revision-1 caller would pass too short an array. */
+#define FASST_ABI_VERSION 2
+int fasst_abi_version(void);
+
 const char *fasst_last_error(void);
 int fasst_device_count(int *n);
 

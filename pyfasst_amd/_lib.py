@@ -37,6 +37,7 @@ _llp = ctypes.POINTER(ctypes.c_longlong)
 
 # name -> (restype, argtypes); must match include/*.h exactly
 SIGNATURES = {
+    "fasst_abi_version": (ctypes.c_int, []),
     "fasst_last_error": (ctypes.c_char_p, []),
     "fasst_device_count": (ctypes.c_int, [_ip]),
     "fasst_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
@@ -142,6 +143,13 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn = getattr(lib, _name)
     _fn.restype = _res
     _fn.argtypes = _args
+
+# include/fasst_hip.h FASST_ABI_VERSION these signatures were written against
+# (revision 2: 128-bit column sets in fasst_source_powers / fasst_sigma_comp)
+ABI_VERSION = 2
+if lib.fasst_abi_version() != ABI_VERSION:
+    raise ImportError("pyfasst_amd: %s has ABI revision %d, this binding expects %d; rebuild it "
+                      "(make -C pyfasst_amd/csrc)" % (LIB_PATH, lib.fasst_abi_version(), ABI_VERSION))
 
 
 class FasstError(RuntimeError):

@@ -688,22 +688,25 @@ class FASST(object):
         stream (the reference's draw order) and gives every rank of
         component j the parameters A[j].T.  'demix' needs the DEMIX
         estimator (pyfasst.demixTF), which is outside this engine's scope
-        (DESIGN.md §7): NotImplementedError."""
+        (DESIGN.md §7): NotImplementedError.  The method is checked before
+        any component changes type (the reference sets every 'mix_type' to
+        'conv' first, so a caught error left 'conv' components holding 'inst'
+        parameters): a refused call leaves the model as it was."""
         nc = self.audioObject.channels
         for spat_ind, spat_comp in self.spat_comps.items():
             if spat_comp['mix_type'] != 'inst':
                 warnings.warn("Spatial component %d " % spat_ind +
                               "already not instantaneous, overwriting...")
-            spat_comp['mix_type'] = 'conv'
         if initMethod == 'demix':
             raise NotImplementedError("initializeConvParams('demix'): the DEMIX estimator "
                                       "(demixTF) is outside the HIP engine's scope; use 'rand'")
-        elif 'rand' in initMethod:
-            J = len(self.spat_comps)
-            A = (np.random.randn(J, self.nbFreqsSigRepr, nc) +
-                 1j * np.random.randn(J, self.nbFreqsSigRepr, nc))
-        else:
+        elif 'rand' not in initMethod:
             raise ValueError("Init method not implemented.")
+        J = len(self.spat_comps)
+        A = (np.random.randn(J, self.nbFreqsSigRepr, nc) +
+             1j * np.random.randn(J, self.nbFreqsSigRepr, nc))
+        for spat_comp in self.spat_comps.values():
+            spat_comp['mix_type'] = 'conv'
         for nspat, (spat_ind, spat_comp) in enumerate(self.spat_comps.items()):
             spat_comp['params'] = np.zeros([self.rank[nspat], nc, self.nbFreqsSigRepr],
                                            dtype=complex)

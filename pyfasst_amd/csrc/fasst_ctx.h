@@ -100,10 +100,6 @@ struct fasst_ctx {
   // TW contraction form: 0 = k_tw_contract (W operands from L2 per lane),
   // 1 = k_tw_contract_lds (FASST_TWL, read at creation)
   int twl = 1;
-  // the FB numerator contracted inside the E-step (k_estep_mx FBF) where the
-  // structure allows it (fbf_on in fasst_em.hip); FASST_FBF=1 at creation.
-  // Measured slower (profiles/r6_ab_fbf.txt): off
-  int fbf = 0;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart

@@ -242,10 +242,6 @@ struct EArgs {
   double *hatW;                           // [J][Tp][Fp]: rho = hat_W / max(V, eps)
   double *part;                           // [nchunk][Fp][NACC]
   double *llpart;                         // [nchunk][nft]
-  // FBF (k_estep_mx's fused FB numerator): (FW.TW)^T [J][Tp][KP] and the
-  // numerator partials [nchunk][J][Fp][KP] (k_fb_contract's bnum layout)
-  const double *FWHt;
-  double *fbnum;
   int F, T, Fp, Tp, KP, R, ntt, tpc, nft;
   int ybase, tbase;  // this launch's chunks start at partial ybase, frame tile tbase (ntt = end)
   int roff[kMaxJ + 1];
@@ -341,11 +337,9 @@ __host__ __device__ constexpr bool mx_w_in_lds() {
   return (size_t)(4 + J * 4 * NKS * 16 + 4 * MXShape<J>::SLAB + J * 4 * 16) * sizeof(double) <=
          160 * 1024;
 }
-// FBF: the rho exchange area of the fused FB numerator, [J][3][4][64]
-template <int J, int NKS, bool FBF = false>
+template <int J, int NKS>
 static constexpr size_t estep_mx_smem() {
-  return (size_t)(4 + (mx_w_in_lds<J, NKS>() ? J * 4 * NKS * 16 : 0) + 4 * MXShape<J>::SLAB +
-                  (FBF ? J * 3 * 256 : 0)) *
+  return (size_t)(4 + (mx_w_in_lds<J, NKS>() ? J * 4 * NKS * 16 : 0) + 4 * MXShape<J>::SLAB) *
          sizeof(double);
 }
 
@@ -377,27 +371,12 @@ __device__ __forceinline__ void es_st(double v, __amdgpu_buffer_rsrc_t r, unsign
 
 // (J = 4 at K = 128: the 64 KB W tile leaves one block per CU, so one wave
 // per SIMD and the full register file for the pipelined V tile)
-//
-// FBF (J <= 4, KP <= 32, one spectral component per source): the FB
-// numerator num_j[f][k] = sum_t rho_j[f][t] (FW.H)^T[t][k] of
-// update_spectral_components (audioModel.py:1521-1575, N1) is contracted
-// here, so rho is read by the TW contraction only (k_fb_contract and its
-// 655 MB re-read of rho at C3 go).  A lane's rho of point i (bin f0 + fl,
-// frame t0 + tq + 4 i) is exactly the A operand of the 16x16x4 step i over
-// the tile's frames, so no lane ever moves data: wave w owns source w, and the
-// other waves hand it their tile's rho_w through an LDS exchange area
-// ([dest source][3 slots][4 steps][64 lanes], written as the points are
-// formed); each round of four frame tiles the owner contracts the four tiles
-// with (FW.H)^T from L2 (NKS / 4 16-column accumulators), between two block
-// barriers.  The numerator partials are written per frame chunk into
-// k_fb_contract's layout, read by k_fb_update unchanged.
-template <int J, int NKS, int RKU, bool FBF = false>
+template <int J, int NKS, int RKU>
 __global__ __launch_bounds__(256, (J > 4 || (J == 4 && NKS == 32)) ? 1 : 2)
 __attribute__((amdgpu_waves_per_eu(1, (J > 4 || (J == 4 && NKS == 32)) ? 1 : 2))) FASST_NO_LDS_PAIRING
 void k_estep_mx(const EArgs a) {
   HALT_GUARD(a.halt);
   using S = MXShape<J>;
-  static_assert(!FBF || (J <= 4 && NKS <= 8), "fused FB numerator: J <= 4, KP <= 32");
   constexpr bool VR = S::VR, RP = S::RP;
   constexpr int Q = S::Q;
   constexpr int NP = S::NP, NPG = S::NPG, NVG = S::NVG;
@@ -540,445 +519,333 @@ void k_estep_mx(const EArgs a) {
   constexpr bool CXE = J > 4;
   double cxv[4][4];
   if (CXE && tb + wvu < te) load_cx(tb + wvu, cxv);
-
-  // FBF: the fused FB numerator (see above the kernel)
-  constexpr int NKC = FBF ? NKS / 4 : 1;   // 16-column tiles of num
-  double *s_fbx = s_slab + 4 * S::SLAB;    // [J][3][4][64] rho exchange area
-  d4 fba[NKC];                             // source wvu's num: bins x 16 columns per tile
+  for (int tt = tb + wvu; tt < te; tt += 4) {
+    const int t0 = tt * 16;
+    int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
+    asm volatile("" : "+v"(lofs));
+    // all TW operands in flight before the first MFMA (the scheduler would
+    // otherwise pair each load with its MFMA and wait on every one); with more
+    // than 32 operands (J > 4 or K > 32 at J = 4) the sources beyond the first
+    // 32 operands load next to their own MFMAs
+    // (VR: none up front -- the V loop below pipelines them source by source)
+    // CP: more operands than that (J <= 4 at K >= 64): the V tiles as one
+    // pipeline of 8-MFMA chunks over (source, k), each chunk's TW operands
+    // issued two chunks ahead -- the per-source inline loads left each
+    // source's load latency exposed (J = 4, K = 128: 2.70 ms).  (The same
+    // pipeline for the VR loop with W from L2, J > 4 at K = 128, crashes
+    // ROCm 7.2's compiler at distance 2 and spills 0.4-1.8 KB per lane at 1.)
+    constexpr bool CP = !VR && J * NKS > 32;
+    constexpr int JA = (VR || CP) ? 1 : (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
+    double twv[JA][NKS];
 #pragma unroll
-  for (int n = 0; n < NKC; ++n) fba[n] = d4{0.0, 0.0, 0.0, 0.0};
-  double own[4] = {0.0, 0.0, 0.0, 0.0};    // the wave's own tile's rho of its source
-  const __amdgpu_buffer_rsrc_t r_fwh = es_rsrc(FBF && wvu < J ? a.FWHt + (size_t)wvu * a.Tp * KP : a.TW);
-  const unsigned vo_fb = (unsigned)(tq * KP + fl) * 8u;   // (FW.H)^T[t0 + 4 i + tq][16 n + fl]
-  // one round = frame tiles tr .. tr + 3, wave v's tile tr + v.  Slot s < 3 of
-  // the owner holds the tile of wave s + (s >= owner), slot 3 is its own tile.
-  auto fb_round = [&](int tr) {
-#ifndef FBF_DBG
-#define FBF_DBG 0
-#endif
-    if (FBF_DBG == 3) return;
-    double bo[4][4][NKC];   // (FW.H)^T operands, in flight across the first barrier
-    if (FBF_DBG != 1 && wvu < J) {
+    for (int j = 0; j < (CP ? 0 : JA); ++j) {
+      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int tv = tr + (s == 3 ? wvu : s + (s >= wvu));
-        if (tv < te)
+      for (int s = 0; s < NKS; ++s)
+        twv[j][s] = SA ? es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u)
+                       : tw[(size_t)(4 * s) * a.Tp];
+    }
+    if constexpr (!CXE) load_cx(tt, cxv);  // this tile's Cx (in flight with the TW operands)
+    __builtin_amdgcn_sched_barrier(0);
+    d4 v[J];
+    if constexpr (CP) {
+      constexpr int CH = 8, CPS = NKS / CH, NCH = J * CPS, PD = 2;   // chunks, prefetch distance
+      static_assert(NKS % CH == 0, "k chunks of 8");
+      double ta[PD + 1][CH], wa[PD + 1][WL ? 1 : CH];
+      auto ld = [&](int u, int sl) {
+        const int j = u / CPS, s0 = (u % CPS) * CH;
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int c = 0; c < CH; ++c) {
+          const int s = s0 + c;
+          ta[sl][c] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u);
+          if constexpr (!WL)
+            wa[sl][c] = a.Wkf[lofs + ((size_t)j * KP + tq + 4 * s) * a.Fp + f];
+        }
+      };
 #pragma unroll
-            for (int n = 0; n < NKC; ++n)
-              bo[s][i][n] = es_ld<0>(r_fwh, vo_fb, (unsigned)(((tv * 16 + 4 * i) * KP + 16 * n) * 8));
+      for (int u = 0; u < PD; ++u) ld(u, u);
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        if (u + PD < NCH) ld(u + PD, (u + PD) % (PD + 1));
+        __builtin_amdgcn_sched_barrier(0);
+        const int j = u / CPS, s0 = (u % CPS) * CH, sl = u % (PD + 1);
+        if (s0 == 0) v[j] = d4{0.0, 0.0, 0.0, 0.0};
+        const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          v[j] = mfma4(ta[sl][c], WL ? sw[4 * (s0 + c) * 16] : wa[sl][WL ? 0 : c], v[j]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    }
-    // every wave's rho of the round is in the area (LDS only: the operand
-    // loads above and the rho stores stay in flight)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    double av[3][4];
-    if (FBF_DBG != 1 && wvu < J) {
-      const double *rx = s_fbx + wvu * (3 * 256) + lane;
+    } else if constexpr (VR && !(WL || NKS <= 16)) {
+      // J > 4 at K = 128 (W from L2): a runtime loop over the sources, each
+      // source's V tile a 4-chunk pipeline of 8 MFMAs with the next chunk's TW
+      // and W operands in flight (the last chunk prefetches source j + 1's
+      // first), written to the VST slab as soon as it is formed -- the fully
+      // unrolled form crashes or spills (CP above); the inline loads left one
+      // L2 round trip per source exposed (J = 8, K = 128: 6.85 ms)
+      slab_fence0();   // the previous tile's last reads before these writes
+      constexpr int CH = 8, CPS = NKS / CH;
+      double ta[2][CH], wa[2][CH];
+      auto ld = [&](int j, int s0, int sl) {
 #pragma unroll
-      for (int s = 0; s < 3; ++s)
-        if (tr + s + (s >= wvu) < te)
+        for (int c = 0; c < CH; ++c) {
+          ta[sl][c] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * (s0 + c)) * a.Tp) * 8u);
+          wa[sl][c] = a.Wkf[lofs + ((size_t)j * KP + tq + 4 * (s0 + c)) * a.Fp + f];
+        }
+      };
+      ld(0, 0, 0);
+#pragma unroll 1
+      for (int j = 0; j < J; ++j) {
+        d4 vj = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) av[s][i] = rx[(4 * s + i) * 64];
-    }
-    // ... and read, before any wave writes the next round's
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (FBF_DBG == 2 && wvu < J) {
-      for (int s = 0; s < 4; ++s) {
-        const int tv = tr + (s == 3 ? wvu : s + (s >= wvu));
-        if (tv < te)
-          for (int i = 0; i < 4; ++i)
-            for (int n = 0; n < NKC; ++n) fba[n][i] += (s == 3 ? own[i] : av[s < 3 ? s : 0][i]) + bo[s][i][n];
+        for (int c = 0; c < CPS; ++c) {
+          const int sl = c & 1;
+          if (c + 1 < CPS)
+            ld(j, (c + 1) * CH, sl ^ 1);
+          else if (j + 1 < J)
+            ld(j + 1, 0, sl ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cc = 0; cc < CH; ++cc) vj = mfma4(ta[sl][cc], wa[sl][cc], vj);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] = vj[i];
       }
-    }
-    if (FBF_DBG == 0 && wvu < J) {
+    } else if constexpr (VR) {
+      // source j + 1's TW operands in flight while source j's MFMAs run; the
+      // barriers keep the scheduler from hoisting every source's loads (at
+      // K = 64 / 128 they alone would fill the register file)
+      // (W from L2 at K = 128, J = 8: no prefetch, or the operands alone spill)
+      constexpr bool PFS = WL || NKS <= 16;
+      double tn[NKS];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int tv = tr + (s == 3 ? wvu : s + (s >= wvu));
-        if (tv < te)
+      for (int s = 0; s < NKS; ++s) tn[s] = twv[0][s];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int n = 0; n < NKC; ++n)
-              fba[n] = mfma4(s == 3 ? own[i] : av[s < 3 ? s : 0][i], bo[s][i][n], fba[n]);
-      }
-    }
-  };
-  // (FBF: every wave takes part in every round's barriers, tile or not)
-  const int nround = (te - tb + 3) >> 2;
-  for (int rr = 0, tt = tb + wvu; FBF ? rr < nround : tt < te; ++rr, tt += 4) {
-    // (FBF: a wave with no tile in the last round still takes part in its
-    // barriers and contracts the other waves' tiles)
-    if (!FBF || tt < te) {
-      const int t0 = tt * 16;
-      int lofs = 0;  // launder: re-read the loop-invariant LDS data per tile
-      asm volatile("" : "+v"(lofs));
-      // all TW operands in flight before the first MFMA (the scheduler would
-      // otherwise pair each load with its MFMA and wait on every one); with more
-      // than 32 operands (J > 4 or K > 32 at J = 4) the sources beyond the first
-      // 32 operands load next to their own MFMAs
-      // (VR: none up front -- the V loop below pipelines them source by source)
-      // CP: more operands than that (J <= 4 at K >= 64): the V tiles as one
-      // pipeline of 8-MFMA chunks over (source, k), each chunk's TW operands
-      // issued two chunks ahead -- the per-source inline loads left each
-      // source's load latency exposed (J = 4, K = 128: 2.70 ms).  (The same
-      // pipeline for the VR loop with W from L2, J > 4 at K = 128, crashes
-      // ROCm 7.2's compiler at distance 2 and spills 0.4-1.8 KB per lane at 1.)
-      constexpr bool CP = !VR && J * NKS > 32;
-      constexpr int JA = (VR || CP) ? 1 : (J * NKS <= 32) ? J : (32 / NKS > 0 ? 32 / NKS : 1);
-      double twv[JA][NKS];
-#pragma unroll
-      for (int j = 0; j < (CP ? 0 : JA); ++j) {
-        const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
+      for (int j = 0; j < J; ++j) {
+        double tc[NKS];
 #pragma unroll
         for (int s = 0; s < NKS; ++s)
-          twv[j][s] = SA ? es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u)
-                         : tw[(size_t)(4 * s) * a.Tp];
-      }
-      if constexpr (!CXE) load_cx(tt, cxv);  // this tile's Cx (in flight with the TW operands)
-      __builtin_amdgcn_sched_barrier(0);
-      d4 v[J];
-      if constexpr (CP) {
-        constexpr int CH = 8, CPS = NKS / CH, NCH = J * CPS, PD = 2;   // chunks, prefetch distance
-        static_assert(NKS % CH == 0, "k chunks of 8");
-        double ta[PD + 1][CH], wa[PD + 1][WL ? 1 : CH];
-        auto ld = [&](int u, int sl) {
-          const int j = u / CPS, s0 = (u % CPS) * CH;
-#pragma unroll
-          for (int c = 0; c < CH; ++c) {
-            const int s = s0 + c;
-            ta[sl][c] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u);
-            if constexpr (!WL)
-              wa[sl][c] = a.Wkf[lofs + ((size_t)j * KP + tq + 4 * s) * a.Fp + f];
-          }
-        };
-#pragma unroll
-        for (int u = 0; u < PD; ++u) ld(u, u);
-#pragma unroll
-        for (int u = 0; u < NCH; ++u) {
-          if (u + PD < NCH) ld(u + PD, (u + PD) % (PD + 1));
-          __builtin_amdgcn_sched_barrier(0);
-          const int j = u / CPS, s0 = (u % CPS) * CH, sl = u % (PD + 1);
-          if (s0 == 0) v[j] = d4{0.0, 0.0, 0.0, 0.0};
-          const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
-#pragma unroll
-          for (int c = 0; c < CH; ++c)
-            v[j] = mfma4(ta[sl][c], WL ? sw[4 * (s0 + c) * 16] : wa[sl][WL ? 0 : c], v[j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else if constexpr (VR && !(WL || NKS <= 16)) {
-        // J > 4 at K = 128 (W from L2): a runtime loop over the sources, each
-        // source's V tile a 4-chunk pipeline of 8 MFMAs with the next chunk's TW
-        // and W operands in flight (the last chunk prefetches source j + 1's
-        // first), written to the VST slab as soon as it is formed -- the fully
-        // unrolled form crashes or spills (CP above); the inline loads left one
-        // L2 round trip per source exposed (J = 8, K = 128: 6.85 ms)
-        slab_fence0();   // the previous tile's last reads before these writes
-        constexpr int CH = 8, CPS = NKS / CH;
-        double ta[2][CH], wa[2][CH];
-        auto ld = [&](int j, int s0, int sl) {
-#pragma unroll
-          for (int c = 0; c < CH; ++c) {
-            ta[sl][c] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * (s0 + c)) * a.Tp) * 8u);
-            wa[sl][c] = a.Wkf[lofs + ((size_t)j * KP + tq + 4 * (s0 + c)) * a.Fp + f];
-          }
-        };
-        ld(0, 0, 0);
-#pragma unroll 1
-        for (int j = 0; j < J; ++j) {
-          d4 vj = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int c = 0; c < CPS; ++c) {
-            const int sl = c & 1;
-            if (c + 1 < CPS)
-              ld(j, (c + 1) * CH, sl ^ 1);
-            else if (j + 1 < J)
-              ld(j + 1, 0, sl ^ 1);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int cc = 0; cc < CH; ++cc) vj = mfma4(ta[sl][cc], wa[sl][cc], vj);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] = vj[i];
-        }
-      } else if constexpr (VR) {
-        // source j + 1's TW operands in flight while source j's MFMAs run; the
-        // barriers keep the scheduler from hoisting every source's loads (at
-        // K = 64 / 128 they alone would fill the register file)
-        // (W from L2 at K = 128, J = 8: no prefetch, or the operands alone spill)
-        constexpr bool PFS = WL || NKS <= 16;
-        double tn[NKS];
-#pragma unroll
-        for (int s = 0; s < NKS; ++s) tn[s] = twv[0][s];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          double tc[NKS];
+          tc[s] = PFS || j == 0 ? tn[s]
+                               : es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u);
+        if (PFS && j + 1 < J) {
 #pragma unroll
           for (int s = 0; s < NKS; ++s)
-            tc[s] = PFS || j == 0 ? tn[s]
-                                 : es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)((j * KP + 4 * s) * a.Tp) * 8u);
-          if (PFS && j + 1 < J) {
-#pragma unroll
-            for (int s = 0; s < NKS; ++s)
-              tn[s] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)(((j + 1) * KP + 4 * s) * a.Tp) * 8u);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          v[j] = d4{0.0, 0.0, 0.0, 0.0};
-          const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
-          const double *gw = a.Wkf + lofs + ((size_t)j * KP + tq) * a.Fp + f;
-#pragma unroll
-          for (int s = 0; s < NKS; ++s)
-            v[j] = mfma4(tc[s], WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
-          __builtin_amdgcn_sched_barrier(0);
+            tn[s] = es_ld<0>(es_rsrc(a.TW + t0), vo_tw, (unsigned)(((j + 1) * KP + 4 * s) * a.Tp) * 8u);
         }
-      }
-#pragma unroll
-      for (int j = 0; j < ((VR || CP) ? 0 : J); ++j) {
+        __builtin_amdgcn_sched_barrier(0);
         v[j] = d4{0.0, 0.0, 0.0, 0.0};
         const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
         const double *gw = a.Wkf + lofs + ((size_t)j * KP + tq) * a.Fp + f;
-        const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
         for (int s = 0; s < NKS; ++s)
-          v[j] = mfma4(j < JA ? twv[j < JA ? j : 0][s] : tw[(size_t)(4 * s) * a.Tp],
-                       WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
+          v[j] = mfma4(tc[s], WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (VST && (WL || NKS <= 16)) {   // (else written by the loop above)
-        slab_fence0();   // the previous tile's last reads before these writes
+    }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < ((VR || CP) ? 0 : J); ++j) {
+      v[j] = d4{0.0, 0.0, 0.0, 0.0};
+      const double *sw = s_w + lofs + (j * KP + tq) * 16 + fl;
+      const double *gw = a.Wkf + lofs + ((size_t)j * KP + tq) * a.Fp + f;
+      const double *tw = a.TW + ((size_t)j * KP + tq) * a.Tp + t0 + fl;
 #pragma unroll
-          for (int j = 0; j < J; ++j) wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] = v[j][i];
+      for (int s = 0; s < NKS; ++s)
+        v[j] = mfma4(j < JA ? twv[j < JA ? j : 0][s] : tw[(size_t)(4 * s) * a.Tp],
+                     WL ? sw[4 * s * 16] : gw[(size_t)(4 * s) * a.Fp], v[j]);
+    }
+    if constexpr (VST && (WL || NKS <= 16)) {   // (else written by the loop above)
+      slab_fence0();   // the previous tile's last reads before these writes
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j) wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] = v[j][i];
+    }
+    const double *cj = s_cj + lofs + fl;
+    // the lane's Sigma_x coefficients: LDS (re-read per tile) or, with
+    // CJR, the registers loaded once per kernel
+    auto cjv = [&](int j, int c) { return CJR ? cjr[j][c] : cj[(j * 4 + c) * 16]; };
+    // point i of the lane's four (frame t0 + tq + 4 i): Sigma_x, its guarded
+    // inverse, loglik, P = Cx S, N = S Cx S - S, and rho stored; no LDS
+    auto pt_valu = [&](int i, double (&P)[8], double (&N)[4]) {
+      const int t = t0 + tq + 4 * i;
+      const double x00 = cxv[0][i], x11 = cxv[1][i], xr = cxv[2][i], xi = cxv[3][i];
+      double V[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) V[j] = VST ? wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] : v[j][i];
+      // Sigma_x = sum_r V_r a_r a_r^H + PSD I   (compute_suff_stat :613-652)
+      double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        d0 += cjv(j, 0) * V[j];
+        d1 += cjv(j, 1) * V[j];
+        ore += cjv(j, 2) * V[j];
+        oim += cjv(j, 3) * V[j];
       }
-      const double *cj = s_cj + lofs + fl;
-      // the lane's Sigma_x coefficients: LDS (re-read per tile) or, with
-      // CJR, the registers loaded once per kernel
-      auto cjv = [&](int j, int c) { return CJR ? cjr[j][c] : cj[(j * 4 + c) * 16]; };
-      // point i of the lane's four (frame t0 + tq + 4 i): Sigma_x, its guarded
-      // inverse, loglik, P = Cx S, N = S Cx S - S, and rho stored; no LDS
-      auto pt_valu = [&](int i, double (&P)[8], double (&N)[4]) {
-        const int t = t0 + tq + 4 * i;
-        const double x00 = cxv[0][i], x11 = cxv[1][i], xr = cxv[2][i], xi = cxv[3][i];
-        double V[J];
+      // inv_herm_mat_2d (signalTools.py:177-194)
+      double det = d0 * d1 - (ore * ore + oim * oim);
+      const double dg = det + kEps;
+      const double sg = dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0);
+      det = sg * fmax(fabs(det), kEps);
+      const double rdet = rcp_nr(det);
+      const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
+      if (fvalid && t < a.T) {
+        // log(det pi) as mantissa product x 2^exponent (v_frexp_*: 0, inf and
+        // NaN pass through the mantissa, so log(lm) gives -inf / inf / NaN as
+        // log() would; a negative det, which the guard only lets through for
+        // a Sigma_x that is not positive semi-definite, is flagged in xmin)
+        const double x = det * M_PI;
+        lev += (double)__builtin_amdgcn_frexp_exp(x);
+        lm *= __builtin_amdgcn_frexp_mant(x);
+        xmin = fmin(xmin, x);
+        ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
+      }
+      // P = Cx S, N = S Cx S - S = P^H S - S
+      P[0] = x00 * i0 + xr * ior + xi * ioi;   // p00r
+      P[1] = xi * ior - xr * ioi;              // p00i
+      P[2] = x00 * ior + xr * i1;              // p01r
+      P[3] = x00 * ioi + xi * i1;              // p01i
+      P[4] = xr * i0 + x11 * ior;              // p10r
+      P[5] = -xi * i0 - x11 * ioi;             // p10i
+      P[6] = xr * ior + xi * ioi + x11 * i1;   // p11r
+      P[7] = xr * ioi - xi * ior;              // p11i
+      N[0] = P[0] * i0 + (P[4] * ior - P[5] * ioi) - i0;          // n00
+      N[1] = (P[2] * ior + P[3] * ioi) + P[6] * i1 - i1;          // n11
+      N[2] = P[0] * ior + P[1] * ioi + P[4] * i1 - ior;           // n01r
+      N[3] = P[0] * ioi - P[1] * ior - P[5] * i1 - ioi;           // n01i
+      // hat_W[j] = mean over the ranks of j of |V^2 a_r^H N a_r + V| (:727-729,
+      // :413-414) in the rank-merged form |V^2 (sum_r a_r^H N a_r) / rk + V|
+      // (each rank's term is a posterior second moment, >= 0: the two forms
+      // differ by rounding), with sum_r a_r^H N a_r = tr(N sum_r a_r a_r^H) from
+      // the Sigma_x coefficients; stored as rho = (hat_W / vm^2) vm,
+      // vm = max(V, eps): the FB ratio of update_spectral_components
+      // (:1521-1575, N1), formed where V is at hand
+      // Since V >= 0, rho = |V^2 q + V| / max(V, eps) = |V q + 1| min(V / eps, 1)
+      // (q = a^H N a / rk): no reciprocal (the two forms differ by rounding)
+      // NF: the factors 2 (the off-diagonal pair) and 1 / rk (a uniform rank)
+      // folded into N once per point instead of once per source
+      double Nf[4];
+      {
+        const double ir = RKU ? 1.0 / (double)RKU : 1.0;
+        Nf[0] = N[0] * ir;
+        Nf[1] = N[1] * ir;
+        Nf[2] = N[2] * (2.0 * ir);
+        Nf[3] = N[3] * (2.0 * ir);
+      }
 #pragma unroll
-        for (int j = 0; j < J; ++j) V[j] = VST ? wrv[i * 4 * S::VGS + (j >> 2) * 64 + (j & 3)] : v[j][i];
-        // Sigma_x = sum_r V_r a_r a_r^H + PSD I   (compute_suff_stat :613-652)
-        double d0 = psd, d1 = psd, ore = 0.0, oim = 0.0;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          d0 += cjv(j, 0) * V[j];
-          d1 += cjv(j, 1) * V[j];
-          ore += cjv(j, 2) * V[j];
-          oim += cjv(j, 3) * V[j];
+      for (int j = 0; j < J; ++j) {
+        const double Vj = V[j];
+        double q;
+        if constexpr (NF) {
+          q = cjv(j, 0) * Nf[0] + cjv(j, 1) * Nf[1] + cjv(j, 2) * Nf[2] + cjv(j, 3) * Nf[3];
+          if constexpr (RKU == 0) q *= inv_rk[j];
+        } else {
+          const double qa = (cjv(j, 0) * N[0] + cjv(j, 1) * N[1]) +
+                            2.0 * (cjv(j, 2) * N[2] + cjv(j, 3) * N[3]);
+          q = RKU == 1 ? qa : qa * inv_rk[j];
         }
-        // inv_herm_mat_2d (signalTools.py:177-194)
-        double det = d0 * d1 - (ore * ore + oim * oim);
-        const double dg = det + kEps;
-        const double sg = dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0);
-        det = sg * fmax(fabs(det), kEps);
-        const double rdet = rcp_nr(det);
-        const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
-        if (fvalid && t < a.T) {
-          // log(det pi) as mantissa product x 2^exponent (v_frexp_*: 0, inf and
-          // NaN pass through the mantissa, so log(lm) gives -inf / inf / NaN as
-          // log() would; a negative det, which the guard only lets through for
-          // a Sigma_x that is not positive semi-definite, is flagged in xmin)
-          const double x = det * M_PI;
-          lev += (double)__builtin_amdgcn_frexp_exp(x);
-          lm *= __builtin_amdgcn_frexp_mant(x);
-          xmin = fmin(xmin, x);
-          ll += i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi);
-        }
-        // P = Cx S, N = S Cx S - S = P^H S - S
-        P[0] = x00 * i0 + xr * ior + xi * ioi;   // p00r
-        P[1] = xi * ior - xr * ioi;              // p00i
-        P[2] = x00 * ior + xr * i1;              // p01r
-        P[3] = x00 * ioi + xi * i1;              // p01i
-        P[4] = xr * i0 + x11 * ior;              // p10r
-        P[5] = -xi * i0 - x11 * ioi;             // p10i
-        P[6] = xr * ior + xi * ioi + x11 * i1;   // p11r
-        P[7] = xr * ioi - xi * ior;              // p11i
-        N[0] = P[0] * i0 + (P[4] * ior - P[5] * ioi) - i0;          // n00
-        N[1] = (P[2] * ior + P[3] * ioi) + P[6] * i1 - i1;          // n11
-        N[2] = P[0] * ior + P[1] * ioi + P[4] * i1 - ior;           // n01r
-        N[3] = P[0] * ioi - P[1] * ior - P[5] * i1 - ioi;           // n01i
-        // hat_W[j] = mean over the ranks of j of |V^2 a_r^H N a_r + V| (:727-729,
-        // :413-414) in the rank-merged form |V^2 (sum_r a_r^H N a_r) / rk + V|
-        // (each rank's term is a posterior second moment, >= 0: the two forms
-        // differ by rounding), with sum_r a_r^H N a_r = tr(N sum_r a_r a_r^H) from
-        // the Sigma_x coefficients; stored as rho = (hat_W / vm^2) vm,
-        // vm = max(V, eps): the FB ratio of update_spectral_components
-        // (:1521-1575, N1), formed where V is at hand
-        // Since V >= 0, rho = |V^2 q + V| / max(V, eps) = |V q + 1| min(V / eps, 1)
-        // (q = a^H N a / rk): no reciprocal (the two forms differ by rounding)
-        // NF: the factors 2 (the off-diagonal pair) and 1 / rk (a uniform rank)
-        // folded into N once per point instead of once per source
-        double Nf[4];
-        {
-          const double ir = RKU ? 1.0 / (double)RKU : 1.0;
-          Nf[0] = N[0] * ir;
-          Nf[1] = N[1] * ir;
-          Nf[2] = N[2] * (2.0 * ir);
-          Nf[3] = N[3] * (2.0 * ir);
-        }
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          const double Vj = V[j];
-          double q;
-          if constexpr (NF) {
-            q = cjv(j, 0) * Nf[0] + cjv(j, 1) * Nf[1] + cjv(j, 2) * Nf[2] + cjv(j, 3) * Nf[3];
-            if constexpr (RKU == 0) q *= inv_rk[j];
-          } else {
-            const double qa = (cjv(j, 0) * N[0] + cjv(j, 1) * N[1]) +
-                              2.0 * (cjv(j, 2) * N[2] + cjv(j, 3) * N[3]);
-            q = RKU == 1 ? qa : qa * inv_rk[j];
-          }
-          const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
-          if constexpr (SA)
-            es_st<2>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
-                                 (unsigned)(4 * i * a.Fp) * 8u);
-          else
-            __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
-          if constexpr (FBF) {   // source j's owner gets it through the area
-            if (j == wvu) {
-              own[i] = val;
-            } else {
-              // (the lane offset laundered per point: one VGPR, the slot
-              // offset added from an SGPR at the store, not four hoisted
-              // per-source addresses)
-              unsigned fo = (unsigned)lane * 8u;
-              asm volatile("" : "+v"(fo));
-              const unsigned so = (unsigned)(((j * 3 + (wvu < j ? wvu : wvu - 1)) * 4 + i) * 64 * 8);
-              *(double *)((char *)s_fbx + (fo + so)) = val;
-            }
-          }
-        }
-      };
-      // point i's MFMA operands -> the wave's slab (reader layout)
-      auto pt_write = [&](int i, const double (&P)[8], const double (&N)[4]) {
-        if constexpr (VST) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            wpn[0 * 64 + c] = P[c];
-            wpn[1 * 64 + c] = P[4 + c];
-            wpn[2 * 64 + c] = N[c];
-          }
-          return;
-        }
-        double V[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) V[j] = v[j][i];
-#pragma unroll
-        for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
+        const double val = fabs(fma(Vj, q, 1.0)) * fmin(Vj * (1.0 / kEps), 1.0);
+        if constexpr (SA)
+          es_st<2>(val, es_rsrc(a.hatW + ((size_t)j * a.Tp + t0) * a.Fp), vo_cx,
+                               (unsigned)(4 * i * a.Fp) * 8u);
+        else
+          __builtin_nontemporal_store(val, a.hatW + ((size_t)j * a.Tp + t) * a.Fp + f);
+      }
+    };
+    // point i's MFMA operands -> the wave's slab (reader layout)
+    auto pt_write = [&](int i, const double (&P)[8], const double (&N)[4]) {
+      if constexpr (VST) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          wr[(S::SP + 0) * 64 + c] = P[c];
-          wr[(S::SP + 1) * 64 + c] = P[4 + c];
-          wr[S::SN * 64 + c] = N[c];
+          wpn[0 * 64 + c] = P[c];
+          wpn[1 * 64 + c] = P[4 + c];
+          wpn[2 * 64 + c] = N[c];
         }
-        if constexpr (!RP) {
-          int p = 0;
+        return;
+      }
+      double V[J];
 #pragma unroll
-          for (int j1 = 0; j1 < J; ++j1)
+      for (int j = 0; j < J; ++j) V[j] = v[j][i];
 #pragma unroll
-            for (int j2 = j1; j2 < J; ++j2, ++p)
-              wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
-        }
-      };
-      // SWP (J >= 4): the next point's VALU work sits between this point's slab
-      // reads and its MFMAs (J = 4 with the reader-formed pairs: 0.370 -> 0.367
-      // ms alone, 0.373 -> 0.3625 with CJR; with the writer-formed pairs it was
-      // neutral; at J > 4 the unpipelined form also tripped ROCm 7.2's
-      // AGPR-copy rewrite pass)
-      constexpr bool SWP = J >= 4;
+      for (int j = 0; j < J; ++j) wr[(j >> 2) * 64 + (j & 3)] = V[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        wr[(S::SP + 0) * 64 + c] = P[c];
+        wr[(S::SP + 1) * 64 + c] = P[4 + c];
+        wr[S::SN * 64 + c] = N[c];
+      }
+      if constexpr (!RP) {
+        int p = 0;
+#pragma unroll
+        for (int j1 = 0; j1 < J; ++j1)
+#pragma unroll
+          for (int j2 = j1; j2 < J; ++j2, ++p)
+            wr[(S::SV2 + (p >> 2)) * 64 + (p & 3)] = V[j1] * V[j2];
+      }
+    };
+    // SWP (J >= 4): the next point's VALU work sits between this point's slab
+    // reads and its MFMAs (J = 4 with the reader-formed pairs: 0.370 -> 0.367
+    // ms alone, 0.373 -> 0.3625 with CJR; with the writer-formed pairs it was
+    // neutral; at J > 4 the unpipelined form also tripped ROCm 7.2's
+    // AGPR-copy rewrite pass)
+    constexpr bool SWP = J >= 4;
 
-      auto slab_fence = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      };
-      // the slab's operands of the 4 bin groups in flight at once, then the
-      // MFMAs (read -> wait -> MFMA one at a time left the LDS latency exposed);
-      // with SWP the next point's VALU work sits between the reads and the
-      // MFMAs (its slab writes after them)
-      auto mfma_pass = [&](int i, auto between) {
-        if constexpr (VST) {
-          // the bin groups in two halves (half the operands live)
+    auto slab_fence = [&]() {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // the slab's operands of the 4 bin groups in flight at once, then the
+    // MFMAs (read -> wait -> MFMA one at a time left the LDS latency exposed);
+    // with SWP the next point's VALU work sits between the reads and the
+    // MFMAs (its slab writes after them)
+    auto mfma_pass = [&](int i, auto between) {
+      if constexpr (VST) {
+        // the bin groups in two halves (half the operands live)
 #pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            double w[2][Q], pn[2][3];
+        for (int hh = 0; hh < 2; ++hh) {
+          double w[2][Q], pn[2][3];
 #pragma unroll
-            for (int g2 = 0; g2 < 2; ++g2) {
-              const int g = 2 * hh + g2;
+          for (int g2 = 0; g2 < 2; ++g2) {
+            const int g = 2 * hh + g2;
 #pragma unroll
-              for (int e = 0; e < Q; ++e) w[g2][e] = rdq[(4 * i + g) * S::VGS + vro[e]];
+            for (int e = 0; e < Q; ++e) w[g2][e] = rdq[(4 * i + g) * S::VGS + vro[e]];
 #pragma unroll
-              for (int q = 0; q < 3; ++q) pn[g2][q] = rpn[g * S::PGS + q * 64];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (hh == 0) {
-              between();
-              __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int g2 = 0; g2 < 2; ++g2) {
-              const int g = 2 * hh + g2;
-#pragma unroll
-              for (int vg = 0; vg < NVG; ++vg) {
-                xacc[g][vg][0] = mfma44(w[g2][4 * vg], pn[g2][0], xacc[g][vg][0]);
-                xacc[g][vg][1] = mfma44(w[g2][4 * vg], pn[g2][1], xacc[g][vg][1]);
-              }
-#pragma unroll
-              for (int h = 0; h < NPG; ++h)
-                if (rp_live<J>(h))
-                  pacc[g][h] = mfma44(w[g2][rp_base<Q>(h)] * w[g2][(rp_base<Q>(h) + rp_d<Q>(h)) & (Q - 1)],
-                                      pn[g2][2], pacc[g][h]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          return;
-        }
-        if constexpr (RP) {
-          // rotated sources W_e, then P lo / hi and N, of the 4 bin groups
-          double w[4][Q], pn[4][3];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-#pragma unroll
-            for (int e = 0; e < Q; ++e) w[g][e] = rdq[g * S::GS + vro[e]];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) pn[g][q] = rd[g * S::GS + (S::SP + q) * 64];
+            for (int q = 0; q < 3; ++q) pn[g2][q] = rpn[g * S::PGS + q * 64];
           }
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (SWP) {
+          if (hh == 0) {
             between();
             __builtin_amdgcn_sched_barrier(0);
           }
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
+          for (int g2 = 0; g2 < 2; ++g2) {
+            const int g = 2 * hh + g2;
 #pragma unroll
             for (int vg = 0; vg < NVG; ++vg) {
-              xacc[g][vg][0] = mfma44(w[g][4 * vg], pn[g][0], xacc[g][vg][0]);
-              xacc[g][vg][1] = mfma44(w[g][4 * vg], pn[g][1], xacc[g][vg][1]);
+              xacc[g][vg][0] = mfma44(w[g2][4 * vg], pn[g2][0], xacc[g][vg][0]);
+              xacc[g][vg][1] = mfma44(w[g2][4 * vg], pn[g2][1], xacc[g][vg][1]);
             }
 #pragma unroll
             for (int h = 0; h < NPG; ++h)
               if (rp_live<J>(h))
-                pacc[g][h] = mfma44(w[g][rp_base<Q>(h)] * w[g][(rp_base<Q>(h) + rp_d<Q>(h)) & (Q - 1)],
-                                    pn[g][2], pacc[g][h]);
+                pacc[g][h] = mfma44(w[g2][rp_base<Q>(h)] * w[g2][(rp_base<Q>(h) + rp_d<Q>(h)) & (Q - 1)],
+                                    pn[g2][2], pacc[g][h]);
           }
-          return;
+          __builtin_amdgcn_sched_barrier(0);
         }
-        double opd[4][S::NSET];
+        return;
+      }
+      if constexpr (RP) {
+        // rotated sources W_e, then P lo / hi and N, of the 4 bin groups
+        double w[4][Q], pn[4][3];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+        for (int g = 0; g < 4; ++g) {
 #pragma unroll
-          for (int q = 0; q < S::NSET; ++q) opd[g][q] = rd[g * S::GS + q * 64];
+          for (int e = 0; e < Q; ++e) w[g][e] = rdq[g * S::GS + vro[e]];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) pn[g][q] = rd[g * S::GS + (S::SP + q) * 64];
+        }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (SWP) {
           between();
@@ -988,54 +855,69 @@ void k_estep_mx(const EArgs a) {
         for (int g = 0; g < 4; ++g) {
 #pragma unroll
           for (int vg = 0; vg < NVG; ++vg) {
-            xacc[g][vg][0] = mfma44(opd[g][vg], opd[g][S::SP], xacc[g][vg][0]);
-            xacc[g][vg][1] = mfma44(opd[g][vg], opd[g][S::SP + 1], xacc[g][vg][1]);
+            xacc[g][vg][0] = mfma44(w[g][4 * vg], pn[g][0], xacc[g][vg][0]);
+            xacc[g][vg][1] = mfma44(w[g][4 * vg], pn[g][1], xacc[g][vg][1]);
           }
 #pragma unroll
           for (int h = 0; h < NPG; ++h)
-            pacc[g][h] = mfma44(opd[g][S::SV2 + h], opd[g][S::SN], pacc[g][h]);
+            if (rp_live<J>(h))
+              pacc[g][h] = mfma44(w[g][rp_base<Q>(h)] * w[g][(rp_base<Q>(h) + rp_d<Q>(h)) & (Q - 1)],
+                                  pn[g][2], pacc[g][h]);
         }
-      };
-      if constexpr (SWP) {
-        double Pc[8], Nc[4];
-        pt_valu(0, Pc, Nc);
-        pt_write(0, Pc, Nc);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          slab_fence();   // point i's slab writes land before the cross-lane reads
-          double Pn[8], Nn[4];
-          mfma_pass(i, [&]() {
-            if (i < 3) pt_valu(i + 1, Pn, Nn);
-            if (CXE && i == 2 && tt + 4 < te) load_cx(tt + 4, cxv);
-          });
-          slab_fence();   // point i + 1's writes must not overtake point i's reads
-          if (i < 3) pt_write(i + 1, Pn, Nn);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          double P[8], N[4];
-          pt_valu(i, P, N);
-          pt_write(i, P, N);
-          slab_fence();   // the slab writes land before the cross-lane reads
-          mfma_pass(i, []() {});
-          slab_fence();   // the next point's writes must not overtake these reads
-        }
+        return;
       }
-      // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
-      lev += (double)__builtin_amdgcn_frexp_exp(lm);
-      lm = __builtin_amdgcn_frexp_mant(lm);
+      double opd[4][S::NSET];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int q = 0; q < S::NSET; ++q) opd[g][q] = rd[g * S::GS + q * 64];
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SWP) {
+        between();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int vg = 0; vg < NVG; ++vg) {
+          xacc[g][vg][0] = mfma44(opd[g][vg], opd[g][S::SP], xacc[g][vg][0]);
+          xacc[g][vg][1] = mfma44(opd[g][vg], opd[g][S::SP + 1], xacc[g][vg][1]);
+        }
+#pragma unroll
+        for (int h = 0; h < NPG; ++h)
+          pacc[g][h] = mfma44(opd[g][S::SV2 + h], opd[g][S::SN], pacc[g][h]);
+      }
+    };
+    if constexpr (SWP) {
+      double Pc[8], Nc[4];
+      pt_valu(0, Pc, Nc);
+      pt_write(0, Pc, Nc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        slab_fence();   // point i's slab writes land before the cross-lane reads
+        double Pn[8], Nn[4];
+        mfma_pass(i, [&]() {
+          if (i < 3) pt_valu(i + 1, Pn, Nn);
+          if (CXE && i == 2 && tt + 4 < te) load_cx(tt + 4, cxv);
+        });
+        slab_fence();   // point i + 1's writes must not overtake point i's reads
+        if (i < 3) pt_write(i + 1, Pn, Nn);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double P[8], N[4];
+        pt_valu(i, P, N);
+        pt_write(i, P, N);
+        slab_fence();   // the slab writes land before the cross-lane reads
+        mfma_pass(i, []() {});
+        slab_fence();   // the next point's writes must not overtake these reads
+      }
     }
-    if constexpr (FBF) fb_round(tb + 4 * rr);
+    // keep lm in [0.5, 1): at most 4 factors >= 0.5 were multiplied in
+    lev += (double)__builtin_amdgcn_frexp_exp(lm);
+    lm = __builtin_amdgcn_frexp_mant(lm);
   }
-  if constexpr (FBF)
-    if (wvu < J) {   // source wvu's numerator partial of this frame chunk
-      double *o = a.fbnum + (((size_t)(a.ybase + bi.y) * J + wvu) * a.Fp + f0 + tq) * KP + fl;
-#pragma unroll
-      for (int n = 0; n < NKC; ++n)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) o[(size_t)(4 * m) * KP + 16 * n] = fba[n][m];
-    }
   ll += (log(lm) + lev * M_LN2) + (xmin < 0.0 ? NAN : 0.0);
 
   // epilogue: lane (X = m, b, Y = n) holds, per bin group g, the 4x4 blocks
@@ -3371,6 +3253,30 @@ static int best_split(long unit, long cap, int max_split) {
   return 1;
 }
 
+// Dynamic-LDS ceilings of the kernels whose launches may pass the 64 KB
+// default, raised once per model configuration to the most any structure asks
+// of them (not per iteration: the sizes depend only on the model shape, and
+// a ceiling above a launch's own size costs nothing)
+static int set_lds_limits() {
+  struct L {
+    const void *f;
+    size_t bytes;
+  };
+  const L lim[] = {
+      {(const void *)k_fw_reduce, (size_t)3 * 32 * kMaxKP * sizeof(double)},
+      {(const void *)k_fwh_t<true>, (size_t)(16 + 64) * kMaxKP * sizeof(double)},
+      {(const void *)k_egen_stats, (size_t)(kMaxJ + 12) * 256 * sizeof(double)},
+      {(const void *)k_mix<(4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64, (kMaxR * kMaxR + 63) / 64>,
+       mix_smem(kMaxJ, kMaxR, kMaxKP, 4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ)},
+  };
+  for (const L &l : lim)
+    if (hipFuncSetAttribute(l.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l.bytes) != hipSuccess) {
+      set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize, %zu) failed", l.bytes);
+      return FASST_ERR_DEVICE;
+    }
+  return FASST_OK;
+}
+
 int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const int *convj) {
   if (J < 1 || J > kMaxJ) {
     set_error("J=%d outside the HIP path (1..%d sources)", J, kMaxJ);
@@ -3390,6 +3296,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
               kMaxKP);
     return FASST_ERR_UNSUPPORTED;
   }
+  if (int st = set_lds_limits()) return st;
   c->J = J;
   c->R = R;
   c->convm = 0;
@@ -3498,9 +3405,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   // (+8 chunks: the interleaved E-step / FB ranges round their chunks up)
   ALLOC(epart, (size_t)(c->nchunk_e + 8) * Fp * c->nacc);
   ALLOC(llpart, (size_t)(c->nchunk_e + 8) * c->nft);
-  // (the FB numerator partials: nchunk_b chunks from k_fb_contract, or
-  // nchunk_e from the E-step's fused form)
-  ALLOC(bnum, (size_t)(std::max(c->nchunk_b, c->nchunk_e) + 8) * J * Fp * KP);
+  ALLOC(bnum, (size_t)(c->nchunk_b + 8) * J * Fp * KP);
   // FW update (free FW only, allocated with the model so set_spectral may switch it on)
   ALLOC(gden, (size_t)c->nchunk_b * J * Fp * KP);
   ALLOC(TWt, (size_t)J * Tp * KP);
@@ -3708,9 +3613,20 @@ static int launch_renorm(fasst_ctx *c, int iter) {
   return FASST_OK;
 }
 
-// gem_iteration's fused tail (see k_renorm_scales): the single-component
-// path without time blobs or free FW.  Off unless FASST_FAST_TAIL=1 until it
-// has passed the GPU parity suite (built and reviewed, not yet run on a GPU)
+// gem_iteration's fused renormalisation tail (§3.3a of DESIGN.md; see
+// k_renorm_scales), the default for the structures it covers: one spectral
+// component per source (!multi), no time blobs (!anytb), no free FW.  The
+// context's ftail (FASST_FAST_TAIL, read at creation) selects the form:
+//   0  the unfused k_renorm_stats / _apply / _final (the A/B reference);
+//   1  the fused tail: k_fb_update's stage-1 statistics, k_renorm_scales /
+//      _rows and the next W on the side stream beside the TW contraction,
+//      the TW rescale inside k_tw_update, k_renorm_tail;
+//   2  (default) as 1, and at KP <= 64 k_tw_update also forms the next
+//      iteration's (FW.TW)^T and TW row-sum partials (reduced into hsum by
+//      k_renorm_tail), so the next iteration of the batch skips
+//      launch_spectral_prep.
+// Every form is tested against the others and the oracle, halted batches
+// included (tests/test_gpu_fast_tail.py).
 static bool fast_tail(const fasst_ctx *c) {
   if (!c->ftail || c->multi || c->anytb) return false;
   for (int j = 0; j < c->J; ++j)
@@ -3792,55 +3708,29 @@ static void estep_dispatch(const fasst_ctx *c, F &&f) {
   }
 }
 
-// the structures whose FB numerator the E-step contracts (k_estep_mx FBF):
-// one spectral component per source (the multi-block path forms its own
-// ratio planes), J <= 4 (a wave owns a source), KP <= 32
-static bool fbf_shape(const fasst_ctx *c) { return c->fbf && c->J <= 4 && c->KP <= 32; }
-static bool fbf_on(const fasst_ctx *c) { return fbf_shape(c) && !c->multi; }
-
-template <class T>
-static constexpr bool fbf_inst() {
-  return T::J <= 4 && T::NKS <= 8;
-}
-
-static void launch_estep(fasst_ctx *c, const EArgs &e, int ny, bool fbf) {
+static void launch_estep(fasst_ctx *c, const EArgs &e, int ny) {
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
     prof_begin(c, KESTEP);
-    if constexpr (fbf_inst<T>()) {
-      if (fbf) {
-        k_estep_mx<T::J, T::NKS, T::RKU, true>
-            <<<dim3(c->nft, ny), 256, estep_mx_smem<T::J, T::NKS, true>(), c->stream>>>(e);
-        prof_end(c, KESTEP);
-        return;
-      }
-    }
     k_estep_mx<T::J, T::NKS, T::RKU>
         <<<dim3(c->nft, ny), 256, estep_mx_smem<T::J, T::NKS>(), c->stream>>>(e);
     prof_end(c, KESTEP);
   });
 }
 
-// resident E-step blocks per CU (the lesser of the two forms where the
-// structure may take the fused FB numerator)
-template <int J, int NKS, int RKU, bool FBF>
-static int estep_occ_of() {
-  constexpr size_t smem = estep_mx_smem<J, NKS, FBF>();
-  (void)hipFuncSetAttribute((const void *)k_estep_mx<J, NKS, RKU, FBF>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_estep_mx<J, NKS, RKU, FBF>, 256, smem) !=
-      hipSuccess)
-    n = 1;
-  return std::max(1, n);
-}
+// resident E-step blocks per CU
 static int estep_occupancy(const fasst_ctx *c) {
   int occ = 1;
   estep_dispatch(c, [&](auto tag) {
     using T = decltype(tag);
-    occ = estep_occ_of<T::J, T::NKS, T::RKU, false>();
-    if constexpr (fbf_inst<T>())
-      if (fbf_shape(c)) occ = std::min(occ, estep_occ_of<T::J, T::NKS, T::RKU, true>());
+    constexpr size_t smem = estep_mx_smem<T::J, T::NKS>();
+    (void)hipFuncSetAttribute((const void *)k_estep_mx<T::J, T::NKS, T::RKU>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_estep_mx<T::J, T::NKS, T::RKU>, 256,
+                                                     smem) != hipSuccess)
+      n = 1;
+    occ = std::max(1, n);
   });
   return occ;
 }
@@ -3852,8 +3742,7 @@ constexpr int tpw_for() { return NKC > 4 ? 1 : kTPW; }
 static int tpw_of(const fasst_ctx *c) { return c->KP > 64 ? 1 : kTPW; }
 
 static void launch_fw_reduce(fasst_ctx *c, const FWArgs &w) {
-  const size_t lds = (size_t)3 * w.fpc * c->KP * sizeof(double);
-  (void)hipFuncSetAttribute((const void *)k_fw_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t lds = (size_t)3 * w.fpc * c->KP * sizeof(double);   // (ceiling: set_lds_limits)
   k_fw_reduce<<<dim3(w.nfc, c->J), 256, lds, c->stream>>>(w);
 }
 
@@ -4258,9 +4147,8 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
   prof_begin(c, KFWH, side);
   bool any_fw = false;
   for (int j = 0; j < J; ++j) any_fw |= c->fw_free[j] != 0;
-  if (c->KP > 64)   // 16-row FW chunk + TW tile: 80 KB of LDS (two blocks per CU)
-    FASST_HIP(hipFuncSetAttribute((const void *)k_fwh_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((16 + 64) * c->KP * sizeof(double))));
+  // (KP > 64: 16-row FW chunk + TW tile, 80 KB of LDS, two blocks per CU;
+  // ceiling set by set_lds_limits)
   (c->KP > 64 ? k_fwh_t<true> : k_fwh_t<false>)<<<dim3((c->Tp + 63) / 64, J), 256,
             c->KP > 64 ? (16 + 64) * c->KP * sizeof(double) : fw_lds(c, c->KP * 64),
             side>>>(c->FW.p, c->TW.p, c->FWHt.p, any_fw ? c->TWt.p : nullptr, J, c->Tp, c->KP,
@@ -4279,10 +4167,8 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
 // c->hatW (rho_j = hat_W_j / max(V_j, eps), V from the parameters before the
 // update), after launch_spectral_prep and launch_w_old.  tail (fast_tail
 // models inside gem_iteration): 1 = the fused renormalisation tail on the
-// main stream, 2 = its side-stream part forked beside the TW contraction.
-// fb_done: the E-step formed the FB numerator partials (k_estep_mx FBF, its
-// nchunk_e frame chunks), so k_fb_contract is skipped
-static int spectral_update(fasst_ctx *c, double omega, int tail = 0, bool fb_done = false) {
+// main stream, 2 = its side-stream part forked beside the TW contraction
+static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   const int J = c->J;
   const int nkc = c->KP / 16;
   bool any_fw = false;
@@ -4352,7 +4238,7 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0, bool fb_don
   u.Fp = c->Fp;
   u.KP = c->KP;
   u.J = J;
-  u.nchunk = fb_done ? c->nchunk_e : c->nchunk_b;
+  u.nchunk = c->nchunk_b;
   u.omega = omega;
   u.bden = nullptr;
   u.pmax = tail ? c->rpmax2.p : nullptr;
@@ -4381,15 +4267,13 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0, bool fb_don
     t.tw_free[j] = tu.tw_free[j] = in ? c->tw_free[j] : 0;
     u.fb_free[j] = in ? c->fb_free[j] : 0;
   }
-  if (!fb_done) {
-    switch (nkc) {
-      case 1: launch_contract<1>(c, b, t, true); break;
-      case 2: launch_contract<2>(c, b, t, true); break;
-      case 4: launch_contract<4>(c, b, t, true); break;
-      default: launch_contract<8>(c, b, t, true); break;
-    }
-    FASST_LAUNCH_CHECK();
+  switch (nkc) {
+    case 1: launch_contract<1>(c, b, t, true); break;
+    case 2: launch_contract<2>(c, b, t, true); break;
+    case 4: launch_contract<4>(c, b, t, true); break;
+    default: launch_contract<8>(c, b, t, true); break;
   }
+  FASST_LAUNCH_CHECK();
   if (int st = check_tail_args(c, u, tu)) return st;
   prof_begin(c, KFBU);
   (c->KP > 64 ? k_fb_update<true> : k_fb_update<false>)<<<dim3(c->nft, J), 256,
@@ -4503,12 +4387,8 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   // tail in the same batch: nothing to fork)
   const bool prep_ready = c->prep_ready;
   c->prep_ready = 0;
-  // (the fused FB numerator reads FWHt in the E-step: the prep is then joined
-  // before it, only the first iteration of a batch forms it)
-  const bool fbf = J <= 8 && fbf_on(c);
   int st = prep_ready ? FASST_OK : launch_spectral_prep(c, fork);
   if (st) return st;
-  if (fbf && fork && !prep_ready) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   const bool w_ready = c->w_ready;   // (the previous iteration's fused tail formed W)
   c->w_ready = 0;
   if (!w_ready && (st = launch_w_old(c))) return st;
@@ -4527,8 +4407,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.halt = c->halt;
   e.part = c->epart.p;
   e.llpart = c->llpart.p;
-  e.FWHt = c->FWHt.p;
-  e.fbnum = c->bnum.p;
   e.F = c->F;
   e.T = c->T;
   e.Fp = c->Fp;
@@ -4548,16 +4426,14 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     gg.J = J;
     prof_begin(c, KESTEP);
     k_egen_point<<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg);
-    const size_t lds = (size_t)(J + 12) * 256 * sizeof(double);
-    (void)hipFuncSetAttribute((const void *)k_egen_stats, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const size_t lds = (size_t)(J + 12) * 256 * sizeof(double);   // (ceiling: set_lds_limits)
     k_egen_stats<<<dim3(c->nft, c->nchunk_e), 256, lds, c->stream>>>(e, gg);
     prof_end(c, KESTEP);
   } else {
-    launch_estep(c, e, c->nchunk_e, fbf);
+    launch_estep(c, e, c->nchunk_e);
   }
   FASST_LAUNCH_CHECK();
-  if (fork && !prep_ready && !fbf)
-    FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));   // hsum, FWHt below
+  if (fork && !prep_ready) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
   const bool ft = fast_tail(c);
   if (!ft) {   // (fused tail: summed by k_renorm_tail)
     prof_begin(c, KLL);
@@ -4599,8 +4475,6 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
       const int q = (c->nacc + 63) / 64;
       constexpr int QX = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64;
       if (c->R > 16) {   // (R^2 > 256 hat_Rss entries: 16 per lane; up to ~73 KB of LDS)
-        (void)hipFuncSetAttribute((const void *)k_mix<QX, (kMaxR * kMaxR + 63) / 64>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)ms);
         k_mix<QX, (kMaxR * kMaxR + 63) / 64><<<c->F, 64, ms, c->stream>>>(m);
       }
       else if (q <= 2)
@@ -4638,7 +4512,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     }
   }
   (void)all_free;
-  if ((st = spectral_update(c, omega, ft ? (fork ? 2 : 1) : 0, fbf && FBF_DBG == 0))) return st;
+  if ((st = spectral_update(c, omega, ft ? (fork ? 2 : 1) : 0))) return st;
   if (!ft) return launch_renorm(c, iter);
   if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
   RArgs r = renorm_args(c);
@@ -4665,6 +4539,8 @@ using namespace fasst;
 extern "C" {
 
 const char *fasst_last_error(void) { return fasst::g_err.c_str(); }
+
+int fasst_abi_version(void) { return FASST_ABI_VERSION; }
 
 int fasst_device_count(int *n) {
   FASST_HIP(hipGetDeviceCount(n));
@@ -4694,7 +4570,6 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v);
   if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
   if (const char *v = getenv("FASST_TWL")) c->twl = atoi(v);
-  if (const char *v = getenv("FASST_FBF")) c->fbf = atoi(v) != 0;
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||

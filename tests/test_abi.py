@@ -59,3 +59,14 @@ def test_step_abi_refuses_bad_shapes_before_touching_a_device():
     assert "conv" in _lib.last_error()
     st = _lib.lib.fasst_suff_stat(None, 17, *([None] * 8))
     assert st == _lib.FASST_ERR_SHAPE
+
+
+def test_abi_revision_matches_header_and_binding():
+    """The header's FASST_ABI_VERSION, the library's fasst_abi_version() and
+    the binding's ABI_VERSION agree (the loader refuses a library of another
+    revision: a revision-1 caller of fasst_source_powers passed one mask word
+    per component where revision 2 reads two)."""
+    from pyfasst_amd import _lib
+    src = open(os.path.join(ROOT, "include", "fasst_hip.h")).read()
+    hdr = int(re.search(r"#define FASST_ABI_VERSION (\d+)", src).group(1))
+    assert _lib.lib.fasst_abi_version() == hdr == _lib.ABI_VERSION

@@ -1,15 +1,12 @@
 """The fused renormalisation tail (fasst_em.hip: k_fb_update statistics,
 k_renorm_scales / _rows on the side stream, TW rescale inside k_tw_update,
-k_renorm_tail; renormalize_parameters, audioModel.py:1980-2040) and the FB
-numerator contracted inside the E-step (k_estep_mx FBF;
-update_spectral_components, audioModel.py:1521-1575) against the unfused
-kernels (FASST_FAST_TAIL=0, FASST_FBF=0, read when a context is created) and
-the oracle, on the structures they cover: one spectral component per source,
-fixed FW, no time blobs.  Every fused mode is run: FASST_FAST_TAIL=1 (the
-tail alone), 2 (the default: the tail also forms the next iteration's
-(FW.TW)^T and TW row sums, and the next iteration skips its prep), each with
-and without the fused FB numerator (the default for J <= 4, KP <= 32).
-Halted batches (a TW restart raised mid-batch) are covered in every mode:
+k_renorm_tail; renormalize_parameters, audioModel.py:1980-2040) against the
+unfused kernels (FASST_FAST_TAIL=0, read when a context is created) and the
+oracle, on the structures it covers: one spectral component per source,
+fixed FW, no time blobs.  Both fused modes are run: FASST_FAST_TAIL=1 (the
+tail alone) and 2 (the default: the tail also forms the next iteration's
+(FW.TW)^T and TW row sums at KP <= 64, and the next iteration of the batch
+skips its prep).  Halted batches (a TW restart raised mid-batch) are covered in every mode:
 the host swaps the W buffers of iterations the device skipped, and fasst_run
 rebuilds W (and the prep) from the parameters."""
 import numpy as np
@@ -42,14 +39,13 @@ def _models(F, T, J, K, rank, iters, conv=True, seed=0):
     return m, o, X
 
 
-# (FASST_FAST_TAIL, FASST_FBF); UNFUSED is the reference mode
-MODES = [("1", "0"), ("2", "0"), ("1", "1"), ("2", "1")]
-UNFUSED = ("0", "0")
+# FASST_FAST_TAIL values; UNFUSED is the reference mode
+MODES = ["1", "2"]
+UNFUSED = "0"
 
 
 def _run(monkeypatch, mode, args, kw, prep=None, restart_seed=None):
-    monkeypatch.setenv("FASST_FAST_TAIL", mode[0])
-    monkeypatch.setenv("FASST_FBF", mode[1])
+    monkeypatch.setenv("FASST_FAST_TAIL", mode)
     m, o, X = _models(*args, **kw)
     if prep:
         prep(m)
@@ -67,12 +63,12 @@ CASES = [
     ((97, 203, 3, 40, [1, 2, 1], 4), True),   # mixed ranks, K padded to 64 (the LDS prep path)
     ((97, 150, 2, 100, 2, 3), True),      # K > 64 (KP = 128: FW from L2)
     ((65, 77, 6, 8, 2, 3), True),         # J > 4
-    ((81, 181, 2, 16, 1, 5), True),       # J = 2, KP = 16: two waves own no source
-    ((70, 97, 4, 20, 2, 4), True),        # K = 20 padded to 32; 7 frame tiles: a wave idles in the last round
+    ((81, 181, 2, 16, 1, 5), True),       # J = 2, KP = 16
+    ((70, 97, 4, 20, 2, 4), True),        # K = 20 padded to 32, 7 frame tiles
 ]
 
 
-@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail%s_fbf%s" % m)
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail" + m)
 @pytest.mark.parametrize("args,conv", CASES)
 def test_fast_tail_vs_unfused_and_oracle(monkeypatch, args, conv, mode):
     mf, o, X, llf = _run(monkeypatch, mode, args, dict(conv=conv))
@@ -100,7 +96,7 @@ def _dead_tw(mod):   # tiny but non-zero: the mixing solve stays regular
     mod.spec_comps[1]['factor'][0]['TW'][:] = 1e-30
 
 
-@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail%s_fbf%s" % m)
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail" + m)
 def test_fast_tail_restart_halts_the_batch(monkeypatch, mode):
     """sum(TW) < eps after the first iteration: k_renorm_tail raises the
     restart flag, the batch's later iterations return at entry, the host
@@ -120,7 +116,7 @@ def test_fast_tail_restart_halts_the_batch(monkeypatch, mode):
     assert rel(np.abs(Sf), np.abs(o.separated_images(X))) < 1e-8
 
 
-@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail%s_fbf%s" % m)
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "tail" + m)
 def test_fast_tail_second_run_after_restart(monkeypatch, mode):
     """A model run again after a restarted run starts from the host
     parameters (W rebuilt at the batch start, not a stale swapped buffer)."""

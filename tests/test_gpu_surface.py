@@ -46,10 +46,15 @@ def test_initialize_conv_params_rand_vs_reference(tmp_path):
 def test_initialize_conv_params_other_methods(tmp_path):
     g = load("convinit_rand")
     m = _convinit_model(tmp_path, g)
+    before = {j: (c['mix_type'], c['params'].copy()) for j, c in m.spat_comps.items()}
     with pytest.raises(NotImplementedError):   # DEMIX is out of scope
         m.initializeConvParams()
     with pytest.raises(ValueError):
         m.initializeConvParams(initMethod='svd')
+    # a refused call leaves every component as it was ('inst', its params)
+    for j, c in m.spat_comps.items():
+        assert c['mix_type'] == before[j][0] == 'inst'
+        assert np.array_equal(c['params'], before[j][1])
 
 
 def test_comp_spat_cmps_powers_vs_oracle():
