@@ -95,11 +95,6 @@ struct fasst_ctx {
   // fasst_em.hip) unless FASST_FAST_TAIL=0 was set when this context was
   // created; 2 (default): it also forms the next iteration's FWHt / hsum
   int ftail = 2;
-  // every launch of an iteration on the main stream (FASST_SERIAL_PREP=1: A/B)
-  int serial = 0;
-  // TW contraction form: 0 = k_tw_contract (W operands from L2 per lane),
-  // 1 = k_tw_contract_lds (FASST_TWL, read at creation)
-  int twl = 1;
   fasst::DBuf<double2> rss, rxs;
   fasst::DBuf<int> flags;        // [0] singular, [1..nslot] TW restart, [kFlagHalt] halt,
                                  // [kFlagIter] iteration that raised a restart

@@ -1666,12 +1666,9 @@ struct UArgs {
   double omega;
   int kb0[kMaxJ], kb1[kMaxJ], fb_free[kMaxJ];  // columns [kb0, kb1) are updated
   // fused tail (pmax non-null): the renormalisation's stage-1 statistics of
-  // this block's 16 bins, FB column maxima [J][nft][KP] and ('conv') the
-  // mixing filters' energy [J][nft]
-  double *pmax, *pe;
-  const double2 *A;
-  int roff[kMaxJ + 1];
-  unsigned convm;
+  // this block's 16 bins, the FB column maxima [J][nft][KP] (the mixing
+  // filters' energy is k_renorm_scales', read after the mixing update)
+  double *pmax;
   const int *halt;
 };
 __device__ double block_sum(double x, double *s);
@@ -1760,17 +1757,6 @@ __global__ __launch_bounds__(256) void k_fb_update(const UArgs a) {
     double m = -INFINITY;
     for (int fl = 0; fl < nb; ++fl) m = fmax(m, s_fb[fl * PB + k]);
     a.pmax[((size_t)j * gridDim.x + blockIdx.x) * KP + k] = m;
-  }
-  if (a.convm >> j & 1u) {
-    __shared__ double s_e[256];
-    const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
-    double e = 0.0;
-    for (int idx = threadIdx.x; idx < nr * 2 * nb; idx += blockDim.x) {
-      const double2 x = a.A[(size_t)(2 * r0 + idx / nb) * a.Fp + f0 + idx % nb];
-      e += x.x * x.x + x.y * x.y;
-    }
-    e = block_sum(e, s_e);
-    if (threadIdx.x == 0) a.pe[(size_t)j * gridDim.x + blockIdx.x] = e;
   }
 }
 
@@ -2606,10 +2592,10 @@ struct RArgs {
   double *pe;     // [J][nchunk] partial mixing-filter energy (conv)
   double *tpart;  // [nslot][nchunk] partial sums of the rescaled TW, per block
   int *flags;
-  // fused tail (k_renorm_scales / _rows / _tail): k_fb_update's statistics
-  // [J][nstat][KP] and [J][nstat], k_tw_update's restart sums [nslot][ntb],
-  // the E-step's loglik partials
-  const double *pmax2, *pe2, *tpart2, *llpart;
+  // fused tail (k_renorm_scales / _rows / _tail): k_fb_update's column
+  // maxima [J][nstat][KP], k_tw_update's restart sums [nslot][ntb], the
+  // E-step's loglik partials
+  const double *pmax2, *tpart2, *llpart;
   double *ll_out;
   // k_tw_update's TW row-sum partials [J][KP][ntb] -> hsum [J][KP] (null: the
   // next iteration's k_tw_rowsum forms hsum)
@@ -2844,42 +2830,58 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
 
 // Fused tail of gem_iteration (one spectral component per source, no time
 // blobs, fixed FW): the same renormalize_parameters (audioModel.py:1991-2037)
-// with the stage-1 statistics taken by k_fb_update, the scales formed once
-// per source (k_renorm_scales) and the FB / mixing / FW rescale
-// (k_renorm_rows) on the side stream while the TW contraction runs; TW's
-// rescale and restart sums ride in k_tw_update, and k_renorm_tail closes the
-// iteration with the restart test and the loglik sum.
+// with the FB column maxima taken by k_fb_update, the scales formed once per
+// source (k_renorm_scales) after the mixing update, and the FB / mixing / FW
+// rescale (k_renorm_rows) on the side stream while the TW contraction runs;
+// TW's rescale and restart sums ride in k_tw_update, and k_renorm_tail closes
+// the iteration with the restart test and the loglik sum.
+//
+// k_renorm_scales, one block per source: e_j = mean |params|^2 (the 'conv'
+// filters read from A itself, 'inst' from Pinst), w_j[k] = e_j max_f FB[f][k]
+// (0 -> 1), w2_j[c] = mean_r FW[r][c] w_j[r] over the K live rows (0 -> 1).
+// Every thread issues its loads in batches before using any: the round-5
+// form walked the 129 maxima, the energy partials and the K x K FW as chains
+// of dependent loads (105 us beside the TW contraction, profiles/r5_bench.txt)
 __global__ __launch_bounds__(256) void k_renorm_scales(const RArgs a) {
   HALT_GUARD(a.halt);
+  constexpr int B = 8;   // loads in flight per thread and batch
   __shared__ double s_red[256];
   __shared__ double s_w[kMaxKP];
-  __shared__ double s_e;
   const int j = blockIdx.x, K = a.K[j], KP = a.KP, ns = a.nstat;
   const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
   const bool cj = a.convm >> j & 1u;
-  if (cj) {
-    double e = 0.0;
-    for (int q = threadIdx.x; q < ns; q += blockDim.x) e += a.pe2[(size_t)j * ns + q];
-    e = block_sum(e, s_red);
-    if (threadIdx.x == 0) s_e = e / (double)(nr * 2 * a.F);
-  } else if (threadIdx.x == 0) {
-    double e = 0.0;
-    for (int q = 0; q < nr * 2; ++q) {
-      const double2 x = a.Pinst[2 * r0 + q];
-      e += x.x * x.x + x.y * x.y;
+  // e_j: the 'conv' filters A[r][c][f] of the source's nr ranks
+  const int ne = cj ? nr * 2 * a.F : nr * 2;
+  double e = 0.0;
+  for (int base = threadIdx.x; base < ne; base += B * blockDim.x) {
+    double2 x[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int idx = base + u * blockDim.x;
+      x[u] = idx >= ne ? make_double2(0.0, 0.0)
+                       : (cj ? a.A[(size_t)(2 * r0 + idx / a.F) * a.Fp + idx % a.F] : a.Pinst[2 * r0 + idx]);
     }
-    s_e = e / (double)(nr * 2);
+#pragma unroll
+    for (int u = 0; u < B; ++u) e += x[u].x * x[u].x + x[u].y * x[u].y;
   }
-  // column maxima over the blocks: thread (g, k) takes blocks q = g mod G
+  e = block_sum(e, s_red) / (double)ne;
+  // column maxima over k_fb_update's blocks: thread (g, k) takes blocks
+  // q = g mod G (max is exact in any order)
   const int G = (int)blockDim.x / KP;
   double m = -INFINITY;
   if (threadIdx.x < G * KP)
-    for (int q = threadIdx.x / KP; q < ns; q += G)
-      m = fmax(m, a.pmax2[((size_t)j * ns + q) * KP + threadIdx.x % KP]);
+    for (int q0 = threadIdx.x / KP; q0 < ns; q0 += B * G) {
+      double x[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int q = q0 + u * G;
+        x[u] = q < ns ? a.pmax2[((size_t)j * ns + q) * KP + threadIdx.x % KP] : -INFINITY;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) m = fmax(m, x[u]);
+    }
+  s_red[threadIdx.x] = m;
   __syncthreads();
-  if (threadIdx.x < G * KP) s_red[threadIdx.x] = m;
-  __syncthreads();
-  const double e = s_e;
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {   // (KP <= kMaxKP < 256)
     double x = -INFINITY;
     for (int g = 0; g < G; ++g) x = fmax(x, s_red[g * KP + k]);
@@ -2891,9 +2893,16 @@ __global__ __launch_bounds__(256) void k_renorm_scales(const RArgs a) {
   const double *fw = a.FW + (size_t)j * KP * KP;
   for (int cc = threadIdx.x; cc < KP; cc += blockDim.x) {
     double s = 1.0;
-    if (cc < K) {   // FW.mean(axis=0) of the column's spectral component
+    if (cc < K) {   // FW.mean(axis=0) of the column's spectral component, in row order
       s = 0.0;
-      for (int r = 0; r < K; ++r) s += fw[r * KP + cc] * s_w[r];
+      for (int r0b = 0; r0b < K; r0b += B) {
+        double x[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) x[u] = r0b + u < K ? fw[(r0b + u) * KP + cc] : 0.0;
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+          if (r0b + u < K) s += x[u] * s_w[r0b + u];
+      }
       s /= (double)K;
       if (s == 0.0) s = 1.0;
     }
@@ -3224,7 +3233,7 @@ static int launch_grid(size_t n, int block = 256) {
 }
 
 static int estep_occupancy(const fasst_ctx *c);
-static int contract_occupancy(const fasst_ctx *c, bool fb);
+static int contract_occupancy(const fasst_ctx *c);
 static int twl_occupancy(const fasst_ctx *c, int *units);
 static int tpw_of(const fasst_ctx *c);
 // bins per block of the FW update's f-contraction (k_fw_reduce holds three
@@ -3359,24 +3368,16 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   if (const char *v = getenv("FASST_NCHUNK_E")) c->nchunk_e = std::max(1, std::min(atoi(v), c->ntt));
   c->tpc_e = (c->ntt + c->nchunk_e - 1) / c->nchunk_e;
   c->nchunk_e = (c->ntt + c->tpc_e - 1) / c->tpc_e;
-  const long cap_b = (long)contract_occupancy(c, true) * ncu;
+  const long cap_b = (long)contract_occupancy(c) * ncu;
   c->nchunk_b = best_split((long)((c->nft + kFPW - 1) / kFPW) * J, cap_b, c->ntt / 32);
   if (const char *v = getenv("FASST_NCHUNK_B")) c->nchunk_b = std::max(1, std::min(atoi(v), c->ntt));
   c->tpc_b = (c->ntt + c->nchunk_b - 1) / c->nchunk_b;
   c->nchunk_b = (c->ntt + c->tpc_b - 1) / c->tpc_b;
-  long cap_t = (long)contract_occupancy(c, false) * ncu;
   // (the bin split also multiplies k_tw_update's reduction: a fixed, small
   // split measured best at C3)
   c->nsplit_t = std::max(1, std::min(4, c->nft / 32));
-  int tw_units = (c->ntt + tpw_of(c) - 1) / tpw_of(c);
-  {
-    int u = 0;
-    const int occ = twl_occupancy(c, &u);
-    if (occ) {
-      cap_t = (long)occ * ncu;
-      tw_units = u;
-    }
-  }
+  int tw_units = 0;
+  const long cap_t = (long)twl_occupancy(c, &tw_units) * ncu;
   if ((long)tw_units * J * c->nsplit_t < cap_t)
     c->nsplit_t = best_split((long)tw_units * J, cap_t, c->nft / 16);
   if (const char *v = getenv("FASST_NSPLIT_T")) c->nsplit_t = std::max(1, std::min(atoi(v), c->nft));
@@ -3426,7 +3427,6 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(rtpart, (size_t)kMaxSlot * c->nchunk_r);
   c->ntb = (Tp + 63) / 64;
   ALLOC(rpmax2, (size_t)J * c->nft * KP);
-  ALLOC(rpe2, (size_t)J * c->nft);
   ALLOC(rtpart2, (size_t)kMaxSlot * c->ntb);
   ALLOC(Wkf_next, (size_t)J * KP * Fp);
   ALLOC(hpart, (size_t)J * KP * c->ntb);
@@ -3561,7 +3561,6 @@ static RArgs renorm_args(fasst_ctx *c) {
     r.soff[j] = j <= c->J ? c->soff[j] : c->nslot;
   }
   r.pmax2 = c->rpmax2.p;
-  r.pe2 = c->rpe2.p;
   r.tpart2 = c->rtpart2.p;
   r.llpart = c->llpart.p;
   r.ll_out = nullptr;
@@ -3634,20 +3633,91 @@ static bool fast_tail(const fasst_ctx *c) {
   return true;
 }
 
-// the scales and the FB / mixing / FW rescale, after k_fb_update: on the side
-// stream (fork) beside the TW contraction; ev_scales gates k_tw_update,
-// ev_rows the iteration's end
-static int launch_tail_side(fasst_ctx *c, bool fork) {
-  const RArgs r = renorm_args(c);
-  hipStream_t side = fork ? c->aux : c->stream;
-  if (fork) {
-    FASST_HIP(hipEventRecord(c->ev_tail, c->stream));
-    FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_tail, 0));
+// update_mix_matrix (audioModel.py:766-889) on stream s: k_mix (per-bin
+// statistics, hat_Rss / hat_Rxs, the 'conv' solves) and k_mix_inst (the
+// 'inst' f-mean solve), when some spatial component is free
+static int launch_mix(fasst_ctx *c, hipStream_t s) {
+  const int J = c->J;
+  bool any_free = false;
+  for (int j = 0; j < J; ++j) any_free |= c->spat_free[j] != 0;
+  if (any_free) {
+    MArgs m{};
+    m.part = c->epart.p;
+    m.Wkf = c->Wkf.p;
+    m.hsum = c->hsum.p;
+    m.KP = c->KP;
+    m.A = c->A.p;
+    m.rss = c->rss.p;
+    m.rxs = c->rxs.p;
+    m.flags = c->flags.p;
+    m.halt = c->halt;
+    m.F = c->F;
+    m.Fp = c->Fp;
+    m.J = J;
+    m.R = c->R;
+    m.nchunk = c->nchunk_e;
+    m.nacc = c->nacc;
+    m.conv_update = c->conv ? 1 : 0;
+    m.invT = 1.0 / (double)c->T;
+    for (int j = 0; j < J; ++j)
+      for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
+    prof_begin(c, KMIX, s);
+    {
+      const size_t ms = mix_smem(J, c->R, c->KP, c->nacc);
+      const int q = (c->nacc + 63) / 64;
+      constexpr int QX = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64;
+      if (c->R > 16) {   // (R^2 > 256 hat_Rss entries: 16 per lane; up to ~73 KB of LDS)
+        k_mix<QX, (kMaxR * kMaxR + 63) / 64><<<c->F, 64, ms, s>>>(m);
+      }
+      else if (q <= 2)
+        k_mix<2><<<c->F, 64, ms, s>>>(m);
+      else if (q <= 4)   // (J <= 8: 4 J (J + 1) / 2 + 8 J <= 208)
+        k_mix<4><<<c->F, 64, ms, s>>>(m);
+      else
+        k_mix<QX><<<c->F, 64, ms, s>>>(m);
+    }
+    prof_end(c, KMIX, s);
+    FASST_LAUNCH_CHECK();
+    if (!c->conv) {
+      IArgs ia{};
+      ia.rss = c->rss.p;
+      ia.rxs = c->rxs.p;
+      ia.A = c->A.p;
+      ia.Pinst = c->Pinst.p;
+      ia.flags = c->flags.p;
+      ia.halt = c->halt;
+      ia.F = c->F;
+      ia.Fp = c->Fp;
+      ia.R = c->R;
+      ia.nu = ia.no = 0;
+      for (int j = 0; j < J; ++j)
+        for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) {
+          if (c->spat_free[j])
+            ia.upd[ia.nu++] = r;
+          else
+            ia.oth[ia.no++] = r;
+        }
+      prof_begin(c, KMIXI, s);
+      k_mix_inst<<<1, 256, 0, s>>>(ia);
+      prof_end(c, KMIXI, s);
+      FASST_LAUNCH_CHECK();
+    }
   }
+  return FASST_OK;
+}
+
+// the scales and the FB / mixing / FW rescale, after k_fb_update: on the side
+// stream beside the TW contraction; ev_scales gates k_tw_update, ev_rows the
+// iteration's end
+static int launch_tail_side(fasst_ctx *c) {
+  const RArgs r = renorm_args(c);
+  hipStream_t side = c->aux;
+  FASST_HIP(hipEventRecord(c->ev_tail, c->stream));
+  FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_tail, 0));
   prof_begin(c, KREN, side);
   k_renorm_scales<<<c->J, 256, 0, side>>>(r);
   FASST_LAUNCH_CHECK();
-  if (fork) FASST_HIP(hipEventRecord(c->ev_scales, c->aux));
+  FASST_HIP(hipEventRecord(c->ev_scales, c->aux));
   k_renorm_rows<<<dim3(c->nft, c->J), 256, 0, side>>>(r);
   FASST_LAUNCH_CHECK();
   prof_end(c, KREN, side);
@@ -3658,7 +3728,7 @@ static int launch_tail_side(fasst_ctx *c, bool fork) {
                                                      c->J, c->Fp, c->KP, c->halt);
   prof_end(c, KW, side);
   FASST_LAUNCH_CHECK();
-  if (fork) FASST_HIP(hipEventRecord(c->ev_rows, c->aux));
+  FASST_HIP(hipEventRecord(c->ev_rows, c->aux));
   return FASST_OK;
 }
 
@@ -3746,15 +3816,34 @@ static void launch_fw_reduce(fasst_ctx *c, const FWArgs &w) {
   k_fw_reduce<<<dim3(w.nfc, c->J), 256, lds, c->stream>>>(w);
 }
 
-// k_tw_contract_lds shapes (NW waves per block, TPW frame tiles per wave, NS
-// stages); c->twl picks one (0: the register-operand k_tw_contract)
-template <class CF>
-static void launch_twl_cfg(fasst_ctx *c, const TArgs &t) {
+// k_tw_contract_lds's shape: 8 waves per block, one frame tile per wave, two
+// LDS stages (C3 same-box A/B, k_tw_contract 0.395 ms: NW x TPW x NS = 8 x 1 x
+// 2 0.378, 4 x 2 x 2 0.379, 4 x 1 x 3 0.396, 4 x 2 x 3 0.437 ms; the other
+// shapes and the register-operand k_tw_contract of rounds 1-4 were deleted
+// after the A/B)
+template <int NKC>
+using TwlShape = TwlCfg<NKC, 8, 1, 2>;
+
+template <int NKC>
+static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb, int nz = 0) {
+  if (fb) {
+    prof_begin(c, KFBC);
+    k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, nz ? nz : c->nchunk_b), 64,
+                               0, c->stream>>>(b);
+    prof_end(c, KFBC);
+    return;
+  }
+  using CF = TwlShape<NKC>;
+  prof_begin(c, KTWC);
   const int g = (c->ntt + CF::NW_ * CF::TPW_ - 1) / (CF::NW_ * CF::TPW_);
   k_tw_contract_lds<CF><<<dim3(g, c->J, c->nsplit_t), CF::NT, CF::smem, c->stream>>>(t);
+  prof_end(c, KTWC);
 }
-template <class CF>
-static int twl_occ_cfg(const fasst_ctx *c, int *units) {
+
+// resident k_tw_contract_lds blocks per CU, and its frame-tile groups (units)
+template <int NKC>
+static int twl_occ_of(const fasst_ctx *c, int *units) {
+  using CF = TwlShape<NKC>;
   (void)hipFuncSetAttribute((const void *)k_tw_contract_lds<CF>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)CF::smem);
   int n = 0;
@@ -3764,74 +3853,24 @@ static int twl_occ_cfg(const fasst_ctx *c, int *units) {
   *units = (c->ntt + CF::NW_ * CF::TPW_ - 1) / (CF::NW_ * CF::TPW_);
   return std::max(1, n);
 }
-// launch (units == nullptr) or occupancy query of shape c->twl at NKC
-template <int NKC>
-static int twl_switch(fasst_ctx *c, const TArgs *t, int *units) {
-  switch (c->twl) {
-#define TWL_CASE(id, NW, TPW, NS)                                  \
-  case id:                                                         \
-    if (!units) launch_twl_cfg<TwlCfg<NKC, NW, TPW, NS>>(c, *t);   \
-    return units ? twl_occ_cfg<TwlCfg<NKC, NW, TPW, NS>>(c, units) : 1;
-    // (C3 same-box A/B, k_tw_contract 0.395 ms: NW x TPW x NS = 8 x 1 x 2
-    // 0.378, 4 x 2 x 2 0.379, 4 x 1 x 3 0.396, 4 x 2 x 3 0.437 ms)
-    TWL_CASE(1, 8, 1, 2)
-#undef TWL_CASE
-    default: return 0;
-  }
-}
-
-template <int NKC>
-static void launch_contract(fasst_ctx *c, const BArgs &b, const TArgs &t, bool fb, int nz = 0) {
-  if (fb) {
-    prof_begin(c, KFBC);
-    k_fb_contract<NKC, kFPW><<<dim3((c->nft + kFPW - 1) / kFPW, c->J, nz ? nz : c->nchunk_b), 64,
-                               0, c->stream>>>(b);
-    prof_end(c, KFBC);
-  } else if (c->twl) {
-    prof_begin(c, KTWC);
-    twl_switch<NKC>(c, &t, nullptr);
-    prof_end(c, KTWC);
-  } else {
-    prof_begin(c, KTWC);
-    constexpr int TPW = tpw_for<NKC>();
-    k_tw_contract<NKC, TPW><<<dim3((c->ntt + TPW - 1) / TPW, c->J, c->nsplit_t), 64, 0,
-                              c->stream>>>(t);
-    prof_end(c, KTWC);
-  }
-}
-
-// resident k_tw_contract_lds blocks per CU (0: c->twl off)
 static int twl_occupancy(const fasst_ctx *c, int *units) {
-  if (!c->twl) return 0;
-  fasst_ctx *cc = const_cast<fasst_ctx *>(c);
   switch (c->KP) {
-    case 16: return twl_switch<1>(cc, nullptr, units);
-    case 32: return twl_switch<2>(cc, nullptr, units);
-    case 64: return twl_switch<4>(cc, nullptr, units);
-    default: return twl_switch<8>(cc, nullptr, units);
+    case 16: return twl_occ_of<1>(c, units);
+    case 32: return twl_occ_of<2>(c, units);
+    case 64: return twl_occ_of<4>(c, units);
+    default: return twl_occ_of<8>(c, units);
   }
 }
 
-static int contract_occupancy(const fasst_ctx *c, bool fb) {
+// resident k_fb_contract waves per CU
+static int contract_occupancy(const fasst_ctx *c) {
   int n = 1;
   hipError_t e = hipSuccess;
   switch (c->KP / 16) {
-    case 1:
-      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<1, kFPW>, 64, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<1, kTPW>, 64, 0);
-      break;
-    case 2:
-      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<2, kFPW>, 64, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<2, kTPW>, 64, 0);
-      break;
-    case 4:
-      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<4, kFPW>, 64, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<4, kTPW>, 64, 0);
-      break;
-    default:
-      e = fb ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<8, kFPW>, 64, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tw_contract<8, 1>, 64, 0);
-      break;
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<1, kFPW>, 64, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<2, kFPW>, 64, 0); break;
+    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<4, kFPW>, 64, 0); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fb_contract<8, kFPW>, 64, 0); break;
   }
   return e == hipSuccess ? std::max(1, n) : 1;
 }
@@ -3848,7 +3887,7 @@ static int contract_occupancy(const fasst_ctx *c, bool fb) {
 // kernel could dereference it (an uninitialised argument struct on the
 // multi-block path once sent garbage pointers to the device)
 static int check_tail_args(const fasst_ctx *c, const UArgs &u, const TUArgs &tu) {
-  const bool ok_u = !u.pmax || (u.pmax == c->rpmax2.p && u.pe == c->rpe2.p && u.A == c->A.p);
+  const bool ok_u = !u.pmax || u.pmax == c->rpmax2.p;
   const bool ok_t = !tu.scal || (tu.scal == c->rscal.p && tu.tpart == c->rtpart2.p &&
                                  (!tu.FWHt || (tu.FWHt == c->FWHt.p && tu.hpart == c->hpart.p &&
                                                tu.FW == c->FW.p)));
@@ -4166,9 +4205,9 @@ static int launch_spectral_prep(fasst_ctx *c, bool fork) {
 // update_spectral_components (audioModel.py:1469-1978) from the rho planes in
 // c->hatW (rho_j = hat_W_j / max(V_j, eps), V from the parameters before the
 // update), after launch_spectral_prep and launch_w_old.  tail (fast_tail
-// models inside gem_iteration): 1 = the fused renormalisation tail on the
-// main stream, 2 = its side-stream part forked beside the TW contraction
-static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
+// models inside gem_iteration): the fused renormalisation tail, its scales /
+// rescale forked onto the side stream beside the TW contraction
+static int spectral_update(fasst_ctx *c, double omega, bool tail = false) {
   const int J = c->J;
   const int nkc = c->KP / 16;
   bool any_fw = false;
@@ -4242,10 +4281,6 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   u.omega = omega;
   u.bden = nullptr;
   u.pmax = tail ? c->rpmax2.p : nullptr;
-  u.pe = c->rpe2.p;
-  u.A = c->A.p;
-  u.convm = c->convm;
-  for (int j = 0; j <= kMaxJ; ++j) u.roff[j] = j <= J ? c->roff[j] : c->R;
   tu.scal = tail ? c->rscal.p : nullptr;
   tu.tpart = c->rtpart2.p;
   tu.ntb = c->ntb;
@@ -4282,7 +4317,7 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   prof_end(c, KFBU);
   FASST_LAUNCH_CHECK();
   if (tail)
-    if (int st = launch_tail_side(c, tail == 2)) return st;
+    if (int st = launch_tail_side(c)) return st;
   if (any_fw) {
     // FW update (:1578-1631) between the FB and TW updates; W_new = FB_new FW_old
     // from k_fb_update is the V_mid operand, then W_new is rebuilt with FW_new
@@ -4341,7 +4376,7 @@ static int spectral_update(fasst_ctx *c, double omega, int tail = 0) {
   }
   FASST_LAUNCH_CHECK();
   // (prep reads the renormalised FW: wait for k_renorm_rows, else the scales)
-  if (tail == 2) FASST_HIP(hipStreamWaitEvent(c->stream, prep ? c->ev_rows : c->ev_scales, 0));
+  if (tail) FASST_HIP(hipStreamWaitEvent(c->stream, prep ? c->ev_rows : c->ev_scales, 0));
   prof_begin(c, KTWU);
   k_tw_update<<<dim3(c->ntb, J), 256, prep ? (size_t)c->KP * 64 * sizeof(double) : 0, c->stream>>>(tu);
   prof_end(c, KTWU);
@@ -4380,14 +4415,11 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
       }
   }
   // (FW.TW)^T and the TW row sums depend only on the previous iteration's
-  // parameters: fork them onto the side stream (FASST_SERIAL_PREP=1 keeps
-  // every launch on the main stream: A/B)
-  const bool fork = !c->serial;
-  // (FWHt and the row sums were formed by the previous iteration's fused
-  // tail in the same batch: nothing to fork)
+  // parameters: forked onto the side stream beside the E-step (unless the
+  // previous iteration's fused tail in the same batch formed them)
   const bool prep_ready = c->prep_ready;
   c->prep_ready = 0;
-  int st = prep_ready ? FASST_OK : launch_spectral_prep(c, fork);
+  int st = prep_ready ? FASST_OK : launch_spectral_prep(c, true);
   if (st) return st;
   const bool w_ready = c->w_ready;   // (the previous iteration's fused tail formed W)
   c->w_ready = 0;
@@ -4433,7 +4465,7 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     launch_estep(c, e, c->nchunk_e);
   }
   FASST_LAUNCH_CHECK();
-  if (fork && !prep_ready) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
+  if (!prep_ready) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_join, 0));  // hsum, FWHt below
   const bool ft = fast_tail(c);
   if (!ft) {   // (fused tail: summed by k_renorm_tail)
     prof_begin(c, KLL);
@@ -4442,79 +4474,14 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     prof_end(c, KLL);
     FASST_LAUNCH_CHECK();
   }
-  // mixing update
-  bool any_free = false, all_free = true;
-  for (int j = 0; j < J; ++j) {
-    any_free |= c->spat_free[j] != 0;
-    all_free &= c->spat_free[j] != 0;
-  }
-  if (any_free) {
-    MArgs m{};
-    m.part = c->epart.p;
-    m.Wkf = c->Wkf.p;
-    m.hsum = c->hsum.p;
-    m.KP = c->KP;
-    m.A = c->A.p;
-    m.rss = c->rss.p;
-    m.rxs = c->rxs.p;
-    m.flags = c->flags.p;
-    m.halt = c->halt;
-    m.F = c->F;
-    m.Fp = c->Fp;
-    m.J = J;
-    m.R = c->R;
-    m.nchunk = c->nchunk_e;
-    m.nacc = c->nacc;
-    m.conv_update = c->conv ? 1 : 0;
-    m.invT = 1.0 / (double)c->T;
-    for (int j = 0; j < J; ++j)
-      for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) m.jr[r] = j;
-    prof_begin(c, KMIX);
-    {
-      const size_t ms = mix_smem(J, c->R, c->KP, c->nacc);
-      const int q = (c->nacc + 63) / 64;
-      constexpr int QX = (4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64;
-      if (c->R > 16) {   // (R^2 > 256 hat_Rss entries: 16 per lane; up to ~73 KB of LDS)
-        k_mix<QX, (kMaxR * kMaxR + 63) / 64><<<c->F, 64, ms, c->stream>>>(m);
-      }
-      else if (q <= 2)
-        k_mix<2><<<c->F, 64, ms, c->stream>>>(m);
-      else if (q <= 4)   // (J <= 8: 4 J (J + 1) / 2 + 8 J <= 208)
-        k_mix<4><<<c->F, 64, ms, c->stream>>>(m);
-      else
-        k_mix<QX><<<c->F, 64, ms, c->stream>>>(m);
-    }
-    prof_end(c, KMIX);
-    FASST_LAUNCH_CHECK();
-    if (!c->conv) {
-      IArgs ia{};
-      ia.rss = c->rss.p;
-      ia.rxs = c->rxs.p;
-      ia.A = c->A.p;
-      ia.Pinst = c->Pinst.p;
-      ia.flags = c->flags.p;
-      ia.halt = c->halt;
-      ia.F = c->F;
-      ia.Fp = c->Fp;
-      ia.R = c->R;
-      ia.nu = ia.no = 0;
-      for (int j = 0; j < J; ++j)
-        for (int r = c->roff[j]; r < c->roff[j + 1]; ++r) {
-          if (c->spat_free[j])
-            ia.upd[ia.nu++] = r;
-          else
-            ia.oth[ia.no++] = r;
-        }
-      prof_begin(c, KMIXI);
-      k_mix_inst<<<1, 256, 0, c->stream>>>(ia);
-      prof_end(c, KMIXI);
-      FASST_LAUNCH_CHECK();
-    }
-  }
-  (void)all_free;
-  if ((st = spectral_update(c, omega, ft ? (fork ? 2 : 1) : 0))) return st;
+  // mixing update (update_mix_matrix, :766-889).  (On the side stream beside
+  // the TW contraction instead, after the FB update: k_mix stretched to 0.18
+  // ms and took 23 us from the TW contraction and 14 us from the FB
+  // contraction for the 30 us it left the critical path; profiles/r6_ab_mix_side.txt)
+  if ((st = launch_mix(c, c->stream))) return st;
+  if ((st = spectral_update(c, omega, ft))) return st;
   if (!ft) return launch_renorm(c, iter);
-  if (fork) FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
+  FASST_HIP(hipStreamWaitEvent(c->stream, c->ev_rows, 0));
   RArgs r = renorm_args(c);
   r.ll_out = ll_dev;
   const bool prep = c->ftail >= 2 && c->KP <= 64;   // (spectral_update's k_tw_update formed FWHt)
@@ -4568,8 +4535,6 @@ int fasst_create(int device, int F, int T, fasst_ctx **out) {
   c->nft = c->Fp / kTile;
   c->ntt = c->Tp / kTile;
   if (const char *v = getenv("FASST_FAST_TAIL")) c->ftail = atoi(v);
-  if (const char *v = getenv("FASST_SERIAL_PREP")) c->serial = atoi(v) != 0;
-  if (const char *v = getenv("FASST_TWL")) c->twl = atoi(v);
   int st = FASST_OK;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
@@ -4645,7 +4610,6 @@ int fasst_destroy(fasst_ctx *c) {
     c->rpe.release();
     c->rtpart.release();
     c->rpmax2.release();
-    c->rpe2.release();
     c->rtpart2.release();
     c->hpart.release();
     c->vgen.release();

@@ -81,6 +81,57 @@ def test_config3_full_size_vs_oracle(name):
         assert v < (1e-6 if k == "absS_elem" else 1e-8), (k, v)
 
 
+def test_config3_every_point_vs_live_oracle(tmp_path):
+    """BASELINE configs[2] at its real size, one GEM iteration and the Wiener
+    images, compared at EVERY bin and frame with the live oracle
+    (tests/oracle_c3_every_point.py, oracle/fasst_ref.py on bin slices in a
+    process pool; started first, so it computes while the GPU runs).  The
+    production launch shapes (15 E-step chunks, 19 FB chunks, 4 TW bin
+    splits, ragged last chunks) are pinned point by point, not through the
+    c3_full fixture's subsample: logliks 1e-10, PSD 1e-14, mixing filters /
+    FB / TW max-normalised 1e-8 and elementwise 1e-6, |S| elementwise 1e-6
+    (each point against its own magnitude, floored at 1e-6 of the max)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = str(tmp_path / "oracle")
+    proc = subprocess.Popen([sys.executable, os.path.join(here, "oracle_c3_every_point.py"), out,
+                             str(min(16, os.cpu_count() or 1))],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        m = _fasst_model("c3_full", iters=1)
+        ll = m.estim_param_a_post_model()
+        S = np.abs(m.separated_images())
+        log, _ = proc.communicate(timeout=900)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+            proc.wait()
+    print(log)
+    assert proc.returncode == 0, log
+    g = lambda n: np.load(os.path.join(out, n + ".npy"))
+    assert rel(ll, g("logliks")) < 1e-10
+    assert rel(m.noise['PSD'], g("psd")) < 1e-14
+    worst = {}
+    for j in range(4):
+        fac = m.spec_comps[j]['factor'][0]
+        for key, a in (("params", m.spat_comps[j]['params']), ("FB", fac['FB']), ("TW", fac['TW']),
+                       ("FW", fac['FW'])):
+            b = g("%s_%d" % (key, j))
+            assert a.shape == b.shape, (key, a.shape, b.shape)
+            worst[key] = max(worst.get(key, 0.0), rel(a, b))
+            if key != "FW":
+                worst[key + "_elem"] = max(worst.get(key + "_elem", 0.0), rel_elem(a, b))
+    Sr = g("absS")
+    assert S.shape == Sr.shape
+    worst["absS"] = rel(S, Sr)
+    worst["absS_elem"] = rel_elem(S, Sr)
+    print("c3 every point, worst relative deviation:", worst)
+    for k, v in worst.items():
+        assert v < (1e-6 if k.endswith("_elem") else 1e-8), (k, v)
+
+
 def test_chunk_overrides_vs_oracle(monkeypatch):
     """Forced multi-chunk reductions (E-step chunks 3, FB chunks 3, TW bin
     splits 2, ragged last chunks) on a small case against the live oracle."""
