@@ -803,15 +803,13 @@ int nmf_create(int device, int F, int N, int K, nmf_ctx **out) {
   // (their buffer offsets into W, Ht and 16-row SX / SXt slabs are 32-bit)
   c->fused = K % 16 == 0 && K <= 64 && (size_t)(N + 32) * K * 8 < 0x7fffffffu &&
              (size_t)(F + 32) * K * 8 < 0x7fffffffu && (size_t)32 * (F + N + 64) * 8 < 0x7fffffffu;
-  if (const char *v = getenv("FASST_NMF_FUSED")) c->fused = c->fused && atoi(v) != 0;
   if (c->fused) {
     const int nft = (F + 15) / 16, ntt = (N + 15) / 16;
     // launch geometry: a 32-wide group of the kept dimension per workgroup,
     // the contracted dimension split over 4 waves x ng groups so the grid
-    // holds about `waves` waves (A/B knob FASST_NMF_WAVES; round 2 at C2,
-    // F=1025 T=2000 K=64: ~1024 waves best, 2048: +20%)
-    int waves = 4 * kNmfCUs;
-    if (const char *v = getenv("FASST_NMF_WAVES")) waves = std::max(4, atoi(v));
+    // holds about `waves` waves (round 2 at C2, F=1025 T=2000 K=64: ~1024
+    // waves best, 2048: +20%)
+    const int waves = 4 * kNmfCUs;
     const int uw = (nft + kNmfPW - 1) / kNmfPW, uh = (ntt + kNmfPW - 1) / kNmfPW;
     int ng = std::max(1, std::min((ntt + 3) / 4, waves / (4 * uw)));
     c->tpc_w = (ntt + 4 * ng - 1) / (4 * ng);
