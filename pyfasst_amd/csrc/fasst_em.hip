@@ -2842,74 +2842,88 @@ __global__ void k_renorm_final(const RArgs a, int J, int iter) {
 // Every thread issues its loads in batches before using any: the round-5
 // form walked the 129 maxima, the energy partials and the K x K FW as chains
 // of dependent loads (105 us beside the TW contraction, profiles/r5_bench.txt)
-__global__ __launch_bounds__(256) void k_renorm_scales(const RArgs a) {
+__global__ __launch_bounds__(1024) void k_renorm_scales(const RArgs a) {
   HALT_GUARD(a.halt);
-  constexpr int B = 8;   // loads in flight per thread and batch
-  __shared__ double s_red[256];
+  constexpr int NT = 1024, B = 16;   // threads; loads in flight per thread and batch
+  __shared__ double s_red[NT];
   __shared__ double s_w[kMaxKP];
-  const int j = blockIdx.x, K = a.K[j], KP = a.KP, ns = a.nstat;
+  const int t = threadIdx.x, j = blockIdx.x, K = a.K[j], KP = a.KP, ns = a.nstat;
   const int r0 = a.roff[j], nr = a.roff[j + 1] - r0;
   const bool cj = a.convm >> j & 1u;
-  // e_j: the 'conv' filters A[r][c][f] of the source's nr ranks
+  // e_j: the 'conv' filters A[r][c][f] of the source's nr ranks (one batch
+  // of loads per thread up to 8 ranks at C3's F)
   const int ne = cj ? nr * 2 * a.F : nr * 2;
   double e = 0.0;
-  for (int base = threadIdx.x; base < ne; base += B * blockDim.x) {
+  for (int base = t; base < ne; base += B * NT) {
     double2 x[B];
 #pragma unroll
     for (int u = 0; u < B; ++u) {
-      const int idx = base + u * blockDim.x;
+      const int idx = base + u * NT;
       x[u] = idx >= ne ? make_double2(0.0, 0.0)
                        : (cj ? a.A[(size_t)(2 * r0 + idx / a.F) * a.Fp + idx % a.F] : a.Pinst[2 * r0 + idx]);
     }
 #pragma unroll
     for (int u = 0; u < B; ++u) e += x[u].x * x[u].x + x[u].y * x[u].y;
   }
-  e = block_sum(e, s_red) / (double)ne;
   // column maxima over k_fb_update's blocks: thread (g, k) takes blocks
-  // q = g mod G (max is exact in any order)
-  const int G = (int)blockDim.x / KP;
+  // q = g mod G (max is exact in any order; 5 per thread at C3)
+  const int G = NT / KP;
   double m = -INFINITY;
-  if (threadIdx.x < G * KP)
-    for (int q0 = threadIdx.x / KP; q0 < ns; q0 += B * G) {
-      double x[B];
+  for (int q0 = t / KP; q0 < ns; q0 += B * G) {
+    double x[B];
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const int q = q0 + u * G;
-        x[u] = q < ns ? a.pmax2[((size_t)j * ns + q) * KP + threadIdx.x % KP] : -INFINITY;
-      }
-#pragma unroll
-      for (int u = 0; u < B; ++u) m = fmax(m, x[u]);
+    for (int u = 0; u < B; ++u) {
+      const int q = q0 + u * G;
+      x[u] = q < ns ? a.pmax2[((size_t)j * ns + q) * KP + t % KP] : -INFINITY;
     }
-  s_red[threadIdx.x] = m;
+#pragma unroll
+    for (int u = 0; u < B; ++u) m = fmax(m, x[u]);
+  }
+  // FW[r][c] of thread (g, c): rows r = g, g + G, ... (all of them in one
+  // batch up to K = 64 at KP = 64, K = 32 at KP = 32: one row per thread)
+  const int cc = t % KP;
+  const double *fw = a.FW + (size_t)j * KP * KP;
+  constexpr int RB = 8;
+  double fr[RB];
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int r = t / KP + u * G;
+    fr[u] = r < K && cc < K ? fw[r * KP + cc] : 0.0;
+  }
+  e = block_sum(e, s_red) / (double)ne;
+  s_red[t] = m;
   __syncthreads();
-  for (int k = threadIdx.x; k < KP; k += blockDim.x) {   // (KP <= kMaxKP < 256)
+  for (int k = t; k < KP; k += NT) {
     double x = -INFINITY;
     for (int g = 0; g < G; ++g) x = fmax(x, s_red[g * KP + k]);
     const double w = x * e;
     s_w[k] = w == 0.0 ? 1.0 : w;
   }
   __syncthreads();
+  // FW.mean(axis=0) of the column's spectral component: the thread's rows,
+  // then the groups in order (one row per group: the sequential row order)
+  double sp = 0.0;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int r = t / KP + u * G;
+    if (r < K) sp += fr[u] * s_w[r];
+  }
+  for (int r = t / KP + RB * G; r < K; r += G) sp += fw[r * KP + cc] * s_w[r];   // (K > RB G only)
+  s_red[t] = sp;
+  __syncthreads();
   double *sc = a.scal + (size_t)j * (2 + 2 * KP);
-  const double *fw = a.FW + (size_t)j * KP * KP;
-  for (int cc = threadIdx.x; cc < KP; cc += blockDim.x) {
+  if (t < KP) {
     double s = 1.0;
-    if (cc < K) {   // FW.mean(axis=0) of the column's spectral component, in row order
+    if (t < K) {
       s = 0.0;
-      for (int r0b = 0; r0b < K; r0b += B) {
-        double x[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) x[u] = r0b + u < K ? fw[(r0b + u) * KP + cc] : 0.0;
-#pragma unroll
-        for (int u = 0; u < B; ++u)
-          if (r0b + u < K) s += x[u] * s_w[r0b + u];
-      }
+      for (int g = 0; g < G; ++g) s += s_red[g * KP + t];
       s /= (double)K;
       if (s == 0.0) s = 1.0;
     }
-    sc[2 + cc] = s_w[cc];
-    sc[2 + KP + cc] = s;
+    sc[2 + t] = s_w[t];
+    sc[2 + KP + t] = s;
   }
-  if (threadIdx.x == 0) sc[0] = e;
+  if (t == 0) sc[0] = e;
 }
 
 // FB rows of 16 bins (FB e / w), the 'conv' filters / sqrt(e); block x = 0
@@ -3715,7 +3729,7 @@ static int launch_tail_side(fasst_ctx *c) {
   FASST_HIP(hipEventRecord(c->ev_tail, c->stream));
   FASST_HIP(hipStreamWaitEvent(c->aux, c->ev_tail, 0));
   prof_begin(c, KREN, side);
-  k_renorm_scales<<<c->J, 256, 0, side>>>(r);
+  k_renorm_scales<<<c->J, 1024, 0, side>>>(r);
   FASST_LAUNCH_CHECK();
   FASST_HIP(hipEventRecord(c->ev_scales, c->aux));
   k_renorm_rows<<<dim3(c->nft, c->J), 256, 0, side>>>(r);
