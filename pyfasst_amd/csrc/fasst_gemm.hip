@@ -157,7 +157,7 @@ int dgemm2(hipStream_t s, int M, int N, int K, const double *A, int lda, const d
     set_error("dgemm2: bad shape M %d N %d K %d (lda %d ldb %d ldc %d)", M, N, K, lda, ldb, ldc);
     return FASST_ERR_SHAPE;
   }
-  Dgemm2Args g;
+  Dgemm2Args g{};
   g.A = A;
   g.B = B;
   g.C = C;
