@@ -1012,41 +1012,63 @@ struct GArgs {
   int J;
 };
 
+// V_j of the tile: per source, its NKS TW / W operand pairs in chunks of CH,
+// every chunk's loads issued one chunk ahead of its MFMAs (two static register
+// buffers; the unrolled (source, chunk) sequence fixes which), so a wave waits
+// one memory round trip per chunk instead of one per MFMA.  The loads are
+// unconditional (a chunk past source J - 1 re-reads its last), so every path
+// reaches each wait with the same loads outstanding.
+template <int NKS>
 __global__ __launch_bounds__(64) void k_egen_point(const EArgs a, const GArgs g) {
   HALT_GUARD(a.halt);
+  constexpr int CH = NKS < 8 ? NKS : 8, NCH = NKS / CH, NST = kMaxJ * NCH;
   const int lane = threadIdx.x, fl = lane & 15, tq = lane >> 4;
   const int tt = blockIdx.x, ft = blockIdx.y, t0 = tt * 16, f0 = ft * 16, f = f0 + fl;
-  const int J = g.J, nks = a.KP >> 2;
+  const int J = g.J;
   __shared__ double s_c[kMaxJ][4][16];   // Sigma_x coefficients of the tile's bins
   __shared__ double s_irk[kMaxJ];
-  if (tq == 0)
-    for (int j = 0; j < J; ++j) {
-      double al = 0, be = 0, gr = 0, gi = 0;
-      for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
-        const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + f];
-        const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + f];
-        al += a0.x * a0.x + a0.y * a0.y;
-        be += a1.x * a1.x + a1.y * a1.y;
-        gr += a0.x * a1.x + a0.y * a1.y;
-        gi += a0.y * a1.x - a0.x * a1.y;
-      }
-      s_c[j][0][fl] = al;
-      s_c[j][1][fl] = be;
-      s_c[j][2][fl] = gr;
-      s_c[j][3][fl] = gi;
+  double ta[2][CH], wa[2][CH];
+  auto load = [&](int buf, int st) {
+    const int j = min(st / NCH, J - 1), s0 = (st % NCH) * CH;
+    const double *tw = a.TW + ((size_t)j * a.KP + tq + 4 * s0) * a.Tp + t0 + fl;
+    const double *wk = a.Wkf + ((size_t)j * a.KP + tq + 4 * s0) * a.Fp + f;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      ta[buf][u] = tw[(size_t)(4 * u) * a.Tp];
+      wa[buf][u] = wk[(size_t)(4 * u) * a.Fp];
     }
+  };
+  load(0, 0);
+  // lane (fl, tq): the coefficients of sources tq, tq + 4, ... of bin fl
+  for (int j = tq; j < J; j += 4) {
+    double al = 0, be = 0, gr = 0, gi = 0;
+    for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
+      const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + f];
+      const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + f];
+      al += a0.x * a0.x + a0.y * a0.y;
+      be += a1.x * a1.x + a1.y * a1.y;
+      gr += a0.x * a1.x + a0.y * a1.y;
+      gi += a0.y * a1.x - a0.x * a1.y;
+    }
+    s_c[j][0][fl] = al;
+    s_c[j][1][fl] = be;
+    s_c[j][2][fl] = gr;
+    s_c[j][3][fl] = gi;
+  }
   if (lane < J) s_irk[lane] = 1.0 / (double)(a.roff[lane + 1] - a.roff[lane]);
-  __syncthreads();
   d4 v[kMaxJ];
 #pragma unroll
-  for (int j = 0; j < kMaxJ; ++j) {
-    v[j] = d4{0.0, 0.0, 0.0, 0.0};
-    if (j < J) {   // (wave-uniform)
-      const double *tw = a.TW + ((size_t)j * a.KP + tq) * a.Tp + t0 + fl;
-      const double *wk = a.Wkf + ((size_t)j * a.KP + tq) * a.Fp + f;
-      for (int s = 0; s < nks; ++s) v[j] = mfma4(tw[(size_t)(4 * s) * a.Tp], wk[(size_t)(4 * s) * a.Fp], v[j]);
-    }
+  for (int j = 0; j < kMaxJ; ++j) v[j] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    const int j = st / NCH, cur = st & 1;
+    if (j >= J) break;   // (wave-uniform)
+    if (st + 1 < NST) load(cur ^ 1, st + 1);
+    asm volatile("" ::: "memory");   // (keeps the prefetch here, not sunk past the next break)
+#pragma unroll
+    for (int u = 0; u < CH; ++u) v[j] = mfma4(ta[cur][u], wa[cur][u], v[j]);
   }
+  __syncthreads();
   const size_t plane = (size_t)a.Tp * a.Fp;
   const double psd = a.psd[f];
   double ll = 0.0;
@@ -1105,72 +1127,111 @@ __global__ __launch_bounds__(64) void k_egen_point(const EArgs a, const GArgs g)
   if (lane == 0) g.lw[(size_t)tt * a.nft + ft] = ll;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_egen_stats(const EArgs a, const GArgs g) {
+// The statistics as 16x16x4 FP64 MFMAs per bin, frames as the k dimension:
+// with A[m = j1][k = t] = V_j1(t) and B[k = t][n = j2] = V_j2(t) N_c(t),
+// D[j1][j2] accumulates the pair sums of component c for all (j1, j2) at
+// once (the j1 > j2 half is discarded), and B[k = t][n = c] = P_c(t) gives
+// the cross sums D[j][c].  Lane (fl, tq) supplies the A and B operands of
+// row/column fl and frame tq from one LDS read of V_fl(t).  Block = 8 waves
+// on one (16-bin tile, frame chunk); wave wv owns bins 2 wv, 2 wv + 1 (five
+// 16x16 accumulators each).  A frame tile's J + 12 planes are staged point-
+// major in LDS ([16 frames][16 bins][RS], RS = (J + 12) | 1 so the 16 rows a
+// wave reads land on distinct banks), the next tile's values already in
+// flight in registers while the current one is summed.  (Was VALU pair FMAs
+// over the same staged tile at 5.48 ms for J = 16 at C3's size;
+// profiles/r6_struct_J16K32_sum.txt.)
+constexpr int kEgsThreads = 512;
+constexpr int kEgsRows = (kMaxJ + 12) | 1;
+__global__ __launch_bounds__(kEgsThreads) void k_egen_stats(const EArgs a, const GArgs g) {
   HALT_GUARD(a.halt);
-  // wave wv, lane (bin b, component n): the pair sums V_j1 V_j2 N_n of
-  // j1 = wv + 4 q (q < 4; wave-uniform, each over j2 = j1 .. J - 1) and the
-  // cross sums V_j P_c of source j = 4 wv + n; per frame a lane reads its
-  // bin's V_j, N and P once (registers) and V_j1 of each task from LDS
   const int J = g.J, NP = J * (J + 1) / 2, NACC = 4 * NP + 8 * J;
-  const int tid = threadIdx.x, lane = tid & 63, b = lane & 15, n = lane >> 4;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), jx = 4 * wv + n;
+  const int tid = threadIdx.x, lane = tid & 63, fl = lane & 15, tq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ft = blockIdx.x, f0 = ft * 16, y = blockIdx.y;
-  extern __shared__ __attribute__((aligned(16))) double s_t[];   // [J + 12][16 frames][16 bins]
-  double pacc[4][kMaxJ], xacc[8];
+  const int nr = J + 12, RS = nr | 1;
+  extern __shared__ __attribute__((aligned(16))) double s_t[];   // [16 frames][16 bins][RS]
+  d4 acc[2][5];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-    for (int j2 = 0; j2 < kMaxJ; ++j2) pacc[q][j2] = 0.0;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) xacc[c] = 0.0;
+    for (int c = 0; c < 5; ++c) acc[bi][c] = d4{0.0, 0.0, 0.0, 0.0};
   const size_t plane = (size_t)a.Tp * a.Fp;
   const int tb = a.tbase + y * a.tpc, te = min(tb + a.tpc, a.ntt);
-  const int nr = J + 12;
-  for (int tt = tb; tt < te; ++tt) {
-    __syncthreads();   // (the previous tile's reads)
-    for (int idx = tid; idx < nr * 256; idx += 256) {
-      const int r = idx >> 8, e = idx & 255, tl = e >> 4, fl = e & 15;
-      const size_t o = (size_t)(tt * 16 + tl) * a.Fp + f0 + fl;
-      s_t[idx] = r < J ? g.V[r * plane + o] : g.NP[(r - J) * plane + o];
-    }
-    __syncthreads();
-    for (int tl = 0; tl < 16; ++tl) {
-      const double *col = s_t + tl * 16 + b;   // row r at col[256 r]
-      double v[kMaxJ];
+  // staging: thread tid carries point e = tid & 255 of rows r = 2 k + (tid >> 8)
+  // (wave-uniform: each row's plane is a scalar base, the point a 32-bit offset)
+  const int e = tid & 255, rh = __builtin_amdgcn_readfirstlane(tid >> 8), etl = e >> 4, efl = e & 15;
+  constexpr int kPre = (kMaxJ + 12 + 1) / 2;
+  double pre[2][kPre];   // two tiles in flight
+  // Loads and stores unconditional (rows past nr repeat the last; a tile
+  // past the chunk re-reads its last and is never staged), so every path
+  // reaches the loop head with the same two batches outstanding and the
+  // older one is waited for alone.
+  auto load = [&](double(&p)[kPre], int tt) {
+    const unsigned o = (unsigned)((min(tt, te - 1) * 16 + etl) * a.Fp + f0 + efl);
 #pragma unroll
-      for (int j = 0; j < kMaxJ; ++j) v[j] = j < J ? col[256 * j] : 0.0;
-      const double nn = col[256 * (J + n)];
+    for (int k = 0; k < kPre; ++k) {
+      const int r = min(2 * k + rh, nr - 1);
+      const double *base = r < J ? g.V + r * plane : g.NP + (r - J) * plane;
+      p[k] = __builtin_nontemporal_load(base + o);
+    }
+  };
+  auto stage = [&](const double(&p)[kPre]) {
+    __syncthreads();   // (the previous tile's reads)
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) s_t[e * RS + min(2 * k + rh, nr - 1)] = p[k];
+    __syncthreads();
+  };
+  // MFMA operands: lane (fl, tq) reads V_fl (fl < J), N_0..3 and P_fl (fl <
+  // 8) of its point; out-of-range lanes read a valid slot and select zero
+  const int vcol = min(fl, J - 1), xcol = J + 4 + (fl & 7);
+  const bool vok = fl < J, xok = fl < 8;
+  auto sum_tile = [&]() {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi) {
+      const int b = 2 * wv + bi;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int j1 = wv + 4 * q;   // (wave-uniform: scalar branches)
-        if (j1 < J) {
-          const double vn = col[256 * j1] * nn;   // V_j1 N_n
-#pragma unroll
-          for (int j2 = 0; j2 < kMaxJ; ++j2)
-            if (j2 >= j1 && j2 < J) pacc[q][j2] = fma(vn, v[j2], pacc[q][j2]);
-        }
-      }
-      if (jx < J) {
-        const double vj = col[256 * jx];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) xacc[c] = fma(vj, col[256 * (J + 4 + c)], xacc[c]);
+        const double *pt = s_t + ((4 * q + tq) * 16 + b) * RS;   // point (frame 4 q + tq, bin b)
+        const double vr = pt[vcol], pr = pt[xcol];
+        const double n0 = pt[J], n1 = pt[J + 1], n2 = pt[J + 2], n3 = pt[J + 3];
+        const double v = vok ? vr : 0.0, px = xok ? pr : 0.0;
+        acc[bi][0] = mfma4(v, v * n0, acc[bi][0]);
+        acc[bi][1] = mfma4(v, v * n1, acc[bi][1]);
+        acc[bi][2] = mfma4(v, v * n2, acc[bi][2]);
+        acc[bi][3] = mfma4(v, v * n3, acc[bi][3]);
+        acc[bi][4] = mfma4(v, px, acc[bi][4]);
       }
     }
-  }
-  double *out = a.part + ((size_t)(a.ybase + y) * a.Fp + f0 + b) * NACC;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j1 = wv + 4 * q;
-    if (j1 < J) {
-      const int p0 = j1 * J - j1 * (j1 - 1) / 2;   // canonical index of (j1, j1)
-#pragma unroll
-      for (int j2 = 0; j2 < kMaxJ; ++j2)
-        if (j2 >= j1 && j2 < J) out[4 * (p0 + j2 - j1) + n] = pacc[q][j2];
+  };
+  if (tb < te) {
+    load(pre[0], tb);
+    load(pre[1], tb + 1);
+    for (int tt = tb; tt < te; tt += 2) {
+      stage(pre[0]);
+      load(pre[0], tt + 2);
+      sum_tile();
+      if (tt + 1 < te) {   // (block-uniform)
+        stage(pre[1]);
+        sum_tile();
+      }
+      load(pre[1], tt + 3);
     }
   }
-  if (jx < J)
+  // lane (fl, tq), register i: D[tq + 4 i][fl]
 #pragma unroll
-    for (int c = 0; c < 8; ++c) out[4 * NP + 8 * jx + c] = xacc[c];
+  for (int bi = 0; bi < 2; ++bi) {
+    double *out = a.part + ((size_t)(a.ybase + y) * a.Fp + f0 + 2 * wv + bi) * NACC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j1 = tq + 4 * i, j2 = fl;
+      if (j1 <= j2 && j2 < J) {
+        const int p = j1 * J - j1 * (j1 - 1) / 2 + j2 - j1;   // canonical index of (j1, j2)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[4 * p + c] = acc[bi][c][i];
+      }
+      if (j1 < J && fl < 8) out[4 * NP + 8 * j1 + fl] = acc[bi][4][i];
+    }
+  }
   if (tid == 0) {   // the chunk's loglik, its tiles in order
     double l = 0.0;
     for (int tt = tb; tt < te; ++tt) l += g.lw[(size_t)tt * a.nft + ft];
@@ -3288,7 +3349,7 @@ static int set_lds_limits() {
   const L lim[] = {
       {(const void *)k_fw_reduce, (size_t)3 * 32 * kMaxKP * sizeof(double)},
       {(const void *)k_fwh_t<true>, (size_t)(16 + 64) * kMaxKP * sizeof(double)},
-      {(const void *)k_egen_stats, (size_t)(kMaxJ + 12) * 256 * sizeof(double)},
+      {(const void *)k_egen_stats, (size_t)kEgsRows * 256 * sizeof(double)},
       {(const void *)k_mix<(4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64, (kMaxR * kMaxR + 63) / 64>,
        mix_smem(kMaxJ, kMaxR, kMaxKP, 4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ)},
   };
@@ -4471,9 +4532,14 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
     gg.lw = c->lgen.p;
     gg.J = J;
     prof_begin(c, KESTEP);
-    k_egen_point<<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg);
-    const size_t lds = (size_t)(J + 12) * 256 * sizeof(double);   // (ceiling: set_lds_limits)
-    k_egen_stats<<<dim3(c->nft, c->nchunk_e), 256, lds, c->stream>>>(e, gg);
+    switch (c->KP) {
+      case 16: k_egen_point<4><<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg); break;
+      case 32: k_egen_point<8><<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg); break;
+      case 64: k_egen_point<16><<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg); break;
+      default: k_egen_point<32><<<dim3(c->ntt, c->nft), 64, 0, c->stream>>>(e, gg); break;
+    }
+    const size_t lds = (size_t)((J + 12) | 1) * 256 * sizeof(double);   // (ceiling: set_lds_limits)
+    k_egen_stats<<<dim3(c->nft, c->nchunk_e), kEgsThreads, lds, c->stream>>>(e, gg);
     prof_end(c, KESTEP);
   } else {
     launch_estep(c, e, c->nchunk_e);
