@@ -1239,6 +1239,217 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_stats(const EArgs a, const
   }
 }
 
+// Fused many-source E-step (J > 8, KP <= 32): k_egen_point's point pass and
+// k_egen_stats' statistics in one block per (16-bin tile, frame chunk), V, N
+// and P never leaving the LDS slab (the two-pass form writes and re-reads
+// 28 planes, 4.6 GB at J = 16 and C3's size, and its point pass is bound by
+// those writes; profiles/r6_ab_egen_point.txt).  Per frame tile, three phases
+// between barriers:
+//   V      wave wv forms V of sources 2 wv, 2 wv + 1 on 16x16x4 MFMA (its W
+//          operands held in registers for the chunk, the next tile's TW
+//          operands loaded while the current tile is summed) into the slab;
+//   point  thread pair (2 e, 2 e + 1) owns point e: Sigma_x summed over the
+//          even / odd sources and combined across the pair, then both form
+//          the guarded inverse, P and N (the pair's halves write N and P to
+//          the slab) and rho of their own sources to global;
+//   stats  as k_egen_stats, from the slab.
+template <int NKS>
+__global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const GArgs g) {
+  HALT_GUARD(a.halt);
+  const int J = g.J, NP = J * (J + 1) / 2, NACC = 4 * NP + 8 * J;
+  const int tid = threadIdx.x, lane = tid & 63, fl = lane & 15, tq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ft = blockIdx.x, f0 = ft * 16, y = blockIdx.y;
+  const int nr = J + 12, RS = nr | 1;
+  const int tb = a.tbase + y * a.tpc, te = min(tb + a.tpc, a.ntt);
+  const size_t plane = (size_t)a.Tp * a.Fp;
+  extern __shared__ __attribute__((aligned(16))) double s_t[];   // [256 points][RS], then W
+  double *s_w = s_t + 256 * RS;           // [J][KP][16 bins]: the tile's W operands
+  __shared__ double s_cf[16][kMaxJ][4];   // Sigma_x coefficients per (bin, source)
+  __shared__ double s_irk[kMaxJ];
+  __shared__ double s_ll[kEgsThreads / 64];
+  if (tid < 16 * J) {
+    const int j = tid >> 4, b = tid & 15, f = f0 + b;
+    double al = 0, be = 0, gr = 0, gi = 0;
+    for (int r = a.roff[j]; r < a.roff[j + 1]; ++r) {
+      const double2 a0 = a.A[(size_t)(2 * r) * a.Fp + f];
+      const double2 a1 = a.A[(size_t)(2 * r + 1) * a.Fp + f];
+      al += a0.x * a0.x + a0.y * a0.y;
+      be += a1.x * a1.x + a1.y * a1.y;
+      gr += a0.x * a1.x + a0.y * a1.y;
+      gi += a0.y * a1.x - a0.x * a1.y;
+    }
+    s_cf[b][j][0] = al;
+    s_cf[b][j][1] = be;
+    s_cf[b][j][2] = gr;
+    s_cf[b][j][3] = gi;
+  }
+  if (tid < J) s_irk[tid] = 1.0 / (double)(a.roff[tid + 1] - a.roff[tid]);
+  constexpr int KP = 4 * NKS;
+  for (int idx = tid; idx < J * KP * 16; idx += kEgsThreads)
+    s_w[idx] = a.Wkf[(size_t)(idx >> 4) * a.Fp + f0 + (idx & 15)];
+  // V phase: sources ja, ja + 1 of this wave (clamped operands past J - 1)
+  const int ja = 2 * wv, jA = min(ja, J - 1), jB = min(ja + 1, J - 1);
+  const double *wA = s_w + (jA * KP + tq) * 16 + fl, *wB = s_w + (jB * KP + tq) * 16 + fl;
+  double tr[2][NKS];
+  auto load_tw = [&](int tt) {
+    const int t = min(tt, te - 1) * 16 + fl;
+    const double *tA = a.TW + ((size_t)jA * a.KP + tq) * a.Tp + t;
+    const double *tB = a.TW + ((size_t)jB * a.KP + tq) * a.Tp + t;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      tr[0][s] = tA[(size_t)(4 * s) * a.Tp];
+      tr[1][s] = tB[(size_t)(4 * s) * a.Tp];
+    }
+  };
+  // point phase: point e = (frame tl, bin b), half h (even / odd sources)
+  const int e = tid >> 1, h = tid & 1, tl = e >> 4, b = e & 15, f = f0 + b;
+  const double psd = a.psd[f];
+  double cx[4];
+  auto load_cx = [&](int tt) {
+    const size_t o = (size_t)(min(tt, te - 1) * 16 + tl) * a.Fp + f;
+    cx[0] = a.cx00[o];
+    cx[1] = a.cx11[o];
+    cx[2] = a.cxr[o];
+    cx[3] = a.cxi[o];
+  };
+  d4 acc[2][5];
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) acc[bi][c] = d4{0.0, 0.0, 0.0, 0.0};
+  const int vcol = min(fl, J - 1), xcol = J + 4 + (fl & 7);
+  const bool vok = fl < J, xok = fl < 8;
+  double ll = 0.0;
+  if (tb < te) {
+    load_tw(tb);
+    load_cx(tb);
+  }
+  for (int tt = tb; tt < te; ++tt) {
+    __syncthreads();   // (the slab's previous readers; at the first tile, s_cf)
+    {
+      d4 vA = d4{0.0, 0.0, 0.0, 0.0}, vB = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        vA = mfma4(tr[0][s], wA[64 * s], vA);
+        vB = mfma4(tr[1][s], wB[64 * s], vB);
+      }
+      load_tw(tt + 1);
+      if (ja < J)   // (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_t[((tq + 4 * i) * 16 + fl) * RS + ja] = vA[i];
+      if (ja + 1 < J)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_t[((tq + 4 * i) * 16 + fl) * RS + ja + 1] = vB[i];
+    }
+    __syncthreads();
+    {
+      double *pt = s_t + e * RS;
+      double d0 = 0.0, d1 = 0.0, ore = 0.0, oim = 0.0;
+#pragma unroll
+      for (int m = 0; m < kMaxJ / 2; ++m) {
+        const int j = 2 * m + h, jc = min(j, J - 1);
+        const double vr = pt[jc], vj = j < J ? vr : 0.0;
+        d0 = fma(s_cf[b][jc][0], vj, d0);
+        d1 = fma(s_cf[b][jc][1], vj, d1);
+        ore = fma(s_cf[b][jc][2], vj, ore);
+        oim = fma(s_cf[b][jc][3], vj, oim);
+      }
+      d0 = psd + (d0 + __shfl_xor(d0, 1, 64));
+      d1 = psd + (d1 + __shfl_xor(d1, 1, 64));
+      ore += __shfl_xor(ore, 1, 64);
+      oim += __shfl_xor(oim, 1, 64);
+      const double x00 = cx[0], x11 = cx[1], xr = cx[2], xi = cx[3];
+      load_cx(tt + 1);
+      // inv_herm_mat_2d (signalTools.py:177-194)
+      double det = d0 * d1 - (ore * ore + oim * oim);
+      const double dg = det + kEps;
+      det = (dg > 0.0 ? 1.0 : (dg < 0.0 ? -1.0 : 0.0)) * fmax(fabs(det), kEps);
+      const double rdet = rcp_nr(det);
+      const double i0 = d1 * rdet, i1 = d0 * rdet, ior = -ore * rdet, ioi = -oim * rdet;
+      const int t = tt * 16 + tl;
+      if (h == 0 && f < a.F && t < a.T)
+        ll += log(det * M_PI) + (i0 * x00 + i1 * x11 + 2.0 * (ior * xr + ioi * xi));
+      double P[8], N[4];
+      P[0] = x00 * i0 + xr * ior + xi * ioi;
+      P[1] = xi * ior - xr * ioi;
+      P[2] = x00 * ior + xr * i1;
+      P[3] = x00 * ioi + xi * i1;
+      P[4] = xr * i0 + x11 * ior;
+      P[5] = -xi * i0 - x11 * ioi;
+      P[6] = xr * ior + xi * ioi + x11 * i1;
+      P[7] = xr * ioi - xi * ior;
+      N[0] = P[0] * i0 + (P[4] * ior - P[5] * ioi) - i0;
+      N[1] = (P[2] * ior + P[3] * ioi) + P[6] * i1 - i1;
+      N[2] = P[0] * ior + P[1] * ioi + P[4] * i1 - ior;
+      N[3] = P[0] * ioi - P[1] * ior - P[5] * i1 - ioi;
+      if (h == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pt[J + c] = N[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pt[J + 4 + c] = P[c];
+      }
+      const size_t o = (size_t)t * a.Fp + f;
+      // (sources past J - 1 clamp to J - 1 and store the very value its
+      // owner stores -- both halves hold bit-identical N -- so the stores
+      // need no lane-divergent branch)
+#pragma unroll
+      for (int m = 0; m < kMaxJ / 2; ++m) {
+        const int j = min(2 * m + h, J - 1);
+        // rho = |V q + 1| min(V / eps, 1), q the rank-merged quadratic form
+        const double q = ((s_cf[b][j][0] * N[0] + s_cf[b][j][1] * N[1]) +
+                          2.0 * (s_cf[b][j][2] * N[2] + s_cf[b][j][3] * N[3])) * s_irk[j];
+        const double vj = pt[j];
+        __builtin_nontemporal_store(fabs(fma(vj, q, 1.0)) * fmin(vj * (1.0 / kEps), 1.0),
+                                    a.hatW + j * plane + o);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi) {
+      const int bb = 2 * wv + bi;
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        const double *pt = s_t + ((4 * q + tq) * 16 + bb) * RS;   // point (frame 4 q + tq, bin bb)
+        const double vr = pt[vcol], pr = pt[xcol];
+        const double n0 = pt[J], n1 = pt[J + 1], n2 = pt[J + 2], n3 = pt[J + 3];
+        const double v = vok ? vr : 0.0, px = xok ? pr : 0.0;
+        acc[bi][0] = mfma4(v, v * n0, acc[bi][0]);
+        acc[bi][1] = mfma4(v, v * n1, acc[bi][1]);
+        acc[bi][2] = mfma4(v, v * n2, acc[bi][2]);
+        acc[bi][3] = mfma4(v, v * n3, acc[bi][3]);
+        acc[bi][4] = mfma4(v, px, acc[bi][4]);
+      }
+    }
+  }
+  // lane (fl, tq), register i: D[tq + 4 i][fl]
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    double *out = a.part + ((size_t)(a.ybase + y) * a.Fp + f0 + 2 * wv + bi) * NACC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j1 = tq + 4 * i, j2 = fl;
+      if (j1 <= j2 && j2 < J) {
+        const int p = j1 * J - j1 * (j1 - 1) / 2 + j2 - j1;   // canonical index of (j1, j2)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[4 * p + c] = acc[bi][c][i];
+      }
+      if (j1 < J && fl < 8) out[4 * NP + 8 * j1 + fl] = acc[bi][4][i];
+    }
+  }
+  // the chunk's loglik: lanes in order within a wave, then waves in order
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) ll += __shfl_xor(ll, m, 64);
+  if (lane == 0) s_ll[wv] = ll;
+  __syncthreads();
+  if (tid == 0) {
+    double l = 0.0;
+    for (int w = 0; w < kEgsThreads / 64; ++w) l += s_ll[w];
+    a.llpart[(a.ybase + y) * a.nft + ft] = l;
+  }
+}
+
 // sum_t TW[j][k][t] (for mean_t V_j = W_j . sum_t H_j, the hat_Rss diagonal term)
 __global__ void k_tw_rowsum(const double *__restrict__ TW, double *__restrict__ hsum, int T,
                             int Tp, const int *halt) {
@@ -3350,6 +3561,8 @@ static int set_lds_limits() {
       {(const void *)k_fw_reduce, (size_t)3 * 32 * kMaxKP * sizeof(double)},
       {(const void *)k_fwh_t<true>, (size_t)(16 + 64) * kMaxKP * sizeof(double)},
       {(const void *)k_egen_stats, (size_t)kEgsRows * 256 * sizeof(double)},
+      {(const void *)k_egen_fused<4>, (size_t)(kEgsRows * 256 + kMaxJ * 16 * 16) * sizeof(double)},
+      {(const void *)k_egen_fused<8>, (size_t)(kEgsRows * 256 + kMaxJ * 32 * 16) * sizeof(double)},
       {(const void *)k_mix<(4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ + 63) / 64, (kMaxR * kMaxR + 63) / 64>,
        mix_smem(kMaxJ, kMaxR, kMaxKP, 4 * (kMaxJ * (kMaxJ + 1) / 2) + 8 * kMaxJ)},
   };
@@ -3505,7 +3718,7 @@ int configure_model(fasst_ctx *c, int J, const int *rank, const int *K, const in
   ALLOC(rtpart2, (size_t)kMaxSlot * c->ntb);
   ALLOC(Wkf_next, (size_t)J * KP * Fp);
   ALLOC(hpart, (size_t)J * KP * c->ntb);
-  if (J > 8) {   // the two-pass E-step's scratch: V_j, N, P planes and per-tile logliks
+  if (J > 8 && KP > 32) {   // the two-pass E-step's scratch: V_j, N, P planes and per-tile logliks
     ALLOC(vgen, (size_t)J * Tp * Fp);
     ALLOC(npgen, (size_t)12 * Tp * Fp);
     ALLOC(lgen, (size_t)c->ntt * c->nft);
@@ -4525,7 +4738,17 @@ static int gem_iteration(fasst_ctx *c, const double *psd_dev, double *ll_dev, do
   e.nft = c->nft;
   for (int j = 0; j <= kMaxJ; ++j) e.roff[j] = j <= J ? c->roff[j] : c->R;
   e.ybase = e.tbase = 0;
-  if (J > 8) {   // the two-pass E-step (k_egen_point / k_egen_stats)
+  if (J > 8 && c->KP <= 32) {   // the fused many-source E-step
+    GArgs gg{};
+    gg.J = J;
+    const size_t lds = (size_t)(((J + 12) | 1) * 256 + J * c->KP * 16) * sizeof(double);   // (ceiling: set_lds_limits)
+    prof_begin(c, KESTEP);
+    if (c->KP == 16)
+      k_egen_fused<4><<<dim3(c->nft, c->nchunk_e), kEgsThreads, lds, c->stream>>>(e, gg);
+    else
+      k_egen_fused<8><<<dim3(c->nft, c->nchunk_e), kEgsThreads, lds, c->stream>>>(e, gg);
+    prof_end(c, KESTEP);
+  } else if (J > 8) {   // the two-pass E-step (k_egen_point / k_egen_stats)
     GArgs gg{};
     gg.V = c->vgen.p;
     gg.NP = c->npgen.p;
