@@ -1265,7 +1265,11 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
   const size_t plane = (size_t)a.Tp * a.Fp;
   extern __shared__ __attribute__((aligned(16))) double s_t[];   // [256 points][RS], then W
   double *s_w = s_t + 256 * RS;           // [J][KP][16 bins]: the tile's W operands
-  __shared__ double s_cf[16][kMaxJ][4];   // Sigma_x coefficients per (bin, source)
+  // Sigma_x coefficients per (source, component, bin), the source stride 80
+  // doubles (= 16 mod 32 banks) so a half-wave's 16 bins x even / odd
+  // sources fall on 32 distinct banks
+  __shared__ double s_cfb[kMaxJ][80];
+  auto cf = [&](int b, int j, int c) -> double & { return s_cfb[j][16 * c + b]; };
   __shared__ double s_irk[kMaxJ];
   __shared__ double s_ll[kEgsThreads / 64];
   if (tid < 16 * J) {
@@ -1279,10 +1283,10 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
       gr += a0.x * a1.x + a0.y * a1.y;
       gi += a0.y * a1.x - a0.x * a1.y;
     }
-    s_cf[b][j][0] = al;
-    s_cf[b][j][1] = be;
-    s_cf[b][j][2] = gr;
-    s_cf[b][j][3] = gi;
+    cf(b, j, 0) = al;
+    cf(b, j, 1) = be;
+    cf(b, j, 2) = gr;
+    cf(b, j, 3) = gi;
   }
   if (tid < J) s_irk[tid] = 1.0 / (double)(a.roff[tid + 1] - a.roff[tid]);
   constexpr int KP = 4 * NKS;
@@ -1350,10 +1354,10 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
       for (int m = 0; m < kMaxJ / 2; ++m) {
         const int j = 2 * m + h, jc = min(j, J - 1);
         const double vr = pt[jc], vj = j < J ? vr : 0.0;
-        d0 = fma(s_cf[b][jc][0], vj, d0);
-        d1 = fma(s_cf[b][jc][1], vj, d1);
-        ore = fma(s_cf[b][jc][2], vj, ore);
-        oim = fma(s_cf[b][jc][3], vj, oim);
+        d0 = fma(cf(b, jc, 0), vj, d0);
+        d1 = fma(cf(b, jc, 1), vj, d1);
+        ore = fma(cf(b, jc, 2), vj, ore);
+        oim = fma(cf(b, jc, 3), vj, oim);
       }
       d0 = psd + (d0 + __shfl_xor(d0, 1, 64));
       d1 = psd + (d1 + __shfl_xor(d1, 1, 64));
@@ -1398,8 +1402,8 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
       for (int m = 0; m < kMaxJ / 2; ++m) {
         const int j = min(2 * m + h, J - 1);
         // rho = |V q + 1| min(V / eps, 1), q the rank-merged quadratic form
-        const double q = ((s_cf[b][j][0] * N[0] + s_cf[b][j][1] * N[1]) +
-                          2.0 * (s_cf[b][j][2] * N[2] + s_cf[b][j][3] * N[3])) * s_irk[j];
+        const double q = ((cf(b, j, 0) * N[0] + cf(b, j, 1) * N[1]) +
+                          2.0 * (cf(b, j, 2) * N[2] + cf(b, j, 3) * N[3])) * s_irk[j];
         const double vj = pt[j];
         __builtin_nontemporal_store(fabs(fma(vj, q, 1.0)) * fmin(vj * (1.0 / kEps), 1.0),
                                     a.hatW + j * plane + o);
