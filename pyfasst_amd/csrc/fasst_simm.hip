@@ -307,19 +307,27 @@ __global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(const SPl p, const doubl
   for (int q = 0; q < NO; ++q)
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc[q][i] = d4{0.0, 0.0, 0.0, 0.0};
+  // Every operand of a 16-bin step is loaded unconditionally, in one batch:
+  // a bin past the chunk re-reads the chunk's last bin and a frame past N the
+  // last frame (finite values: hat_of floors at eps), and the step's WM rows
+  // are zeroed for them instead, so the MFMAs add exact zeros and columns
+  // past N are never stored.  (Guarded loads compiled into one exec branch
+  // per load with a full vmcnt wait before the MFMAs.)
+  const int nc = min(n, N - 1);
   for (int k0 = kb; k0 < ke; k0 += 16) {
-    double sfv[4], smv[NC][4], sv[NC][4];
+    double sfv[4], smv[NC][4], sv[NC][4], wa[4][3];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int f = k0 + 4 * s + tq;
-      const bool ok = nin && f < ke;
-      const size_t idx = (size_t)f * N + n;
-      sfv[s] = ok ? CLD(p.SF0[idx]) : 0.0;
+      const int f = min(k0 + 4 * s + tq, ke - 1);
+      const size_t idx = (size_t)f * N + nc;
+      sfv[s] = CLD(p.SF0[idx]);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        smv[c][s] = ok ? CLD(sm[c][idx]) : 0.0;
-        sv[c][s] = ok ? CLD(ss[c][idx]) : 0.0;
+        smv[c][s] = CLD(sm[c][idx]);
+        sv[c][s] = CLD(ss[c][idx]);
       }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) wa[s][i] = WM[(size_t)f * R + min(i * 16 + fl, R - 1)];
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -329,20 +337,16 @@ __global__ __launch_bounds__(256, 2) void k_simm_wmt_xy(const SPl p, const doubl
         sfv[s] *= cs;
         if (nin && fok) SST(p.SF0w[(size_t)f * N + n], sfv[s]);
       }
-      const double sp = fok ? sphi_of<KM>(sW + (size_t)(f - kb) * K, h, K) : 0.0;
+      const double sp = sphi_of<KM>(sW + (size_t)(min(f, ke - 1) - kb) * K, h, K);
       double hv[2];
       hat_of<ST>(sfv[s], sp, smv[0][s], ST ? smv[NC - 1][s] : 0.0, aR2, aL2, hv[0], hv[1]);
       double a[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int r = i * 16 + fl;
-        a[i] = (fok && r < R) ? WM[(size_t)f * R + r] : 0.0;  // zero rows outside [kb, ke)
-      }
+      for (int i = 0; i < 3; ++i) a[i] = (fok && i * 16 + fl < R) ? wa[s][i] : 0.0;  // zero rows outside [kb, ke)
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double x, y;
         xy_of<ST>(hv[c], sv[c][s], x, y);
-        if (!(nin && fok)) x = y = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           acc[2 * c][i] = gmfma(a[i], x, acc[2 * c][i]);
@@ -409,23 +413,28 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
   // chunk column of MFMA j's k = tq, and its staged position
   auto kcol = [&](int j) { return V16 ? 8 * (j >> 1) + 2 * tq + (j & 1) : tq + 4 * j; };
   auto kpos = [&](int k) { return V16 ? (k & 1) * (KC / 2) + (k >> 1) : k; };
+  // Every load of a chunk is issued unconditionally, in one batch: a row
+  // past F re-reads row F - 1 and a frame past the chunk the chunk's last
+  // frame (finite values: hat_of floors at eps); the staged B operand (HM's
+  // chunk) is zero for those frames, so their products are exact zeros, and
+  // rows past F are never stored.  (Guarded loads compiled into one exec
+  // branch per load with a full vmcnt wait before the MFMAs.)
+  const int fr = min(f, F - 1);
   for (int kc = kb; kc < ke; kc += KC) {
-    const size_t base = (size_t)f * N + kc + tq;
     double sfv[NJ], smv[NC][NJ], sv[NC][NJ];
     if constexpr (V16) {
       typedef double dv2 __attribute__((ext_vector_type(2)));
-      const size_t b2 = (size_t)f * N + kc + 2 * tq;
 #pragma unroll
       for (int j = 0; j < NJ / 2; ++j) {
-        const bool ok = fin && kc + 8 * j + 2 * tq < ke;   // pairs never straddle ke (even)
-        const dv2 z = {0.0, 0.0};
-        const dv2 a0 = ok ? *(const dv2 *)(p.SF0 + b2 + 8 * j) : z;
+        // (pairs never straddle ke: N, the chunk bounds and ke are even)
+        const size_t b2 = (size_t)fr * N + min(kc + 8 * j + 2 * tq, ke - 2);
+        const dv2 a0 = *(const dv2 *)(p.SF0 + b2);
         sfv[2 * j] = a0.x;
         sfv[2 * j + 1] = a0.y;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          const dv2 a1 = ok ? *(const dv2 *)(sm[c] + b2 + 8 * j) : z;
-          const dv2 a2 = ok ? *(const dv2 *)(ss[c] + b2 + 8 * j) : z;
+          const dv2 a1 = *(const dv2 *)(sm[c] + b2);
+          const dv2 a2 = *(const dv2 *)(ss[c] + b2);
           smv[c][2 * j] = a1.x;
           smv[c][2 * j + 1] = a1.y;
           sv[c][2 * j] = a2.x;
@@ -435,28 +444,28 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
     } else {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const bool ok = fin && kc + tq + 4 * j < ke;
         // plain (cached) loads: a lane group reads 32 bytes of a row per
         // instruction, the rest of the line arrives with the next j's
-        sfv[j] = ok ? p.SF0[base + 4 * j] : 0.0;
+        const size_t i = (size_t)fr * N + min(kc + tq + 4 * j, ke - 1);
+        sfv[j] = p.SF0[i];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          smv[c][j] = ok ? sm[c][base + 4 * j] : 0.0;
-          sv[c][j] = ok ? ss[c][base + 4 * j] : 0.0;
+          smv[c][j] = sm[c][i];
+          sv[c][j] = ss[c][i];
         }
       }
     }
-    double hm[(NR * KC + 255) / 256];  // chunk of HM (48 rows), HPHI (8 rows), pend
+    double hm[(NR * KC + 255) / 256];  // chunk of HM (48 rows), HPHI (KM rows), pend
 #pragma unroll
     for (int t = 0; t < (NR * KC + 255) / 256; ++t) {
-      const int e = tid + 256 * t, r = e / KC, k = e % KC, col = kc + k;
-      double v = 0.0;
-      if (col < ke) {
-        if (r < 48) v = r < R ? HM[(size_t)r * N + col] : 0.0;
-        else if (r < 48 + KM) v = r - 48 < K ? p.HPHI[(size_t)(r - 48) * N + col] : 0.0;
-        else if (r == NR - 1) v = p.pend ? p.pend[col] : 1.0;
-      }
-      hm[t] = v;
+      const int e = tid + 256 * t, r = min(e / KC, NR - 1), col = kc + e % KC, cc = min(col, ke - 1);
+      // (a clamped, always valid address per row kind; the value selected after)
+      const double *src = r < 48 ? HM + (size_t)min(r, R - 1) * N + cc
+                          : r < 48 + KM ? p.HPHI + (size_t)min(r - 48, K - 1) * N + cc
+                                        : (p.pend ? p.pend + cc : HM + cc);
+      const double v = *src;
+      const bool valid = r < 48 ? r < R : r < 48 + KM ? r - 48 < K : p.pend != nullptr;
+      hm[t] = col >= ke ? 0.0 : valid ? v : (r == NR - 1 ? 1.0 : 0.0);
     }
     __syncthreads();
 #pragma unroll
@@ -486,7 +495,6 @@ __global__ __launch_bounds__(256, 2) void k_simm_xy_hmt(const SPl p, const doubl
       for (int c = 0; c < NC; ++c) {
         double x, y;
         xy_of<ST>(hv[c], sv[c][j], x, y);
-        if (!ok) x = y = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           acc[2 * c][i] = gmfma(x, b[i], acc[2 * c][i]);
