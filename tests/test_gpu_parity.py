@@ -236,6 +236,9 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     # headline structure and of 8 sources (oracle ~30 s / ~15 s on the host)
     (2049, 1000, 4, 32, 2, 2),
     (2049, 500, 8, 32, 1, 2),
+    # the fused many-source E-step (k_egen_fused) at the full F: 129 bin
+    # tiles, the production frame chunks, J = 16 at rank 2 (total rank 32)
+    (2049, 96, 16, 32, 2, 1),
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
