@@ -1317,13 +1317,20 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
     cx[2] = a.cxr[o];
     cx[3] = a.cxi[o];
   };
-  d4 acc[2][5];
+  // statistics phase: v_mfma_f64_4x4x4_4b with block = bin (lane = 16 X +
+  // 4 b + Y: A[m=Y][k=X], B[k=X][n=Y], D[m=X][n=Y] of block b), k = frame.
+  // Wave wv owns bin quad bq = wv / 2 (bins 4 bq + b) and half hf = wv % 2:
+  // the pair blocks (j1 block jb1 <= j2 block jb2, 4 sources each) of
+  // components 2 hf, 2 hf + 1 and the cross blocks of sources 8 hf .. 8 hf + 7
+  // -- 24 one-double accumulators, upper-triangle blocks only (40% fewer
+  // matrix cycles than all 16 x 16 pairs on 16x16x4)
+  const int X = lane >> 4, Yl = lane & 3, bq = wv >> 1, hf = wv & 1;
+  const int sbin = 4 * bq + ((lane >> 2) & 3);
+  double accp[10][2], accx[2][2];
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
+  for (int pb = 0; pb < 10; ++pb) accp[pb][0] = accp[pb][1] = 0.0;
 #pragma unroll
-    for (int c = 0; c < 5; ++c) acc[bi][c] = d4{0.0, 0.0, 0.0, 0.0};
-  const int vcol = min(fl, J - 1), xcol = J + 4 + (fl & 7);
-  const bool vok = fl < J, xok = fl < 8;
+  for (int u = 0; u < 2; ++u) accx[u][0] = accx[u][1] = 0.0;
   double ll = 0.0;
   if (tb < te) {
     load_tw(tb);
@@ -1410,36 +1417,66 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi) {
-      const int bb = 2 * wv + bi;
 #pragma unroll 1
-      for (int q = 0; q < 4; ++q) {
-        const double *pt = s_t + ((4 * q + tq) * 16 + bb) * RS;   // point (frame 4 q + tq, bin bb)
-        const double vr = pt[vcol], pr = pt[xcol];
-        const double n0 = pt[J], n1 = pt[J + 1], n2 = pt[J + 2], n3 = pt[J + 3];
-        const double v = vok ? vr : 0.0, px = xok ? pr : 0.0;
-        acc[bi][0] = mfma4(v, v * n0, acc[bi][0]);
-        acc[bi][1] = mfma4(v, v * n1, acc[bi][1]);
-        acc[bi][2] = mfma4(v, v * n2, acc[bi][2]);
-        acc[bi][3] = mfma4(v, v * n3, acc[bi][3]);
-        acc[bi][4] = mfma4(v, px, acc[bi][4]);
+    for (int g = 0; g < 4; ++g) {
+      const double *pt = s_t + ((4 * g + X) * 16 + sbin) * RS;   // point (frame 4 g + X, bin sbin)
+      double va[4], bn[4][2], px[2];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int jj = 4 * jb + Yl;
+        const double v = pt[min(jj, J - 1)];
+        va[jb] = jj < J ? v : 0.0;
+      }
+      const double nc0 = pt[J + 2 * hf], nc1 = pt[J + 2 * hf + 1];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        bn[jb][0] = va[jb] * nc0;
+        bn[jb][1] = va[jb] * nc1;
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) px[cb] = pt[J + 4 + 4 * cb + Yl];
+      // (the ten blocks spelled out: constant register indices)
+#define EGF_PB(pb, j1b, j2b)                                              \
+  if (4 * (j2b) < J) {   /* (wave-uniform) */                             \
+    accp[pb][0] = mfma44(va[j1b], bn[j2b][0], accp[pb][0]);              \
+    accp[pb][1] = mfma44(va[j1b], bn[j2b][1], accp[pb][1]);              \
+  }
+      EGF_PB(0, 0, 0) EGF_PB(1, 0, 1) EGF_PB(2, 0, 2) EGF_PB(3, 0, 3) EGF_PB(4, 1, 1)
+      EGF_PB(5, 1, 2) EGF_PB(6, 1, 3) EGF_PB(7, 2, 2) EGF_PB(8, 2, 3) EGF_PB(9, 3, 3)
+#undef EGF_PB
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (4 * (2 * hf + u) >= J) continue;   // (wave-uniform)
+        // (its own LDS read: selecting va[2 hf + u] became a scratch access)
+        const int jj = 4 * (2 * hf + u) + Yl;
+        const double vr = pt[min(jj, J - 1)], vs = jj < J ? vr : 0.0;
+        accx[u][0] = mfma44(vs, px[0], accx[u][0]);
+        accx[u][1] = mfma44(vs, px[1], accx[u][1]);
       }
     }
   }
-  // lane (fl, tq), register i: D[tq + 4 i][fl]
+  // lane (X, b, Y) holds D[X][Y] of its bin: pair (4 jb1 + X, 4 jb2 + Y),
+  // cross (source 4 jb + X, component 4 cb + Y)
+  {
+    double *out = a.part + ((size_t)(a.ybase + y) * a.Fp + f0 + sbin) * NACC;
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi) {
-    double *out = a.part + ((size_t)(a.ybase + y) * a.Fp + f0 + 2 * wv + bi) * NACC;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j1 = tq + 4 * i, j2 = fl;
+    for (int pb = 0; pb < 10; ++pb) {
+      const int jb1 = pb < 4 ? 0 : pb < 7 ? 1 : pb < 9 ? 2 : 3;
+      const int jb2 = pb < 4 ? pb : pb < 7 ? pb - 3 : pb < 9 ? pb - 5 : 3;
+      const int j1 = 4 * jb1 + X, j2 = 4 * jb2 + Yl;
       if (j1 <= j2 && j2 < J) {
         const int p = j1 * J - j1 * (j1 - 1) / 2 + j2 - j1;   // canonical index of (j1, j2)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) out[4 * p + c] = acc[bi][c][i];
+        out[4 * p + 2 * hf] = accp[pb][0];
+        out[4 * p + 2 * hf + 1] = accp[pb][1];
       }
-      if (j1 < J && fl < 8) out[4 * NP + 8 * j1 + fl] = acc[bi][4][i];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = 4 * (2 * hf + u) + X;
+      if (j < J) {
+        out[4 * NP + 8 * j + Yl] = accx[u][0];
+        out[4 * NP + 8 * j + 4 + Yl] = accx[u][1];
+      }
     }
   }
   // the chunk's loglik: lanes in order within a wave, then waves in order
