@@ -1356,11 +1356,12 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
     __syncthreads();
     {
       double *pt = s_t + e * RS;
-      double d0 = 0.0, d1 = 0.0, ore = 0.0, oim = 0.0;
+      double d0 = 0.0, d1 = 0.0, ore = 0.0, oim = 0.0, vk[kMaxJ / 2];
 #pragma unroll
       for (int m = 0; m < kMaxJ / 2; ++m) {
         const int j = 2 * m + h, jc = min(j, J - 1);
-        const double vr = pt[jc], vj = j < J ? vr : 0.0;
+        vk[m] = pt[jc];   // (kept for rho below)
+        const double vj = j < J ? vk[m] : 0.0;
         d0 = fma(cf(b, jc, 0), vj, d0);
         d1 = fma(cf(b, jc, 1), vj, d1);
         ore = fma(cf(b, jc, 2), vj, ore);
@@ -1411,7 +1412,7 @@ __global__ __launch_bounds__(kEgsThreads) void k_egen_fused(const EArgs a, const
         // rho = |V q + 1| min(V / eps, 1), q the rank-merged quadratic form
         const double q = ((cf(b, j, 0) * N[0] + cf(b, j, 1) * N[1]) +
                           2.0 * (cf(b, j, 2) * N[2] + cf(b, j, 3) * N[3])) * s_irk[j];
-        const double vj = pt[j];
+        const double vj = vk[m];   // (= pt[j]: the same clamped source)
         __builtin_nontemporal_store(fabs(fma(vj, q, 1.0)) * fmin(vj * (1.0 / kEps), 1.0),
                                     a.hatW + j * plane + o);
       }
