@@ -239,6 +239,8 @@ def _c3_like(F, T, J, K, rank, iters, seed=0):
     # the fused many-source E-step (k_egen_fused) at the full F: 129 bin
     # tiles, the production frame chunks, J = 16 at rank 2 (total rank 32)
     (2049, 96, 16, 32, 2, 1),
+    # ... its KP = 16 form with an odd J, ragged T, rank 1
+    (1025, 77, 11, 12, 1, 2),
 ])
 def test_em_stft_domain_vs_oracle(F, T, J, K, rank, iters):
     m, o, X = _c3_like(F, T, J, K, rank, iters)
