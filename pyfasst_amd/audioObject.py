@@ -1,10 +1,12 @@
-"""Audio I/O (audioObject.py of the reference, scipy.io.wavfile branch).
+"""Audio I/O (audioObject.py of the reference, its scipy.io.wavfile branch).
 
-`AudioObject` reads a WAV and rescales it by max(1.1*max|x|, 1e-10)
-(audioObject.py:112-127); `_write` mirrors wavwrite's encoding choice
-(:83-98).  `SpectralAudio` is an addition: an in-memory observation given
-directly in the STFT domain (channel STFTs X or the packed covariance Cx),
-used for the synthetic STFT-domain benchmarks of BASELINE.json.
+`AudioObject` is a lazily loaded WAV file whose samples are exposed divided
+by max(1.1 max|x|, 1e-10) (audioObject.py:112-127), the scale the FASST model
+code relies on; writing multiplies it back and picks the integer encoding as
+the reference's `wavwrite` does (:83-98).  `SpectralAudio` is an addition: an
+in-memory observation given directly in the STFT domain (channel STFTs X or
+the packed covariance Cx), used for the synthetic STFT-domain benchmarks of
+BASELINE.json.
 """
 import warnings
 
@@ -13,74 +15,86 @@ import scipy.io.wavfile as wav
 
 from .tools.utils import nextpow2, sinebell, hann  # noqa: F401 (re-exported like the reference)
 
+_INT_ENCODINGS = ('int16', 'int32', 'int8')
+
+
+def _smallest_int_encoding(data):
+    """The narrowest of int8 / int16 / int32 whose range the peak needs
+    (thresholds 2**7 and 2**15, as the reference's wavwrite)."""
+    peak = np.abs(data).max()
+    for limit, enc in ((2 ** 15, 'int32'), (2 ** 7, 'int16')):
+        if peak > limit:
+            return enc
+    return 'int8'
+
 
 def wavread(filename, first=0, last=None):
-    fs, data = wav.read(filename)
-    data = data[first:last]
-    return fs, data, data.dtype
+    """(sample rate, samples[first:last], their dtype)."""
+    rate, samples = wav.read(filename)
+    samples = samples[first:last]
+    return rate, samples, samples.dtype
 
 
 def wavwrite(filename, rate, data, formattype='wav', formatenc='int16', formatend='file'):
-    if formatenc not in ('int16', 'int32', 'int8'):
-        if np.abs(data).max() > 2 ** 15:
-            formatenc = 'int32'
-        elif np.abs(data).max() > 2 ** 7:
-            formatenc = 'int16'
-        else:
-            formatenc = 'int8'
-    wav.write(filename, rate, np.array(data, dtype=formatenc))
+    """Write `data` cast to `formatenc`; an encoding other than the three
+    integer ones is replaced by the narrowest that holds the peak."""
+    enc = formatenc if formatenc in _INT_ENCODINGS else _smallest_int_encoding(data)
+    wav.write(filename, rate, np.array(data, dtype=enc))
     return 0
 
 
 class AudioObject(object):
+    """A WAV file read on first access to its data, rate or shape."""
+
     def __init__(self, filename, mode='rw'):
         self.filename = filename
         self.mode = mode
 
+    # -- file access -------------------------------------------------------
     def _read(self):
         if 'r' not in self.mode:
             raise ValueError("Not in read mode.")
-        self._samplerate, self._data, self._encoding = wavread(self.filename)
-        if len(self._data.shape) == 2:
-            self._nframes, self._channels = self._data.shape
-        else:
-            self._nframes = self._data.size
-            self._channels = 1
-        self._maxdata = np.maximum(1.1 * np.abs(self._data).max(), 1e-10)
-        self._data = self._data / self._maxdata
+        rate, samples, enc = wavread(self.filename)
+        self._samplerate, self._encoding = rate, enc
+        self._nframes = samples.shape[0] if samples.ndim == 2 else samples.size
+        self._channels = samples.shape[1] if samples.ndim == 2 else 1
+        self._maxdata = np.maximum(1.1 * np.abs(samples).max(), 1e-10)
+        self._data = samples / self._maxdata
 
     def _write(self):
         if 'w' not in self.mode:
             raise ValueError("Not in write mode.")
-        if not hasattr(self, '_samplerate') and not hasattr(self, '_data'):
+        if not (hasattr(self, '_samplerate') or hasattr(self, '_data')):
             raise AttributeError("Should set sample rate and have data in write mode.")
         wavwrite(filename=self.filename, rate=self._samplerate,
-                 data=self._maxdata * self._data, formatenc=self._encoding)
+                 data=self._data * self._maxdata, formatenc=self._encoding)
+
+    def _loaded(self, attr):
+        if not hasattr(self, attr):
+            self._read()
+        return getattr(self, attr)
+
+    # -- samples -------------------------------------------------------------
+    def _get_data(self):
+        return self._loaded('_data')
 
     def _set_data(self, data):
-        s = data.shape
-        if s[0] < s[1] and s[1] > 2:
-            self._data = np.array(data.T, order='C')
-        else:
-            self._data = np.array(data, order='C')
-        self._maxdata = 1.1 * np.abs(self._data).max()
-        self._encoding = self._data.dtype.name
-        self._data = self._data / self._maxdata
-
-    def _get_data(self):
-        if not hasattr(self, '_data'):
-            self._read()
-        return self._data
+        rows, cols = data.shape[0], data.shape[1]
+        # frames are rows: a wide array of more than two rows is transposed
+        arr = np.array(data.T if (rows < cols and cols > 2) else data, order='C')
+        self._encoding = arr.dtype.name
+        self._maxdata = 1.1 * np.abs(arr).max()
+        self._data = arr / self._maxdata
 
     def _del_data(self):
-        if hasattr(self, '_data'):
-            del self._data
+        self.__dict__.pop('_data', None)
 
     data = property(_get_data, _set_data, _del_data)
 
+    # -- sample rate ---------------------------------------------------------
     def _get_samplerate(self):
-        if not hasattr(self, '_samplerate') and 'r' in self.mode:
-            self._read()
+        if 'r' in self.mode:
+            return self._loaded('_samplerate')
         return self._samplerate
 
     def _set_samplerate(self, samplerate):
@@ -91,17 +105,9 @@ class AudioObject(object):
     samplerate = property(_get_samplerate, _set_samplerate)
     fs = samplerate
 
-    @property
-    def channels(self):
-        if not hasattr(self, '_channels'):
-            self._read()
-        return self._channels
-
-    @property
-    def nframes(self):
-        if not hasattr(self, '_nframes'):
-            self._read()
-        return self._nframes
+    # -- shape ---------------------------------------------------------------
+    channels = property(lambda self: self._loaded('_channels'))
+    nframes = property(lambda self: self._loaded('_nframes'))
 
 
 class SpectralAudio(AudioObject):
